@@ -1,0 +1,204 @@
+"""Benchmark of the NRC hot path on MI355X (BASELINE.json metric, configs[1] at N=1).
+
+A step = one ``infer`` over the frame's queries resident in HBM (2^21 synthetic Cornell queries per
+GPU, the 1080p 1spp batch of configs[1]); ``value`` = total queries over all ranks / max-over-ranks
+time (weak scaling: every rank processes its own 2^21). The same run also times the per-frame
+self-training (configs[2]: 4 x 16,384-sample steps; for N > 1 each rank trains on its own 16,384
+per minibatch with an RCCL all-reduce of the gradient) and reports it as ``train_step_ms``.
+
+Launch: ``python bench.py [--gpus N --steps K --warmup W]``; N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import nrc_loader  # noqa: E402
+
+FLOP_PER_QUERY = 2 * (66 * 64 + 4 * 64 * 64 + 64 * 3)  # 41,600 algorithmic
+BYTES_PER_QUERY = 60 + 12
+TRAIN_FLOP_PER_SAMPLE = 116_352
+PEAK_F16_TFLOPS = 2500.0  # MI355X dense f16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+QUERIES_PER_GPU = 1 << 21
+ROUND = "r01"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--queries", type=int, default=QUERIES_PER_GPU, help="queries per GPU per step")
+    ap.add_argument("--train-frames", type=int, default=20, help="timed frames of 4 x 16384 training")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float) -> dict:
+    """The naive C oracle (FP32, scalar loops) on the host cores, bounded sample of the workload."""
+    orc = nrc_loader.load_oracle()
+    threads = orc.default_threads()
+    n = 4096
+    t0 = time.perf_counter()
+    orc.forward(params, queries[:n], orc.FP32, threads)
+    dt = time.perf_counter() - t0
+    n = int(min(len(queries), max(n, n * target_s / max(dt, 1e-6))))
+    t0 = time.perf_counter()
+    orc.forward(params, queries[:n], orc.FP32, threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt / 1e6, "unit": "M queries/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of the {len(queries)} Cornell queries, oracle/nrc_oracle.c FP32 forward, "
+                      f"{threads} pthreads on {platform.processor() or platform.machine()} "
+                      f"({os.cpu_count()} logical CPUs visible), {dt:.1f} s"}
+
+
+def pmc_traffic() -> float | None:
+    f = ROOT / "profiles" / f"pmc_infer_{ROUND}.json"
+    if f.exists():
+        try:
+            return float(json.loads(f.read_text())["hbm_bytes_per_launch"])
+        except Exception:
+            return None
+    return None
+
+
+def main() -> None:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    nrc = nrc_loader.load()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+
+    seed = nrc.synthetic.SEED + rank
+    nq = args.queries
+    q_np = nrc.synthetic.cornell_queries(nq, seed=seed)
+    q = torch.from_numpy(q_np).to(dev)
+    out = torch.empty((nq, 3), dtype=torch.float32, device=dev)
+    frames_q, frames_t = [], []
+    for f in range(4):
+        tq, tt = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE * 4, seed=seed * 31 + f)
+        frames_q.append(torch.from_numpy(tq).to(dev))
+        frames_t.append(torch.from_numpy(tt).to(dev))
+    stream = torch.cuda.current_stream()
+
+    net = nrc.Network()
+    net.init(stream=stream, encoding=nrc.InputEncoding.Frequency)
+    grad = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
+    trainer = nrc.dp.DataParallelTrainer(net, grad) if distributed else None
+    if distributed:
+        trainer.broadcast_state(net.get_state, net.set_state, [nrc.StateSlot.PARAMS, nrc.StateSlot.INFER], dev)
+
+    def train_frame(fi: int) -> None:
+        tq, tt = frames_q[fi % 4], frames_t[fi % 4]
+        for b in range(4):
+            s = b * nrc.BATCH_SIZE
+            if distributed:
+                trainer.step(tq[s:], tt[s:], nrc.BATCH_SIZE, nrc.BATCH_SIZE * world)
+            else:
+                net.train(tq[s:], tt[s:])
+
+    def barrier():
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # a few frames of self-training first so inference runs on non-trivial (EMA) weights
+    for f in range(4):
+        train_frame(f)
+    for _ in range(args.warmup):
+        net.infer(q, out, nq)
+    barrier()
+
+    # ---- timed inference region: exactly K steps
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        net.infer(q, out, nq)
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step, same stream
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    ms_per_step = wall_max / args.steps * 1e3
+    value = world * nq * args.steps / wall_max / 1e6
+
+    # ---- training: frames of 4 x 16384
+    for f in range(2):
+        train_frame(f)
+    barrier()
+    t0 = time.perf_counter()
+    for f in range(args.train_frames):
+        train_frame(f)
+    barrier()
+    tw = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+    train_frame_ms = float(tw.item()) / args.train_frames * 1e3
+    train_step_ms = train_frame_ms / 4
+
+    achieved = FLOP_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e12
+    result = {
+        "metric": "M radiance queries/sec + train-step ms, 64x5 MLP @ 2M samples/frame",
+        "value": value,
+        "unit": "M queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic (seeded Cornell-box RadianceQuery stream, SURVEY §8(d)); random-init weights "
+                "after 4 frames of self-training",
+        "config": {"workload": "configs[1]: Cornell 1080p 1spp, 2^21-query fused encode+64x5 MLP inference per GPU "
+                               "(fp16 MFMA, f32 accumulate); train: configs[2] 4 x 16384 per frame per GPU",
+                   "queries_per_gpu": nq, "train_batch_per_gpu": nrc.BATCH_SIZE,
+                   "parallelism": f"dp{world}" if world > 1 else "single"},
+        "train_step_ms": train_step_ms,
+        "train_frame_ms": train_frame_ms,
+        "infer_kernel_ms": kernel_ms,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_F16_TFLOPS, "traffic": pmc_traffic(),
+                     "algorithmic_bytes_per_launch": BYTES_PER_QUERY * nq,
+                     "hbm_gbs_algorithmic": BYTES_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e9},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        params = net.get_state(nrc.StateSlot.INFER)
+        result["cpu_baseline"] = cpu_baseline(q_np, params, args.cpu_seconds)
+    net.destroy()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

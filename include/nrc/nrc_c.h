@@ -1,0 +1,132 @@
+/*
+ * nrc/nrc_c.h — C-ABI of the MI355X-native neural radiance cache (drop-in for the reference's
+ * nrc::Network query/train module, /root/reference/nrc/inc/NRCNetwork.h:20-75).
+ *
+ * Plain C: opaque handle, plain device pointers and sizes, int status codes; no C++ or torch types
+ * cross this boundary. Exceptions never cross it: every entry point returns an nrc_status and the
+ * message of the last failure on the calling thread is available from nrc_last_error().
+ *
+ * Buffers are the reference's, byte for byte (include/nrc/layout.h): queries are packed 60-byte
+ * RadianceQuery records (15 f32, 4-byte aligned), outputs and targets packed 12-byte float3.
+ * All work is enqueued on a HIP stream and is asynchronous unless a host loss pointer is given
+ * (that call blocks, as NRCNetwork.cu:130-131 does). A handle is not thread-safe.
+ */
+#ifndef NRC_C_H
+#define NRC_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "layout.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum nrc_status {
+    NRC_OK = 0,
+    NRC_ERR_INVALID_ARGUMENT = 1, /* std::invalid_argument in the reference (NRCNetworkConfigs.h:333-335) */
+    NRC_ERR_DESTROYED = 2,        /* call after destroy(): a silent no-op in the reference (NRCNetwork.cu:119, :142) */
+    NRC_ERR_NOT_INITIALIZED = 3,
+    NRC_ERR_HIP = 4,              /* HIP runtime failure (CU_CHECK -> std::runtime_error in the reference) */
+    NRC_ERR_UNSUPPORTED = 5,
+    NRC_ERR_OUT_OF_MEMORY = 6,
+    NRC_ERR_INTERNAL = 7
+} nrc_status;
+
+typedef struct nrc_net nrc_net;
+
+/* Optional hyper-parameter overrides; nrc_default_config() returns the reference's values for an
+ * encoding (NRCNetworkConfigs.h:11-83, neural_radiance_caching.h:47-54). */
+typedef struct nrc_config {
+    float learning_rate; /* Adam learning rate, TRAIN_LR(encoding) */
+    float beta1, beta2, epsilon, l2_reg;
+    float ema_decay;     /* EMA optimizer wrapper decay (0.99) */
+    float loss_scale;    /* f16 loss scale (128) */
+    uint64_t seed;       /* weight initialisation seed */
+} nrc_config;
+
+/* HyperParams (NRCNetwork.h:10-13) */
+typedef struct nrc_hyper_params {
+    float learning_rate;
+} nrc_hyper_params;
+
+/* Optimizer / model state slots for nrc_get_state / nrc_set_state (checkpoint, parity fixtures). */
+typedef enum nrc_state_slot {
+    NRC_STATE_PARAMS = 0, /* f32 master weights used by training (canonical blob, layout.h) */
+    NRC_STATE_INFER = 1,  /* weights used by infer(): debiased EMA after the first step */
+    NRC_STATE_EMA = 2,    /* raw (biased) EMA accumulator */
+    NRC_STATE_ADAM_M = 3,
+    NRC_STATE_ADAM_V = 4
+} nrc_state_slot;
+
+const char* nrc_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* nrc_last_error(void);
+nrc_config nrc_default_config(int encoding);
+
+/* Network() / ~Network() (NRCNetwork.h:22-24): allocate / free an empty handle. nrc_free on a handle
+ * that was never destroyed prints the reference's warning (NRCNetwork.cu:105-109) and releases it. */
+nrc_status nrc_create(nrc_net** out);
+nrc_status nrc_free(nrc_net* net);
+
+/* init<Verbose>(stream, encoding) (NRCNetwork.h:26-31, NRCNetwork.cu:182-188): set the stream,
+ * select the encoding's config and (re)build the model with freshly initialised weights and
+ * optimizer state. cfg may be NULL (reference defaults). verbose prints the config JSON
+ * (printConfig_, NRCNetwork.cu:198-203). Re-init after destroy revives the handle. */
+nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_config* cfg, int verbose);
+
+/* destroy() (NRCNetwork.h:41): release all device state; later calls return NRC_ERR_DESTROYED.
+ * Idempotent. */
+nrc_status nrc_destroy(nrc_net* net);
+
+/* train(in, tgt, loss_h) / train(in, tgt, stream, loss_h) (NRCNetwork.h:44-46): one optimizer step on
+ * exactly NRC_BATCH_SIZE (16384) samples. loss_h may be NULL; if not, the call blocks and writes the
+ * minibatch loss (Trainer::loss()). */
+nrc_status nrc_train(nrc_net* net, const float* inputs_d, const float* targets_d, float* loss_h);
+nrc_status nrc_train_stream(nrc_net* net, const float* inputs_d, const float* targets_d, hipStream_t stream,
+                            float* loss_h);
+/* Extension: a step on any batch size b >= 1 (the reference fixes b = 16384). */
+nrc_status nrc_train_batch(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b, float* loss_h);
+
+/* infer(in, out, n) / infer(in, out, n, stream) (NRCNetwork.h:49-51). Processes exactly n queries
+ * (the reference rounds n up to 256 and reads/writes past n, NRCNetwork.cu:147-148; this one never
+ * touches the tail). n = 0 is a no-op. Uses the inference (EMA) weights. */
+nrc_status nrc_infer(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n);
+nrc_status nrc_infer_stream(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n, hipStream_t stream);
+
+nrc_status nrc_set_stream(nrc_net* net, hipStream_t stream);           /* setStream (NRCNetwork.h:53) */
+nrc_status nrc_get_stream(const nrc_net* net, hipStream_t* stream);
+nrc_status nrc_set_hyper_params(nrc_net* net, const nrc_hyper_params* hp); /* setHyperParams (:55) */
+nrc_status nrc_set_config(nrc_net* net, int encoding);                 /* setConfig (:57): takes effect at next init */
+nrc_status nrc_get_learning_rate(const nrc_net* net, float* lr);       /* getLearningRate (:61) */
+/* printConfig_ equivalent: the model config as JSON (tcnn's schema). Writes at most cap bytes incl. NUL;
+ * *needed (optional) receives the full length + 1. */
+nrc_status nrc_get_config_json(const nrc_net* net, char* buf, size_t cap, size_t* needed);
+
+/* ---- data-parallel split of train() (new capability: the reference has no collectives) ----
+ * nrc_train_grad writes the loss-scaled gradient of this rank's b samples, normalised by the GLOBAL
+ * batch (3 * global_b), into grad_d[NRC_GRAD_FLOATS] (f32, device), with the local loss at
+ * grad_d[NRC_NUM_PARAMS]. Sum grad_d over ranks (e.g. an RCCL all-reduce), then nrc_train_apply
+ * performs the identical Adam + EMA step on every rank. loss_h: as in nrc_train. */
+#define NRC_GRAD_FLOATS (NRC_NUM_PARAMS + 4)
+nrc_status nrc_train_grad(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
+                          uint32_t global_b, float* grad_d);
+nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h);
+
+/* ---- state access (host buffers of NRC_NUM_PARAMS f32; synchronous) ---- */
+nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst);
+nrc_status nrc_set_state(nrc_net* net, int slot, const float* host_src);
+nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
+nrc_status nrc_set_step(nrc_net* net, uint32_t step);
+
+/* ---- test entry: the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
+nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NRC_C_H */

@@ -1,0 +1,10 @@
+"""MI355X-native neural radiance cache: drop-in for the reference's nrc::Network query/train module.
+
+Product = libnrc_amd.so (hand-written gfx950 HIP kernels behind the C-ABI in include/nrc/nrc_c.h).
+This package is the host-side mirror of the reference interface plus the synthetic Cornell sample
+stream and the data-parallel sharding. The directory name contains hyphens, so it is loaded as the
+module ``nrc_amd`` by ``load()`` in __graft_entry__.py / tests/conftest.py / bench.py.
+"""
+from . import _lib, dp, synthetic  # noqa: F401
+from ._lib import BATCH_SIZE, GRAD_FLOATS, NUM_PARAMS, NrcError  # noqa: F401
+from .network import HyperParams, InputEncoding, Network, StateSlot, current_stream, default_config, encode  # noqa: F401

@@ -1,0 +1,122 @@
+"""ctypes binding of libnrc_amd.so (C-ABI: include/nrc/nrc_c.h).
+
+The product path: there is no CPU fallback. If the HIP library is missing, importing the binding
+raises, and every GPU entry point fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libnrc_amd.so"
+
+NUM_PARAMS = 22528
+GRAD_FLOATS = NUM_PARAMS + 4
+BATCH_SIZE = 16384
+INPUT_DIMS = 15
+OUTPUT_DIMS = 3
+
+NRC_OK = 0
+STATUS_NAMES = {
+    0: "NRC_OK", 1: "NRC_ERR_INVALID_ARGUMENT", 2: "NRC_ERR_DESTROYED", 3: "NRC_ERR_NOT_INITIALIZED",
+    4: "NRC_ERR_HIP", 5: "NRC_ERR_UNSUPPORTED", 6: "NRC_ERR_OUT_OF_MEMORY", 7: "NRC_ERR_INTERNAL",
+}
+
+# Every symbol include/nrc/nrc_c.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "nrc_version", "nrc_last_error", "nrc_default_config", "nrc_create", "nrc_free", "nrc_init", "nrc_destroy",
+    "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
+    "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
+    "nrc_train_grad", "nrc_train_apply", "nrc_get_state", "nrc_set_state", "nrc_get_step", "nrc_set_step",
+    "nrc_encode",
+]
+
+
+class NrcConfig(ctypes.Structure):
+    _fields_ = [("learning_rate", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("epsilon", ctypes.c_float), ("l2_reg", ctypes.c_float), ("ema_decay", ctypes.c_float),
+                ("loss_scale", ctypes.c_float), ("seed", ctypes.c_uint64)]
+
+
+class NrcHyperParams(ctypes.Structure):
+    _fields_ = [("learning_rate", ctypes.c_float)]
+
+
+class NrcError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def build() -> Path:
+    subprocess.run(["make", "-s", "-C", str(PKG_DIR)], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"HIP extension {LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback)")
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, fp, u32 = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32
+    st = ctypes.c_int
+    sigs = {
+        "nrc_version": (ctypes.c_char_p, []),
+        "nrc_last_error": (ctypes.c_char_p, []),
+        "nrc_default_config": (NrcConfig, [ctypes.c_int]),
+        "nrc_create": (st, [ctypes.POINTER(vp)]),
+        "nrc_free": (st, [vp]),
+        "nrc_init": (st, [vp, vp, ctypes.c_int, ctypes.POINTER(NrcConfig), ctypes.c_int]),
+        "nrc_destroy": (st, [vp]),
+        "nrc_train": (st, [vp, fp, fp, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_train_stream": (st, [vp, fp, fp, vp, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_train_batch": (st, [vp, fp, fp, u32, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_infer": (st, [vp, fp, fp, u32]),
+        "nrc_infer_stream": (st, [vp, fp, fp, u32, vp]),
+        "nrc_set_stream": (st, [vp, vp]),
+        "nrc_get_stream": (st, [vp, ctypes.POINTER(vp)]),
+        "nrc_set_hyper_params": (st, [vp, ctypes.POINTER(NrcHyperParams)]),
+        "nrc_set_config": (st, [vp, ctypes.c_int]),
+        "nrc_get_learning_rate": (st, [vp, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_get_config_json": (st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+        "nrc_train_grad": (st, [vp, fp, fp, u32, u32, fp]),
+        "nrc_train_apply": (st, [vp, fp, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_get_state": (st, [vp, ctypes.c_int, fp]),
+        "nrc_set_state": (st, [vp, ctypes.c_int, fp]),
+        "nrc_get_step": (st, [vp, ctypes.POINTER(u32)]),
+        "nrc_set_step": (st, [vp, u32]),
+        "nrc_encode": (st, [fp, fp, u32, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int) -> None:
+    if status != NRC_OK:
+        raise NrcError(status, lib().nrc_last_error().decode(errors="replace"))
+
+
+def last_error() -> str:
+    return lib().nrc_last_error().decode(errors="replace")
+
+
+def exported_symbols() -> list[str]:
+    """Dynamic symbols exported by the library (via the ELF .dynsym, no GPU needed)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB_PATH)], check=True, capture_output=True, text=True)
+    return sorted({line.split()[-1] for line in out.stdout.splitlines() if line.strip()})
+
+
+def default_env_ok() -> bool:
+    return os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0") == "0"

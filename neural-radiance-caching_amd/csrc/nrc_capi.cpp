@@ -1,0 +1,549 @@
+// nrc_capi.cpp — C-ABI implementation (include/nrc/nrc_c.h). Owns parameters, optimizer state,
+// MFMA weight images and workspaces (the reference's tcnn::TrainableModel, NRCNetwork.cu:15-20).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "nrc/nrc_c.h"
+#include "nrc_internal.h"
+
+using namespace nrc_amd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct ApiError : std::runtime_error {
+    nrc_status code;
+    ApiError(nrc_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                              \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            throw HipError(std::string(#expr) + ": " + hipGetErrorString(e_) + " (" + __FILE__ + ":" + \
+                           std::to_string(__LINE__) + ")");                                          \
+    } while (0)
+
+template <class F>
+nrc_status guarded(F&& f) {
+    try {
+        f();
+        g_last_error.clear();
+        return NRC_OK;
+    } catch (const ApiError& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const HipError& e) {
+        g_last_error = e.what();
+        return NRC_ERR_HIP;
+    } catch (const std::bad_alloc& e) {
+        g_last_error = "out of host memory";
+        return NRC_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return NRC_ERR_INTERNAL;
+    } catch (...) {
+        g_last_error = "unknown error";
+        return NRC_ERR_INTERNAL;
+    }
+}
+
+// pcg32 (tcnn common/random.h) for xavier-uniform init [M: tcnn's init cannot be reproduced bit for bit].
+struct Pcg32 {
+    uint64_t state = 0, inc = 1;
+    Pcg32(uint64_t initstate, uint64_t initseq) {
+        inc = (initseq << 1u) | 1u;
+        next();
+        state += initstate;
+        next();
+    }
+    uint32_t next() {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    float next_float() {
+        uint32_t u = (next() >> 9) | 0x3f800000u;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f - 1.0f;
+    }
+};
+
+constexpr int kLayerIn[NRC_NUM_LAYERS] = {NRC_ENC_WIDTH, 64, 64, 64, 64, 64};
+constexpr int kLayerOut[NRC_NUM_LAYERS] = {64, 64, 64, 64, 64, NRC_OUT_PADDED};
+constexpr int kLayerOff[NRC_NUM_LAYERS] = {NRC_W0_OFFSET, NRC_W1_OFFSET, NRC_W2_OFFSET,
+                                           NRC_W3_OFFSET, NRC_W4_OFFSET, NRC_W5_OFFSET};
+
+void init_params(std::vector<float>& p, uint64_t seed) {
+    Pcg32 rng(seed, 0xda3e39cb94b95bdbULL);
+    for (int l = 0; l < NRC_NUM_LAYERS; ++l) {
+        const float scale = std::sqrt(6.0f / (float)(kLayerIn[l] + kLayerOut[l]));
+        const int cnt = kLayerIn[l] * kLayerOut[l];
+        for (int i = 0; i < cnt; ++i) p[kLayerOff[l] + i] = (rng.next_float() * 2.0f - 1.0f) * scale;
+    }
+}
+
+// Position of every canonical parameter inside the forward / backward MFMA fragment images.
+void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd) {
+    fwd.assign(NRC_NUM_PARAMS, -1);
+    bwd.assign(NRC_NUM_PARAMS, -1);
+    // inverse of acc_row over (kk, h, j) for a 64-feature axis
+    int row_kk[64], row_h[64], row_j[64];
+    for (int kk = 0; kk < 4; ++kk)
+        for (int h = 0; h < 2; ++h)
+            for (int j = 0; j < 8; ++j) {
+                const int r = acc_row(kk, h, j);
+                row_kk[r] = kk;
+                row_h[r] = h;
+                row_j[r] = j;
+            }
+    int f_kk[NRC_ENC_WIDTH], f_h[NRC_ENC_WIDTH], f_j[NRC_ENC_WIDTH];
+    for (int h = 0; h < 2; ++h)
+        for (int n = 0; n < 40; ++n) {
+            const int f = slot_feature(n, h);
+            f_kk[f] = n / 8;
+            f_h[f] = h;
+            f_j[f] = n % 8;
+        }
+    auto pos = [](int frag, int lane, int j) { return frag * kFragHalves + lane * 8 + j; };
+    for (int o = 0; o < 64; ++o)
+        for (int f = 0; f < NRC_ENC_WIDTH; ++f)
+            fwd[NRC_W0_OFFSET + o * NRC_ENC_WIDTH + f] = pos(fwd_frag(0, o / 32, f_kk[f]), o % 32 + 32 * f_h[f], f_j[f]);
+    for (int l = 1; l <= 4; ++l)
+        for (int o = 0; o < 64; ++o)
+            for (int i = 0; i < 64; ++i) {
+                const int p = kLayerOff[l] + o * 64 + i;
+                fwd[p] = pos(fwd_frag(l, o / 32, row_kk[i]), o % 32 + 32 * row_h[i], row_j[i]);
+                bwd[p] = pos(bwd_frag(l, i / 32, row_kk[o]), i % 32 + 32 * row_h[o], row_j[o]);
+            }
+    for (int o = 0; o < NRC_OUT_PADDED; ++o)
+        for (int i = 0; i < 64; ++i) {
+            const int p = NRC_W5_OFFSET + o * 64 + i;
+            fwd[p] = pos(fwd_frag(5, 0, row_kk[i]), o + 32 * row_h[i], row_j[i]);
+            // W5^T: rows acc_row(0, h, j) in [0,16) index the output neuron o
+            bwd[p] = pos(bwd_frag(5, i / 32, 0), i % 32 + 32 * row_h[o], row_j[o]);
+        }
+}
+
+std::string config_json(int encoding, const nrc_config& c) {
+    char buf[2048];
+    if (encoding == NRC_ENCODING_FREQUENCY) {
+        std::snprintf(buf, sizeof(buf),
+                      "{\"encoding\":{\"nested\":[{\"n_dims_to_encode\":3,\"n_frequencies\":12,\"otype\":"
+                      "\"TriangleWave\"},{\"n_bins\":4,\"n_dims_to_encode\":6,\"otype\":\"OneBlob\"},{\"n_dims_to_"
+                      "encode\":6,\"otype\":\"Identity\"}],\"otype\":\"Composite\"},\"loss\":{\"otype\":"
+                      "\"RelativeL2Luminance\"},\"network\":{\"activation\":\"ReLU\",\"n_hidden_layers\":5,\"n_"
+                      "neurons\":64,\"otype\":\"FullyFusedMLP\",\"output_activation\":\"ReLU\"},\"optimizer\":{"
+                      "\"decay\":%g,\"nested\":{\"beta1\":%g,\"beta2\":%g,\"epsilon\":%g,\"l2_reg\":%g,\"learning_"
+                      "rate\":%g,\"otype\":\"Adam\"},\"otype\":\"EMA\"}}",
+                      c.ema_decay, c.beta1, c.beta2, c.epsilon, c.l2_reg, c.learning_rate);
+    } else {
+        std::snprintf(buf, sizeof(buf),
+                      "{\"encoding\":{\"nested\":[{\"base_resolution\":16,\"log2_hashmap_size\":15,\"n_dims_to_"
+                      "encode\":3,\"n_features_per_level\":2,\"n_levels\":16,\"otype\":\"HashGrid\",\"per_level_"
+                      "scale\":2.0},{\"n_bins\":4,\"n_dims_to_encode\":6,\"otype\":\"OneBlob\"},{\"n_dims_to_"
+                      "encode\":6,\"otype\":\"Identity\"}],\"otype\":\"Composite\"},\"loss\":{\"otype\":"
+                      "\"RelativeL2Luminance\"},\"network\":{\"activation\":\"ReLU\",\"n_hidden_layers\":5,\"n_"
+                      "neurons\":64,\"otype\":\"FullyFusedMLP\",\"output_activation\":\"ReLU\"},\"optimizer\":{"
+                      "\"decay\":%g,\"nested\":{\"epsilon\":%g,\"l2_reg\":%g,\"learning_rate\":%g,\"otype\":"
+                      "\"Adam\"},\"otype\":\"EMA\"}}",
+                      c.ema_decay, c.epsilon, c.l2_reg, c.learning_rate);
+    }
+    return buf;
+}
+
+}  // namespace
+
+struct nrc_net {
+    hipStream_t stream = nullptr;
+    int encoding = NRC_ENCODING_FREQUENCY;
+    nrc_config cfg{};
+    bool initialized = false;
+    bool destroyed = false;
+    int device = 0;
+    uint32_t step = 0;
+
+    float *params = nullptr, *m = nullptr, *v = nullptr, *ema = nullptr, *infer = nullptr;
+    _Float16 *wf_train = nullptr, *wb_train = nullptr, *wf_infer = nullptr;
+    int *fwd_pos = nullptr, *bwd_pos = nullptr;
+    float* slabs = nullptr;
+    int slab_blocks = 0;
+    float* loss_partials = nullptr;
+    float* grad = nullptr;  // kGradFloats scratch for the fused path
+    float* loss_dev = nullptr;
+    float* loss_host = nullptr;  // pinned
+
+    void release() {
+        auto f = [](void* p) {
+            if (p) (void)hipFree(p);
+        };
+        f(params); f(m); f(v); f(ema); f(infer);
+        f(wf_train); f(wb_train); f(wf_infer);
+        f(fwd_pos); f(bwd_pos);
+        f(slabs); f(loss_partials); f(grad); f(loss_dev);
+        if (loss_host) (void)hipHostFree(loss_host);
+        params = m = v = ema = infer = nullptr;
+        wf_train = wb_train = wf_infer = nullptr;
+        fwd_pos = bwd_pos = nullptr;
+        slabs = loss_partials = grad = loss_dev = loss_host = nullptr;
+        slab_blocks = 0;
+        initialized = false;
+    }
+
+    ModelBuffers buffers() const {
+        ModelBuffers b;
+        b.params = params; b.m = m; b.v = v; b.ema = ema; b.infer = infer;
+        b.wf_train = wf_train; b.wb_train = wb_train; b.wf_infer = wf_infer;
+        b.fwd_pos = fwd_pos; b.bwd_pos = bwd_pos;
+        return b;
+    }
+    OptimArgs optim(uint32_t s) const {
+        OptimArgs o;
+        o.lr = cfg.learning_rate; o.beta1 = cfg.beta1; o.beta2 = cfg.beta2; o.eps = cfg.epsilon;
+        o.l2_reg = cfg.l2_reg; o.ema_decay = cfg.ema_decay; o.loss_scale = cfg.loss_scale; o.step = s;
+        return o;
+    }
+    void ensure_slabs(int blocks) {
+        if (blocks <= slab_blocks) return;
+        if (slabs) HIP_CHECK(hipFree(slabs));
+        if (loss_partials) HIP_CHECK(hipFree(loss_partials));
+        slabs = nullptr;
+        loss_partials = nullptr;
+        slab_blocks = 0;
+        HIP_CHECK(hipMalloc(&slabs, sizeof(float) * (size_t)blocks * NRC_NUM_PARAMS));
+        HIP_CHECK(hipMalloc(&loss_partials, sizeof(float) * (size_t)blocks));
+        slab_blocks = blocks;
+    }
+};
+
+namespace {
+
+void check_live(const nrc_net* net) {
+    if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
+    if (net->destroyed) throw ApiError(NRC_ERR_DESTROYED, "network was destroyed");
+    if (!net->initialized) throw ApiError(NRC_ERR_NOT_INITIALIZED, "network is not initialised (call nrc_init)");
+}
+
+void upload_all(nrc_net* net, const std::vector<float>& params, const std::vector<float>& infer) {
+    HIP_CHECK(hipMemcpy(net->params, params.data(), sizeof(float) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(net->infer, infer.data(), sizeof(float) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+}
+
+void repack(nrc_net* net, hipStream_t s) {
+    HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
+}
+
+void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h) {
+    check_live(net);
+    if (b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "batch size must be >= 1");
+    if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
+    const int blocks = train_blocks(b);
+    net->ensure_slabs(blocks);
+    HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                   net->slabs, net->loss_partials, net->stream));
+    net->step += 1;
+    HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr, net->loss_dev,
+                                 net->buffers(), net->optim(net->step), net->stream));
+    if (loss_h) {
+        HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
+        HIP_CHECK(hipStreamSynchronize(net->stream));
+        *loss_h = *net->loss_host;
+    }
+}
+
+float* slot_ptr(nrc_net* net, int slot) {
+    switch (slot) {
+        case NRC_STATE_PARAMS: return net->params;
+        case NRC_STATE_INFER: return net->infer;
+        case NRC_STATE_EMA: return net->ema;
+        case NRC_STATE_ADAM_M: return net->m;
+        case NRC_STATE_ADAM_V: return net->v;
+        default: throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown state slot " + std::to_string(slot));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nrc_version(void) { return "nrc-mi355x 0.1 (gfx950)"; }
+const char* nrc_last_error(void) { return g_last_error.c_str(); }
+
+nrc_config nrc_default_config(int encoding) {
+    nrc_config c;
+    c.learning_rate = encoding == NRC_ENCODING_HASH ? NRC_TRAIN_LR_HASH : NRC_TRAIN_LR_FREQUENCY;
+    c.beta1 = NRC_ADAM_BETA1;
+    c.beta2 = NRC_ADAM_BETA2;
+    c.epsilon = encoding == NRC_ENCODING_HASH ? NRC_ADAM_EPS_HASH : NRC_ADAM_EPS_FREQ;
+    c.l2_reg = NRC_ADAM_L2_REG;
+    c.ema_decay = NRC_EMA_DECAY;
+    c.loss_scale = NRC_LOSS_SCALE;
+    c.seed = 1337;
+    return c;
+}
+
+nrc_status nrc_create(nrc_net** out) {
+    return guarded([&] {
+        if (!out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output pointer");
+        *out = new nrc_net();
+        (*out)->cfg = nrc_default_config(NRC_ENCODING_FREQUENCY);
+    });
+}
+
+nrc_status nrc_free(nrc_net* net) {
+    return guarded([&] {
+        if (!net) return;
+        if (!net->destroyed && net->initialized)
+            std::fprintf(stderr, "WARNING: NRC Network must be explicitly destroy() in the context it was created in!\n");
+        net->release();
+        delete net;
+    });
+}
+
+nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_config* cfg, int verbose) {
+    return guarded([&] {
+        if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
+        if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
+        if (encoding == NRC_ENCODING_HASH)
+            throw ApiError(NRC_ERR_UNSUPPORTED, "InputEncoding::Hash is not implemented yet (SURVEY §8(f) row 3)");
+        net->release();
+        net->stream = stream;
+        net->encoding = encoding;
+        net->cfg = cfg ? *cfg : nrc_default_config(encoding);
+        net->destroyed = false;
+        net->step = 0;
+        HIP_CHECK(hipGetDevice(&net->device));
+        const size_t pb = sizeof(float) * NRC_NUM_PARAMS;
+        HIP_CHECK(hipMalloc(&net->params, pb));
+        HIP_CHECK(hipMalloc(&net->m, pb));
+        HIP_CHECK(hipMalloc(&net->v, pb));
+        HIP_CHECK(hipMalloc(&net->ema, pb));
+        HIP_CHECK(hipMalloc(&net->infer, pb));
+        HIP_CHECK(hipMalloc(&net->wf_train, sizeof(_Float16) * kFwdHalves));
+        HIP_CHECK(hipMalloc(&net->wb_train, sizeof(_Float16) * kBwdHalves));
+        HIP_CHECK(hipMalloc(&net->wf_infer, sizeof(_Float16) * kFwdHalves));
+        HIP_CHECK(hipMalloc(&net->fwd_pos, sizeof(int) * NRC_NUM_PARAMS));
+        HIP_CHECK(hipMalloc(&net->bwd_pos, sizeof(int) * NRC_NUM_PARAMS));
+        HIP_CHECK(hipMalloc(&net->grad, sizeof(float) * kGradFloats));
+        HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
+        HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
+        HIP_CHECK(hipMemset(net->m, 0, pb));
+        HIP_CHECK(hipMemset(net->v, 0, pb));
+        HIP_CHECK(hipMemset(net->ema, 0, pb));
+        HIP_CHECK(hipMemset(net->wf_train, 0, sizeof(_Float16) * kFwdHalves));
+        HIP_CHECK(hipMemset(net->wb_train, 0, sizeof(_Float16) * kBwdHalves));
+        HIP_CHECK(hipMemset(net->wf_infer, 0, sizeof(_Float16) * kFwdHalves));
+        HIP_CHECK(hipMemset(net->loss_dev, 0, sizeof(float) * 4));
+        std::vector<int> fwd, bwd;
+        build_scatter_maps(fwd, bwd);
+        HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+        std::vector<float> p(NRC_NUM_PARAMS);
+        init_params(p, net->cfg.seed);
+        upload_all(net, p, p);  // before the first step inference uses the initial weights
+        net->initialized = true;
+        repack(net, nullptr);
+        HIP_CHECK(hipDeviceSynchronize());
+        net->ensure_slabs(train_blocks(NRC_BATCH_SIZE));
+        if (verbose) {
+            std::printf("\n----------------------- NETWORK CONFIG -----------------------\n%s\n"
+                        "--------------------------------------------------------------\n\n",
+                        config_json(net->encoding, net->cfg).c_str());
+        }
+    });
+}
+
+nrc_status nrc_destroy(nrc_net* net) {
+    return guarded([&] {
+        if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
+        if (net->destroyed) return;
+        net->release();
+        net->destroyed = true;
+    });
+}
+
+nrc_status nrc_train(nrc_net* net, const float* in, const float* tgt, float* loss_h) {
+    return guarded([&] { do_train(net, in, tgt, NRC_BATCH_SIZE, loss_h); });
+}
+
+nrc_status nrc_train_stream(nrc_net* net, const float* in, const float* tgt, hipStream_t stream, float* loss_h) {
+    return guarded([&] {
+        check_live(net);
+        net->stream = stream;
+        do_train(net, in, tgt, NRC_BATCH_SIZE, loss_h);
+    });
+}
+
+nrc_status nrc_train_batch(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h) {
+    return guarded([&] { do_train(net, in, tgt, b, loss_h); });
+}
+
+nrc_status nrc_infer(nrc_net* net, const float* in, float* out, uint32_t n) {
+    return guarded([&] {
+        check_live(net);
+        if (n == 0) return;
+        if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+        HIP_CHECK(launch_infer(in, out, n, net->wf_infer, net->stream));
+    });
+}
+
+nrc_status nrc_infer_stream(nrc_net* net, const float* in, float* out, uint32_t n, hipStream_t stream) {
+    return guarded([&] {
+        check_live(net);
+        net->stream = stream;
+        if (n == 0) return;
+        if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+        HIP_CHECK(launch_infer(in, out, n, net->wf_infer, net->stream));
+    });
+}
+
+nrc_status nrc_set_stream(nrc_net* net, hipStream_t stream) {
+    return guarded([&] {
+        if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
+        net->stream = stream;
+    });
+}
+
+nrc_status nrc_get_stream(const nrc_net* net, hipStream_t* stream) {
+    return guarded([&] {
+        if (!net || !stream) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null argument");
+        *stream = net->stream;
+    });
+}
+
+nrc_status nrc_set_hyper_params(nrc_net* net, const nrc_hyper_params* hp) {
+    return guarded([&] {
+        check_live(net);
+        if (!hp) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null hyper params");
+        if (!(hp->learning_rate >= 0.0f) || !std::isfinite(hp->learning_rate))
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "learning rate must be finite and >= 0");
+        net->cfg.learning_rate = hp->learning_rate;
+    });
+}
+
+nrc_status nrc_set_config(nrc_net* net, int encoding) {
+    return guarded([&] {
+        if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
+        if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
+        net->encoding = encoding;
+        net->cfg = nrc_default_config(encoding);
+    });
+}
+
+nrc_status nrc_get_learning_rate(const nrc_net* net, float* lr) {
+    return guarded([&] {
+        check_live(net);
+        if (!lr) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output");
+        *lr = net->cfg.learning_rate;
+    });
+}
+
+nrc_status nrc_get_config_json(const nrc_net* net, char* buf, size_t cap, size_t* needed) {
+    return guarded([&] {
+        if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
+        const std::string s = config_json(net->encoding, net->cfg);
+        if (needed) *needed = s.size() + 1;
+        if (buf && cap) {
+            const size_t k = s.size() < cap - 1 ? s.size() : cap - 1;
+            std::memcpy(buf, s.data(), k);
+            buf[k] = '\0';
+        }
+    });
+}
+
+nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b,
+                          float* grad_d) {
+    return guarded([&] {
+        check_live(net);
+        if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
+        if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
+        if (b == 0) {
+            HIP_CHECK(hipMemsetAsync(grad_d, 0, sizeof(float) * kGradFloats, net->stream));
+            return;
+        }
+        if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
+        const int blocks = train_blocks(b);
+        net->ensure_slabs(blocks);
+        HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
+                                       net->wb_train, net->slabs, net->loss_partials, net->stream));
+        HIP_CHECK(launch_reduce_adam(kReduceOnly, net->slabs, blocks, net->loss_partials, grad_d, nullptr,
+                                     net->buffers(), net->optim(net->step + 1), net->stream));
+    });
+}
+
+nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
+    return guarded([&] {
+        check_live(net);
+        if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
+        net->step += 1;
+        HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
+                                     net->buffers(), net->optim(net->step), net->stream));
+        if (loss_h) {
+            HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
+            HIP_CHECK(hipStreamSynchronize(net->stream));
+            *loss_h = *net->loss_host;
+        }
+    });
+}
+
+nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst) {
+    return guarded([&] {
+        check_live(net);
+        if (!host_dst) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null destination");
+        float* src = slot_ptr(net, slot);
+        HIP_CHECK(hipStreamSynchronize(net->stream));
+        HIP_CHECK(hipMemcpy(host_dst, src, sizeof(float) * NRC_NUM_PARAMS, hipMemcpyDeviceToHost));
+    });
+}
+
+nrc_status nrc_set_state(nrc_net* net, int slot, const float* host_src) {
+    return guarded([&] {
+        check_live(net);
+        if (!host_src) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null source");
+        float* dst = slot_ptr(net, slot);
+        HIP_CHECK(hipStreamSynchronize(net->stream));
+        HIP_CHECK(hipMemcpy(dst, host_src, sizeof(float) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+        if (slot == NRC_STATE_PARAMS || slot == NRC_STATE_INFER) {
+            repack(net, net->stream);
+            HIP_CHECK(hipStreamSynchronize(net->stream));
+        }
+    });
+}
+
+nrc_status nrc_get_step(const nrc_net* net, uint32_t* step) {
+    return guarded([&] {
+        check_live(net);
+        if (!step) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output");
+        *step = net->step;
+    });
+}
+
+nrc_status nrc_set_step(nrc_net* net, uint32_t step) {
+    return guarded([&] {
+        check_live(net);
+        net->step = step;
+    });
+}
+
+nrc_status nrc_encode(const float* in, float* enc, uint32_t n, hipStream_t stream) {
+    return guarded([&] {
+        if (n == 0) return;
+        if (!in || !enc) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
+        HIP_CHECK(launch_encode(in, enc, n, stream));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// nrc_internal.h — host-side declarations shared by the C-ABI (nrc_capi.cpp) and the gfx950 kernels
+// (nrc_kernels.hip). Not part of the public interface (that is include/nrc/nrc_c.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nrc/layout.h"
+
+namespace nrc_amd {
+
+// ---- MFMA fragment images (f16). One fragment = one v_mfma_f32_32x32x16_f16 A operand for a whole
+// wave: 64 lanes x 8 halves = 1 KiB, stored lane-linear so a wave loads it with one ds_read_b128.
+constexpr int kFragHalves = 512;
+// forward image: L0 2 M-blocks x 5 k-steps, L1..L4 2 x 4 each, L5 1 x 4          = 46 fragments
+constexpr int kFwdFrags = 2 * 5 + 4 * 2 * 4 + 4;
+// backward image (W_l^T for l = 5..1): L5^T 2 M-blocks x 1 k-step, L4^T..L1^T 2 x 4 = 34 fragments
+constexpr int kBwdFrags = 2 + 4 * 2 * 4;
+constexpr int kFwdHalves = kFwdFrags * kFragHalves;  // 23552 halves = 46 KiB
+constexpr int kBwdHalves = kBwdFrags * kFragHalves;  // 17408 halves = 34 KiB
+
+// Gradient exchange buffer: loss-scaled dL/dW (NRC_NUM_PARAMS f32) followed by the minibatch loss.
+constexpr int kGradFloats = NRC_NUM_PARAMS + 4;
+
+constexpr int kTrainSamplesPerBlock = 128;  // 4 waves x 32 samples
+
+// Fragment index helpers (see DESIGN.md "MFMA operand images").
+__host__ __device__ constexpr int fwd_frag(int layer, int mb, int kk) {
+    return layer == 0 ? mb * 5 + kk : (layer <= 4 ? 10 + (layer - 1) * 8 + mb * 4 + kk : 42 + kk);
+}
+__host__ __device__ constexpr int bwd_frag(int layer, int mb, int kk) {
+    return layer == 5 ? mb : 2 + (layer - 1) * 8 + mb * 4 + kk;
+}
+// Row index of element j of a B fragment for k-step kk taken from a 32x32 accumulator pair
+// (accumulator-as-operand, cdna_hip_programming.md §3): lane half h.
+__host__ __device__ constexpr int acc_row(int kk, int h, int j) {
+    return 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+// Layer-0 K slot -> canonical encoded feature. Each lane half computes 40 slots (n = 8*kk + j):
+// 18 TriangleWave (3 dims x 6 of the 12 octaves), 12 OneBlob (3 dims x 4 bins), 3 Identity, 7 pad.
+__host__ __device__ constexpr int slot_feature(int n, int h) {
+    return n < 18   ? (n / 6) * 12 + (n % 6) + 6 * h
+           : n < 30 ? 36 + (3 * h + (n - 18) / 4) * 4 + (n - 18) % 4
+           : n < 33 ? 60 + 3 * h + (n - 30)
+                    : 66 + (n - 33) + 7 * h;
+}
+// K index (column of the layer-0 MFMA, 0..79) -> canonical feature.
+__host__ __device__ constexpr int k0_feature(int K) {
+    return slot_feature(8 * (K >> 4) + (K & 7), (K >> 3) & 1);
+}
+
+// ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
+hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
+hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
+// fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
+hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
+                                float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,
+                                float* loss_partials, hipStream_t s);
+int train_blocks(int64_t b);
+
+enum ReduceMode { kReduceFused = 0, kReduceOnly = 1, kApplyOnly = 2, kPackOnly = 3 };
+struct OptimArgs {
+    float lr, beta1, beta2, eps, l2_reg, ema_decay, loss_scale;
+    uint32_t step;
+};
+struct ModelBuffers {
+    float *params, *m, *v, *ema, *infer;  // f32 master / Adam / EMA / debiased EMA (inference)
+    _Float16 *wf_train, *wb_train, *wf_infer;
+    const int *fwd_pos, *bwd_pos;
+};
+hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
+                              float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
+                              hipStream_t s);
+
+}  // namespace nrc_amd

@@ -1,0 +1,595 @@
+// nrc_kernels.hip — gfx950 (CDNA4) kernels of the NRC query/train hot path.
+//
+// Replaces the tiny-cuda-nn calls the reference makes from /root/reference/nrc/src/NRCNetwork.cu:
+//   network->inference      (:152)  -> infer_kernel       (fused Composite encode + 64x5 MLP + cast)
+//   trainer->training_step  (:129)  -> train_kernel        (encode + fwd + RelativeL2Luminance + bwd +
+//                                                           per-block weight-gradient partials)
+//                                     reduce_adam_kernel  (fixed-order dW reduce + Adam + EMA + f16 repack)
+//   trainer->loss           (:131)  -> loss partials reduced in reduce_adam_kernel
+//
+// Design: every matmul is a chain of v_mfma_f32_32x32x16_f16 with samples on the MFMA
+// column (lane) axis and features on the row axis, so each layer's f32 accumulator converts in
+// registers into the next layer's B operand (no LDS round trip between layers). Weights live in LDS
+// as pre-swizzled A-operand "fragment images" (one ds_read_b128 per MFMA), packed by
+// reduce_adam_kernel after every optimizer step. Weight gradients (a contraction over samples) go
+// through a per-block LDS transpose read with ds_read_b64_tr_b16.
+#include "nrc_internal.h"
+
+namespace nrc_amd {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma(h8 a, h8 b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f16v zero16() {
+    f16v z = {};
+    return z;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Composite encoding (NRCNetworkConfigs.h:51-81), computed in f32 per lane, 40 K slots per lane half.
+// ------------------------------------------------------------------------------------------------
+struct QLane {
+    float p0, p1, p2;  // position (both halves)
+    float b0, b1, b2;  // OneBlob inputs 3+3h .. 5+3h
+    float i0, i1, i2;  // Identity inputs 9+3h .. 11+3h
+};
+
+__device__ __forceinline__ QLane load_q(const float* __restrict__ q, int64_t s, int h) {
+    const float* r = q + s * NRC_INPUT_DIMS;
+    QLane Q;
+    Q.p0 = r[0];
+    Q.p1 = r[1];
+    Q.p2 = r[2];
+    const float* rb = r + 3 + 3 * h;
+    Q.b0 = rb[0];
+    Q.b1 = rb[1];
+    Q.b2 = rb[2];
+    const float* ri = r + 9 + 3 * h;
+    Q.i0 = ri[0];
+    Q.i1 = ri[1];
+    Q.i2 = ri[2];
+    return Q;
+}
+
+// TriangleWave [L spec choice, SURVEY A.2]: |2 frac(u) - 1|.
+__device__ __forceinline__ float tri(float u) {
+    const float fr = u - floorf(u);
+    return fabsf(2.0f * fr - 1.0f);
+}
+
+// OneBlob quartic CDF with inv_radius = n_bins = 4.
+__device__ __forceinline__ float qcdf(float x) {
+    const float u = x * 4.0f;
+    const float u2 = u * u;
+    const float u4 = u2 * u2;
+    const float v = (1.0f / 16.0f) * u * (15.0f - 10.0f * u2 + 3.0f * u4) + 0.5f;
+    return fminf(fmaxf(v, 0.0f), 1.0f);
+}
+
+__device__ __forceinline__ void one_blob(float x, float* o) {
+    float left[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const float d = 0.25f * (float)b - x;
+        left[b] = qcdf(d) + qcdf(d - 1.0f) + qcdf(d + 1.0f);
+    }
+    o[0] = left[1] - left[0];
+    o[1] = left[2] - left[1];
+    o[2] = left[3] - left[2];
+    o[3] = left[0] + 1.0f - left[3];
+}
+
+// v[n] = value of K slot n (n = 8*kk + j) for lane half h, see slot_feature().
+__device__ __forceinline__ void encode_f32(const QLane& Q, int h, float (&v)[40]) {
+    const float hs = h ? 64.0f : 1.0f;  // octaves 6..11 for the upper half
+    const float p[3] = {Q.p0 * hs, Q.p1 * hs, Q.p2 * hs};
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) v[d * 6 + k] = tri(p[d] * (float)(1 << k));
+    one_blob(Q.b0, &v[18]);
+    one_blob(Q.b1, &v[22]);
+    one_blob(Q.b2, &v[26]);
+    v[30] = Q.i0;
+    v[31] = Q.i1;
+    v[32] = Q.i2;
+#pragma unroll
+    for (int n = 33; n < 40; ++n) v[n] = 1.0f;
+}
+
+__device__ __forceinline__ void encode(const QLane& Q, int h, h8 (&x)[5]) {
+    float v[40];
+    encode_f32(Q, h, v);
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[kk][j] = (_Float16)v[8 * kk + j];
+}
+
+// Accumulator rows 8s..8s+7 -> f16 B fragment of the next layer, ReLU applied (ReLU commutes with
+// round-to-nearest, so this equals f16(relu(acc))).
+__device__ __forceinline__ void relu_pack(const f16v& a, h8& lo, h8& hi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        lo[j] = (_Float16)fmaxf(a[j], 0.0f);
+        hi[j] = (_Float16)fmaxf(a[8 + j], 0.0f);
+    }
+}
+
+// Backward ReLU: delta = f16(acc) where the forward activation a > 0, else 0.
+__device__ __forceinline__ void mask_pack(const f16v& a, const h8& m_lo, const h8& m_hi, h8& lo, h8& hi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        lo[j] = m_lo[j] > (_Float16)0.0f ? (_Float16)a[j] : (_Float16)0.0f;
+        hi[j] = m_hi[j] > (_Float16)0.0f ? (_Float16)a[8 + j] : (_Float16)0.0f;
+    }
+}
+
+template <int KK>
+__device__ __forceinline__ void mlp_layer(const h8* __restrict__ lw, int frag0, const h8 (&x)[KK], int lane,
+                                          f16v& a0, f16v& a1) {
+    a0 = zero16();
+    a1 = zero16();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+        a0 = mfma(lw[(frag0 + kk) * 64 + lane], x[kk], a0);
+        a1 = mfma(lw[(frag0 + KK + kk) * 64 + lane], x[kk], a1);
+    }
+}
+
+// Forward through the five hidden-producing layers; a[l][*] = input of layer l+1 (B fragments).
+__device__ __forceinline__ void mlp_hidden(const h8* __restrict__ lw, const h8 (&x)[5], int lane, h8 (&a)[5][4]) {
+    f16v c0, c1;
+    mlp_layer<5>(lw, fwd_frag(0, 0, 0), x, lane, c0, c1);
+    relu_pack(c0, a[0][0], a[0][1]);
+    relu_pack(c1, a[0][2], a[0][3]);
+#pragma unroll
+    for (int l = 1; l < 5; ++l) {
+        mlp_layer<4>(lw, fwd_frag(l, 0, 0), a[l - 1], lane, c0, c1);
+        relu_pack(c0, a[l][0], a[l][1]);
+        relu_pack(c1, a[l][2], a[l][3]);
+    }
+}
+
+__device__ __forceinline__ f16v mlp_out(const h8* __restrict__ lw, const h8 (&a5)[4], int lane) {
+    f16v o = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) o = mfma(lw[fwd_frag(5, 0, kk) * 64 + lane], a5[kk], o);
+    return o;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Inference: persistent waves, 32 queries per wave-iteration.
+// ------------------------------------------------------------------------------------------------
+constexpr int kInferThreads = 256;
+
+__global__ __launch_bounds__(kInferThreads) void infer_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                              int64_t n, const h8* __restrict__ wf) {
+    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    for (int i = threadIdx.x; i < kFwdFrags * 64; i += kInferThreads) lw[i] = wf[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    const int64_t ntiles = (n + 31) >> 5;
+    const int64_t wstride = (int64_t)gridDim.x * (kInferThreads / 64);
+    int64_t tile = (int64_t)blockIdx.x * (kInferThreads / 64) + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    const int64_t last = n - 1;
+
+    QLane Q = load_q(q, min(tile * 32 + r, last), h);
+    for (; tile < ntiles; tile += wstride) {
+        const int64_t s = tile * 32 + r;
+        h8 x[5];
+        encode(Q, h, x);
+        const int64_t nt = tile + wstride;
+        if (nt < ntiles) Q = load_q(q, min(nt * 32 + r, last), h);
+
+        h8 a[5][4];
+        mlp_hidden(lw, x, lane, a);
+        const f16v o = mlp_out(lw, a[4], lane);
+        // Output rows 0..2 sit in registers 0..2 of lanes 0..31 (C/D map row = (reg&3)+8(reg>>2)+4h).
+        // tcnn casts the f16 network output to f32 (trim_and_cast).
+        if (h == 0 && s < n) {
+            float* dst = out + s * NRC_OUTPUT_DIMS;
+            dst[0] = (float)(_Float16)fmaxf(o[0], 0.0f);
+            dst[1] = (float)(_Float16)fmaxf(o[1], 0.0f);
+            dst[2] = (float)(_Float16)fmaxf(o[2], 0.0f);
+        }
+    }
+}
+
+// Standalone encoding kernel (HBM-bound; used by the parity tests of the encoding): writes the f32
+// features in canonical tcnn order, [n][80].
+__global__ void encode_kernel(const float* __restrict__ q, float* __restrict__ enc, int64_t n) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = gid >> 1;
+    const int h = (int)(gid & 1);
+    if (s >= n) return;
+    const QLane Q = load_q(q, s, h);
+    float v[40];
+    encode_f32(Q, h, v);
+#pragma unroll
+    for (int k = 0; k < 40; ++k) enc[s * NRC_ENC_WIDTH + slot_feature(k, h)] = v[k];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Training: one block = 4 waves = 128 samples.
+// ------------------------------------------------------------------------------------------------
+// LDS images of activations / deltas for the weight-gradient GEMMs: [128 samples][64 features] f16,
+// 128-B rows, 8-byte slots XOR-swizzled by a bijection of (s mod 16) so that both the row writes
+// (ds_write_b64, one sample per lane) and the transposed reads (ds_read_b64_tr_b16) are conflict-free.
+__device__ __forceinline__ int img_off(int s, int c) {
+    const int hs = (s & 1) | (((s >> 1) & 1) << 3) | (((s >> 2) & 3) << 1);
+    return s * 128 + ((((c >> 2) ^ hs)) << 3) + ((c & 3) << 1);
+}
+
+__device__ __forceinline__ h4 tr_read(const char* p) {
+    const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
+    return __builtin_bit_cast(h4, v);
+}
+
+__device__ __forceinline__ h8 cat(h4 a, h4 b) {
+    h8 r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+    return r;
+}
+
+// MFMA operand with samples on k: lane (row = 32*fb + (lane&31), half hh) gets samples 16kk+8hh+0..7
+// of that feature, from a [sample][feature] image (cdna_hip_programming.md T10).
+__device__ __forceinline__ h8 tr_frag(const char* img, int fb, int kk, int lane) {
+    const int g = lane >> 4, idx = lane & 15, q = idx >> 2, p = idx & 3;
+    const int c = 32 * fb + 16 * (g & 1) + 4 * p;
+    const int s0 = 16 * kk + 8 * (g >> 1) + q;
+    return cat(tr_read(img + img_off(s0, c)), tr_read(img + img_off(s0 + 4, c)));
+}
+
+// Same for the 16-wide x_hi image ([128][16] f16, 32-B rows); lanes for features >= 16 read the same
+// addresses as their partners (results discarded).
+__device__ __forceinline__ h8 tr_frag_xhi(const char* img, int kk, int lane) {
+    const int g = lane >> 4, idx = lane & 15, q = idx >> 2, p = idx & 3;
+    const int s0 = 16 * kk + 8 * (g >> 1) + q;
+    return cat(tr_read(img + s0 * 32 + 8 * p), tr_read(img + (s0 + 4) * 32 + 8 * p));
+}
+
+__device__ __forceinline__ void store_h4(char* img, int off, h8 v, int j0) {
+    h4 t;
+    t[0] = v[j0]; t[1] = v[j0 + 1]; t[2] = v[j0 + 2]; t[3] = v[j0 + 3];
+    *(h4*)(img + off) = t;
+}
+
+// Write a 64-row activation/delta held as 4 B fragments (rows acc_row(kk,h,j)) into the image.
+__device__ __forceinline__ void write_rows64(char* img, int sl, int h, const h8 (&f)[4]) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int jg = 0; jg < 2; ++jg) store_h4(img, img_off(sl, acc_row(kk, h, 4 * jg)), f[kk], 4 * jg);
+}
+
+constexpr int kLdsWf = kFwdHalves * 2;   // 47104
+constexpr int kLdsWb = kBwdHalves * 2;   // 34816
+constexpr int kLdsImg = 128 * 128;       // 16384
+constexpr int kLdsXhi = 128 * 32;        // 4096
+constexpr int kLdsTrain = kLdsWf + kLdsWb + 2 * kLdsImg + kLdsXhi + 16;
+
+// dW output block (mb, nb) of layer L: A = delta image (features = output rows), B = activation image.
+template <int L>
+__device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, const char* img_xh, int mb, int nb,
+                                         int lane, float* __restrict__ slab) {
+    f16v acc = zero16();
+    const bool zero_a = (L == 5) && (lane & 16);  // rows 16..31 of the 16-row output delta do not exist
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        h8 A = tr_frag(img_d, mb, kk, lane);
+        if (zero_a) A = h8{};
+        h8 B;
+        if (L == 0 && nb == 2) B = tr_frag_xhi(img_xh, kk, lane);
+        else B = tr_frag(img_a, nb, kk, lane);
+        acc = mfma(A, B, acc);
+    }
+    const int h = lane >> 5, col = 32 * nb + (lane & 31);
+    constexpr int in_dim = (L == 0) ? NRC_ENC_WIDTH : NRC_WIDTH;
+    constexpr int off = L == 0 ? NRC_W0_OFFSET
+                        : L == 1 ? NRC_W1_OFFSET
+                        : L == 2 ? NRC_W2_OFFSET
+                        : L == 3 ? NRC_W3_OFFSET
+                        : L == 4 ? NRC_W4_OFFSET
+                                 : NRC_W5_OFFSET;
+    int fcol = col;
+    if (L == 0) {
+        if (col >= NRC_ENC_WIDTH) return;
+        fcol = k0_feature(col);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (L == 5 && row >= NRC_OUT_PADDED) continue;
+        slab[off + row * in_dim + fcol] = acc[reg];
+    }
+}
+
+template <int L>
+__device__ __forceinline__ void dw_layer(const char* img_d, const char* img_a, const char* img_xh, int wave, int lane,
+                                         float* __restrict__ slab) {
+    if (L == 5) {
+        if (wave < 2) dw_block<5>(img_d, img_a, img_xh, 0, wave, lane, slab);
+    } else if (L == 0) {
+        dw_block<0>(img_d, img_a, img_xh, wave / 3, wave % 3, lane, slab);
+        if (wave < 2) dw_block<0>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane, slab);
+    } else {
+        dw_block<L>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane, slab);
+    }
+}
+
+// delta_{L-1} = (W_L^T delta_L) * [a_L > 0]
+template <int L>
+__device__ __forceinline__ void bwd_chain(const h8* __restrict__ lwb, const h8 (&d)[4], const h8 (&a)[4], int lane,
+                                          h8 (&dn)[4]) {
+    constexpr int KK = (L == 5) ? 1 : 4;
+    f16v c0 = zero16(), c1 = zero16();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+        c0 = mfma(lwb[bwd_frag(L, 0, kk) * 64 + lane], d[kk], c0);
+        c1 = mfma(lwb[bwd_frag(L, 1, kk) * 64 + lane], d[kk], c1);
+    }
+    mask_pack(c0, a[0], a[1], dn[0], dn[1]);
+    mask_pack(c1, a[2], a[3], dn[2], dn[3]);
+}
+
+__global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__ q, const float* __restrict__ t,
+                                                       int64_t b, float n_total, float loss_scale,
+                                                       const h8* __restrict__ wf, const h8* __restrict__ wb,
+                                                       float* __restrict__ slabs, float* __restrict__ loss_partials) {
+    __shared__ __attribute__((aligned(16))) char smem[kLdsTrain];
+    h8* lwf = (h8*)smem;
+    h8* lwb = (h8*)(smem + kLdsWf);
+    char* img_a = smem + kLdsWf + kLdsWb;
+    char* img_d = img_a + kLdsImg;
+    char* img_xh = img_d + kLdsImg;
+    float* red = (float*)(img_xh + kLdsXhi);
+
+    for (int i = threadIdx.x; i < kFwdFrags * 64; i += 256) lwf[i] = wf[i];
+    for (int i = threadIdx.x; i < kBwdFrags * 64; i += 256) lwb[i] = wb[i];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, r = lane & 31;
+    const int sl = wave * 32 + r;
+    const int64_t s = (int64_t)blockIdx.x * kTrainSamplesPerBlock + sl;
+    const bool valid = s < b;
+    const int64_t sc = valid ? s : b - 1;
+    const QLane Q = load_q(q, sc, h);
+    float tgt[3] = {0.f, 0.f, 0.f};
+    if (h == 0) {
+        tgt[0] = t[sc * 3 + 0];
+        tgt[1] = t[sc * 3 + 1];
+        tgt[2] = t[sc * 3 + 2];
+    }
+    h8 x[5];
+    encode(Q, h, x);
+    __syncthreads();  // weights in LDS
+
+    h8 a[5][4];
+    mlp_hidden(lwf, x, lane, a);
+    const f16v o = mlp_out(lwf, a[4], lane);
+
+    // RelativeL2Luminance on the f16 prediction, loss-scaled f16 gradient, ReLU-masked.
+    float lossv = 0.0f;
+    h8 g[4] = {h8{}, h8{}, h8{}, h8{}};
+    if (h == 0) {
+        float y[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) y[c] = (float)(_Float16)fmaxf(o[c], 0.0f);
+        const float lum = 0.299f * y[0] + 0.587f * y[1] + 0.114f * y[2];
+        const float denom = lum * lum + NRC_LUM_EPS;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float diff = y[c] - tgt[c];
+            const float lv = diff * diff / denom / n_total;
+            const float gv = loss_scale * 2.0f * diff / denom / n_total;
+            lossv += valid ? lv : 0.0f;
+            g[0][c] = (valid && y[c] > 0.0f) ? (_Float16)gv : (_Float16)0.0f;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lossv += __shfl_xor(lossv, off);
+    if (lane == 0) red[wave] = lossv;
+
+    float* slab = slabs + (int64_t)blockIdx.x * NRC_NUM_PARAMS;
+
+    // images for layer 5: delta_5 = g (16 rows, k-step 0 only), a_5
+#pragma unroll
+    for (int jg = 0; jg < 2; ++jg) store_h4(img_d, img_off(sl, acc_row(0, h, 4 * jg)), g[0], 4 * jg);
+    write_rows64(img_a, sl, h, a[4]);
+    __syncthreads();
+    if (threadIdx.x == 0) loss_partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+
+    h8 d4[4], d3[4], d2[4], d1[4], d0[4];
+    // ---- layer 5
+    bwd_chain<5>(lwb, g, a[4], lane, d4);
+    dw_layer<5>(img_d, img_a, img_xh, wave, lane, slab);
+    __syncthreads();
+    write_rows64(img_d, sl, h, d4);
+    write_rows64(img_a, sl, h, a[3]);
+    __syncthreads();
+    // ---- layer 4
+    bwd_chain<4>(lwb, d4, a[3], lane, d3);
+    dw_layer<4>(img_d, img_a, img_xh, wave, lane, slab);
+    __syncthreads();
+    write_rows64(img_d, sl, h, d3);
+    write_rows64(img_a, sl, h, a[2]);
+    __syncthreads();
+    // ---- layer 3
+    bwd_chain<3>(lwb, d3, a[2], lane, d2);
+    dw_layer<3>(img_d, img_a, img_xh, wave, lane, slab);
+    __syncthreads();
+    write_rows64(img_d, sl, h, d2);
+    write_rows64(img_a, sl, h, a[1]);
+    __syncthreads();
+    // ---- layer 2
+    bwd_chain<2>(lwb, d2, a[1], lane, d1);
+    dw_layer<2>(img_d, img_a, img_xh, wave, lane, slab);
+    __syncthreads();
+    write_rows64(img_d, sl, h, d1);
+    write_rows64(img_a, sl, h, a[0]);
+    __syncthreads();
+    // ---- layer 1
+    bwd_chain<1>(lwb, d1, a[0], lane, d0);
+    dw_layer<1>(img_d, img_a, img_xh, wave, lane, slab);
+    __syncthreads();
+    // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a, x_hi -> img_xh)
+    write_rows64(img_d, sl, h, d0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int jg = 0; jg < 2; ++jg) store_h4(img_a, img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
+    *(h8*)(img_xh + sl * 32 + 16 * h) = x[4];
+    __syncthreads();
+    // ---- layer 0
+    dw_layer<0>(img_d, img_a, img_xh, wave, lane, slab);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fixed-order weight-gradient reduction + tcnn Adam + EMA + f16 fragment-image repack.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
+                                                          const float* __restrict__ loss_partials,
+                                                          float* __restrict__ grad_io, float* __restrict__ loss_out,
+                                                          ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+#pragma clang fp contract(off)
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (mode == kReduceFused || mode == kReduceOnly) {
+            float L = 0.0f;
+            for (int i = 0; i < nslabs; ++i) L += loss_partials[i];
+            if (mode == kReduceOnly) grad_io[NRC_NUM_PARAMS] = L;
+            else if (loss_out) loss_out[0] = L;
+        } else if (mode == kApplyOnly && loss_out) {
+            loss_out[0] = grad_io[NRC_NUM_PARAMS];
+        }
+    }
+    if (p >= NRC_NUM_PARAMS) return;
+    float w, inf;
+    if (mode == kPackOnly) {
+        w = mb.params[p];
+        inf = mb.infer[p];
+    } else {
+        float gsum;
+        if (mode == kApplyOnly) {
+            gsum = grad_io[p];
+        } else {
+            // fixed order: 4 interleaved partial sums, combined in a fixed tree
+            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
+            int i = 0;
+            for (; i + 4 <= nslabs; i += 4) {
+                g0 += slabs[(int64_t)(i + 0) * NRC_NUM_PARAMS + p];
+                g1 += slabs[(int64_t)(i + 1) * NRC_NUM_PARAMS + p];
+                g2 += slabs[(int64_t)(i + 2) * NRC_NUM_PARAMS + p];
+                g3 += slabs[(int64_t)(i + 3) * NRC_NUM_PARAMS + p];
+            }
+            for (; i < nslabs; ++i) g0 += slabs[(int64_t)i * NRC_NUM_PARAMS + p];
+            gsum = (g0 + g1) + (g2 + g3);
+            if (mode == kReduceOnly) {
+                grad_io[p] = gsum;
+                return;
+            }
+        }
+        // tcnn Adam (optimizers/adam.h); lr_t and the EMA debias come from the host in f32.
+        float gradient = gsum / oa.loss_scale;
+        w = mb.params[p];
+        gradient += oa.l2_reg * w;
+        const float gsq = gradient * gradient;
+        const float m1 = oa.beta1 * mb.m[p] + (1.0f - oa.beta1) * gradient;
+        const float v1 = oa.beta2 * mb.v[p] + (1.0f - oa.beta2) * gsq;
+        mb.m[p] = m1;
+        mb.v[p] = v1;
+        const float eff = lr_t / (sqrtf(v1) + oa.eps);
+        w = w - eff * m1;
+        mb.params[p] = w;
+        const float e = mb.ema[p] * oa.ema_decay + w * (1.0f - oa.ema_decay);
+        mb.ema[p] = e;
+        inf = e / ema_debias;
+        mb.infer[p] = inf;
+    }
+    const int fp = mb.fwd_pos[p];
+    mb.wf_train[fp] = (_Float16)w;
+    mb.wf_infer[fp] = (_Float16)inf;
+    const int bp = mb.bwd_pos[p];
+    if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static int num_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!cached[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cached[dev] = v;
+    }
+    return cached[dev];
+}
+
+static int infer_blocks_per_cu() {
+    static int cached = 0;
+    if (!cached) {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, infer_kernel, kInferThreads, 0) != hipSuccess || v <= 0)
+            v = 1;
+        cached = v;
+    }
+    return cached;
+}
+
+hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t ntiles = (n + 31) / 32;
+    const int64_t want = (ntiles + 3) / 4;
+    const int64_t cap = (int64_t)num_cus() * infer_blocks_per_cu();
+    const int grid = (int)(want < cap ? want : cap);
+    hipLaunchKernelGGL(infer_kernel, dim3(grid), dim3(kInferThreads), 0, s, queries, out, n, (const h8*)wf);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t threads = 2 * n;
+    const int grid = (int)((threads + 255) / 256);
+    hipLaunchKernelGGL(encode_kernel, dim3(grid), dim3(256), 0, s, queries, enc, n);
+    return hipGetLastError();
+}
+
+int train_blocks(int64_t b) { return (int)((b + kTrainSamplesPerBlock - 1) / kTrainSamplesPerBlock); }
+
+hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
+                                float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,
+                                float* loss_partials, hipStream_t s) {
+    if (b <= 0) return hipSuccess;
+    hipLaunchKernelGGL(train_kernel, dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total, loss_scale,
+                       (const h8*)wf, (const h8*)wb, slabs, loss_partials);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials, float* grad_io,
+                              float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+    // Bias corrections in host f32 (glibc powf/sqrtf), identical to the oracle's.
+    const float step = (float)(oa.step ? oa.step : 1);
+    const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
+    const float ema_debias = 1.0f - powf(oa.ema_decay, step);
+    const int grid = (NRC_NUM_PARAMS + 255) / 256;
+    hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(256), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
+                       loss_out, mb, oa, lr_t, ema_debias);
+    return hipGetLastError();
+}
+
+}  // namespace nrc_amd

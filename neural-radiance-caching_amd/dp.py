@@ -1,0 +1,51 @@
+"""Data-parallel sharding of the NRC hot path over one process per GPU (torch.distributed).
+
+New capability: the reference runs one independent, unsynchronised network
+per device (/root/reference/nrc/src/Device.cpp:420, nrc/inc/Device.h:621) and has no collectives.
+
+* Inference: queries are independent units; each rank takes a contiguous shard of the frame's
+  queries. No collective on the data path.
+* Training: one exchange step per minibatch. Each rank computes the loss-scaled gradient of its local
+  samples normalised by the GLOBAL batch (3 * global_b), the ranks sum it (one all-reduce of
+  NRC_GRAD_FLOATS f32 = 88 KiB: RCCL over xGMI with the "nccl" backend; gloo on CPU), and every rank
+  applies the identical Adam + EMA step, so replicas stay bit-identical.
+
+``backend`` is any object with ``train_grad(inputs, targets, b, global_b, grad)`` and
+``train_apply(grad, loss)`` — ``network.Network`` on the GPU, an oracle-backed stand-in in the
+CPU tests.
+"""
+from __future__ import annotations
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous shard [start, start + count) of n units for rank (sizes differ by at most 1)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    base, rem = divmod(int(n), int(world))
+    start = rank * base + min(rank, rem)
+    count = base + (1 if rank < rem else 0)
+    return start, count
+
+
+class DataParallelTrainer:
+    def __init__(self, backend, grad_buffer, group=None):
+        import torch.distributed as dist
+
+        self.backend = backend
+        self.grad = grad_buffer  # torch tensor of GRAD_FLOATS f32 on the backend's device
+        self.group = group
+        self._dist = dist
+
+    def broadcast_state(self, get_state, set_state, slots, device) -> None:
+        """Make every replica start from rank 0's state (weights, EMA, Adam moments)."""
+        import torch
+
+        for slot in slots:
+            t = torch.from_numpy(get_state(slot)).to(device)
+            self._dist.broadcast(t, src=0, group=self.group)
+            set_state(slot, t.cpu().numpy())
+
+    def step(self, inputs, targets, b_local: int, global_b: int, loss: bool = False):
+        self.backend.train_grad(inputs, targets, b_local, global_b, self.grad)
+        self._dist.all_reduce(self.grad, op=self._dist.ReduceOp.SUM, group=self.group)
+        return self.backend.train_apply(self.grad, loss)

@@ -1,0 +1,229 @@
+"""Host-side mirror of the reference's ``nrc::Network`` (/root/reference/nrc/inc/NRCNetwork.h:20-75)
+over the C-ABI (include/nrc/nrc_c.h).
+
+Method names, argument meaning and error behaviour follow the reference:
+
+=====================================  =========================================================
+reference (NRCNetwork.h)               here
+=====================================  =========================================================
+``Network()`` / ``~Network()``         ``Network()`` / garbage collection (``nrc_create``/``nrc_free``)
+``init<Verbose>(stream, encoding)``    ``init(stream, encoding, verbose=False)``
+``destroy()``                          ``destroy()``
+``train(in, tgt, loss_h)``             ``train(inputs, targets, loss=False)`` -> loss or None
+``train(in, tgt, stream, loss_h)``     ``train(inputs, targets, stream=s, loss=...)``
+``infer(in, out, n)``                  ``infer(inputs, outputs, num_inputs)``
+``infer(in, out, n, stream)``          ``infer(inputs, outputs, num_inputs, stream=s)``
+``setStream`` / ``setHyperParams``     ``setStream`` / ``setHyperParams`` (+ snake_case aliases)
+``setConfig`` / ``getLearningRate``    ``setConfig`` / ``getLearningRate``
+=====================================  =========================================================
+
+As in the reference (NRCNetwork.cu:119, :142), ``train`` / ``infer`` after ``destroy()`` are silent
+no-ops; the C-ABI reports them as ``NRC_ERR_DESTROYED``. Buffers are device pointers: a CUDA
+(HIP) ``torch.Tensor`` (float32, contiguous) or a raw integer address. ``train`` consumes exactly
+``BATCH_SIZE`` = 16384 samples (NRCNetwork.cu:127-128).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from enum import IntEnum
+
+import numpy as np
+
+from . import _lib
+from ._lib import BATCH_SIZE, GRAD_FLOATS, NUM_PARAMS, NrcConfig, NrcError, NrcHyperParams, check, lib
+
+NRC_ERR_DESTROYED = 2
+
+
+class InputEncoding(IntEnum):
+    """nrc::InputEncoding (neural_radiance_caching.h:24-27)."""
+    Frequency = 0
+    Hash = 1
+
+
+class StateSlot(IntEnum):
+    PARAMS = 0
+    INFER = 1
+    EMA = 2
+    ADAM_M = 3
+    ADAM_V = 4
+
+
+@dataclass
+class HyperParams:
+    """nrc::HyperParams (NRCNetwork.h:10-13)."""
+    learningRate: float
+
+
+def _dev_ptr(x, what: str, min_elems: int | None = None) -> int:
+    if x is None:
+        raise ValueError(f"{what}: null buffer")
+    if isinstance(x, int):
+        return x
+    # torch.Tensor (duck-typed so that importing this module does not require torch)
+    if hasattr(x, "data_ptr"):
+        if not x.is_cuda:
+            raise ValueError(f"{what}: tensor must live on the GPU")
+        if str(x.dtype) != "torch.float32":
+            raise ValueError(f"{what}: tensor must be float32")
+        if not x.is_contiguous():
+            raise ValueError(f"{what}: tensor must be contiguous")
+        if min_elems is not None and x.numel() < min_elems:
+            raise ValueError(f"{what}: needs at least {min_elems} floats, got {x.numel()}")
+        return int(x.data_ptr())
+    raise TypeError(f"{what}: expected a CUDA tensor or an integer device address, got {type(x)}")
+
+
+def _stream_ptr(stream) -> int | None:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    if hasattr(stream, "cuda_stream"):
+        return int(stream.cuda_stream)
+    raise TypeError(f"stream: expected torch.cuda.Stream or int, got {type(stream)}")
+
+
+def current_stream() -> int:
+    import torch
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+class Network:
+    """MI355X-native drop-in for nrc::Network."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        check(lib().nrc_create(ctypes.byref(h)))
+        self._h = h
+        self._lib = lib()
+
+    # ---- lifecycle ---------------------------------------------------------------------------
+    def init(self, stream=None, encoding: InputEncoding = InputEncoding.Frequency, verbose: bool = False,
+             config: NrcConfig | None = None) -> None:
+        s = _stream_ptr(stream)
+        cfg = ctypes.byref(config) if config is not None else None
+        check(self._lib.nrc_init(self._h, s, int(encoding), cfg, int(bool(verbose))))
+
+    def destroy(self) -> None:
+        check(self._lib.nrc_destroy(self._h))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self._lib.nrc_free(h)
+            except Exception:
+                pass
+            self._h = ctypes.c_void_p()
+
+    # ---- hot path ----------------------------------------------------------------------------
+    def train(self, inputs, targets, stream=None, loss: bool = False):
+        """One training step on BATCH_SIZE samples; returns the batch loss if loss=True (blocking)."""
+        pi = _dev_ptr(inputs, "inputs", BATCH_SIZE * 15 if hasattr(inputs, "numel") else None)
+        pt = _dev_ptr(targets, "targets", BATCH_SIZE * 3 if hasattr(targets, "numel") else None)
+        lh = ctypes.c_float(float("nan"))
+        lp = ctypes.byref(lh) if loss else None
+        if stream is None:
+            st = self._lib.nrc_train(self._h, pi, pt, lp)
+        else:
+            st = self._lib.nrc_train_stream(self._h, pi, pt, _stream_ptr(stream), lp)
+        if st == NRC_ERR_DESTROYED:
+            return None
+        check(st)
+        return lh.value if loss else None
+
+    def infer(self, inputs, outputs, numInputs: int, stream=None) -> None:
+        n = int(numInputs)
+        if n < 0 or n > 0xFFFFFFFF:
+            raise ValueError("numInputs out of range")
+        pi = _dev_ptr(inputs, "inputs", n * 15 if hasattr(inputs, "numel") else None)
+        po = _dev_ptr(outputs, "outputs", n * 3 if hasattr(outputs, "numel") else None)
+        if stream is None:
+            st = self._lib.nrc_infer(self._h, pi, po, n)
+        else:
+            st = self._lib.nrc_infer_stream(self._h, pi, po, n, _stream_ptr(stream))
+        if st == NRC_ERR_DESTROYED:
+            return None
+        check(st)
+
+    # ---- configuration -----------------------------------------------------------------------
+    def setStream(self, stream) -> None:
+        check(self._lib.nrc_set_stream(self._h, _stream_ptr(stream)))
+
+    def setHyperParams(self, hp: HyperParams) -> None:
+        c = NrcHyperParams(float(hp.learningRate))
+        check(self._lib.nrc_set_hyper_params(self._h, ctypes.byref(c)))
+
+    def setConfig(self, encoding: InputEncoding) -> None:
+        check(self._lib.nrc_set_config(self._h, int(encoding)))
+
+    def getLearningRate(self) -> float:
+        v = ctypes.c_float()
+        check(self._lib.nrc_get_learning_rate(self._h, ctypes.byref(v)))
+        return v.value
+
+    def configJson(self) -> str:
+        need = ctypes.c_size_t()
+        check(self._lib.nrc_get_config_json(self._h, None, 0, ctypes.byref(need)))
+        buf = ctypes.create_string_buffer(need.value)
+        check(self._lib.nrc_get_config_json(self._h, buf, need.value, None))
+        return buf.value.decode()
+
+    set_stream = setStream
+    set_hyper_params = setHyperParams
+    set_config = setConfig
+    get_learning_rate = getLearningRate
+    config_json = configJson
+
+    # ---- extensions: any batch size, data-parallel split, state ---------------------------
+    def train_batch(self, inputs, targets, b: int, loss: bool = False):
+        lh = ctypes.c_float(float("nan"))
+        check(self._lib.nrc_train_batch(self._h, _dev_ptr(inputs, "inputs"), _dev_ptr(targets, "targets"), int(b),
+                                        ctypes.byref(lh) if loss else None))
+        return lh.value if loss else None
+
+    def train_grad(self, inputs, targets, b: int, global_b: int, grad) -> None:
+        check(self._lib.nrc_train_grad(self._h, _dev_ptr(inputs, "inputs") if b else None,
+                                       _dev_ptr(targets, "targets") if b else None, int(b), int(global_b),
+                                       _dev_ptr(grad, "grad", GRAD_FLOATS if hasattr(grad, "numel") else None)))
+
+    def train_apply(self, grad, loss: bool = False):
+        lh = ctypes.c_float(float("nan"))
+        check(self._lib.nrc_train_apply(self._h, _dev_ptr(grad, "grad"), ctypes.byref(lh) if loss else None))
+        return lh.value if loss else None
+
+    def get_state(self, slot: StateSlot = StateSlot.PARAMS) -> np.ndarray:
+        out = np.empty(NUM_PARAMS, dtype=np.float32)
+        check(self._lib.nrc_get_state(self._h, int(slot), out.ctypes.data))
+        return out
+
+    def set_state(self, slot: StateSlot, values) -> None:
+        v = np.ascontiguousarray(values, dtype=np.float32)
+        if v.size != NUM_PARAMS:
+            raise ValueError(f"state must have {NUM_PARAMS} floats")
+        check(self._lib.nrc_set_state(self._h, int(slot), v.ctypes.data))
+
+    @property
+    def step(self) -> int:
+        v = ctypes.c_uint32()
+        check(self._lib.nrc_get_step(self._h, ctypes.byref(v)))
+        return v.value
+
+    @step.setter
+    def step(self, value: int) -> None:
+        check(self._lib.nrc_set_step(self._h, int(value)))
+
+
+def encode(inputs, encoded, n: int, stream=None) -> None:
+    """The Composite encoding alone (test entry): f32 [n][80] canonical feature order."""
+    check(lib().nrc_encode(_dev_ptr(inputs, "inputs"), _dev_ptr(encoded, "encoded"), int(n), _stream_ptr(stream)))
+
+
+def default_config(encoding: InputEncoding = InputEncoding.Frequency) -> NrcConfig:
+    return lib().nrc_default_config(int(encoding))
+
+
+__all__ = ["Network", "InputEncoding", "HyperParams", "StateSlot", "NrcError", "encode", "default_config",
+           "BATCH_SIZE", "NUM_PARAMS", "GRAD_FLOATS", "current_stream"]

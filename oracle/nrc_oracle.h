@@ -1,0 +1,66 @@
+/*
+ * nrc_oracle.h — CPU restatement of the reference's NRC query/train arithmetic.
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker (or the timed CPU baseline). The product path
+ * (neural-radiance-caching_amd/) never links or calls it.
+ *
+ * PARITY UNPINNED: the reference's arithmetic lives in tiny-cuda-nn (submodule
+ * github.com/Depersonalizc/tiny-cuda-nn, /root/reference/.gitmodules:1-3), which is empty in the
+ * reference snapshot, has no recoverable pinned commit and is not importable here. The reference
+ * holds no tests, golden vectors or fixtures for this path. This oracle restates
+ * tcnn's published algorithm as the reference configures it (NRCNetworkConfigs.h:11-83) and is
+ * cross-checked against an independent float64 numpy restatement and torch autograd
+ * (tests/test_oracle.py). Spec choices are tagged [H]/[M]/[L] as in SURVEY.md Appendix A.
+ */
+#ifndef NRC_ORACLE_H
+#define NRC_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Numerics modes.
+ *  ORC_FP32  : exact f32 weights/activations, f64 dot products rounded to f32 per layer.
+ *  ORC_MIXED : the GPU build's numerics model: f16 encoded inputs, f16 weights, f32 accumulate,
+ *              f16 activations between layers, f16 output; f16 loss/backprop gradients; f32 dW.
+ *  ORC_TCNN  : tcnn FullyFusedMLP emulation [M]: as MIXED, but every matmul accumulates in f16
+ *              (one f16 rounding per 16-wide k chunk, WMMA 16x16x16), and the parameter gradient
+ *              is stored as f16 (tcnn keeps PARAMS_T gradients). */
+enum { ORC_FP32 = 0, ORC_MIXED = 1, ORC_TCNN = 2 };
+
+float orc_f16_round(float x);
+
+/* Composite encoding of n queries (15 f32 each, AoS) into n x 80 f32 in canonical tcnn feature
+ * order: [0,36) TriangleWave, [36,60) OneBlob, [60,66) Identity, [66,80) padding = 1.0. */
+void orc_encode(const float* queries, int64_t n, float* enc);
+
+/* Forward pass with the given parameter blob (22528 f32, canonical order, layout.h).
+ * out: n x 3 f32. nthreads >= 1. */
+void orc_forward(const float* params, const float* queries, int64_t n, int mode, float* out,
+                 int nthreads);
+
+/* One training minibatch: loss-scaled parameter gradient of
+ *   L = sum_{s<b, c<3} (y_sc - t_sc)^2 / (lum(y_s)^2 + 0.01) / n_total
+ * (RelativeL2Luminance, denominator not differentiated). Writes grad[22528] = loss_scale * dL/dW
+ * and returns L (the reference's Trainer::loss()). n_total = 3 * global batch. */
+double orc_grad(const float* params, const float* queries, const float* targets, int64_t b,
+                double n_total, float loss_scale, int mode, float* grad, int nthreads);
+
+/* tcnn Adam step followed by the EMA(decay) wrapper [M]. Updates params/m/v/ema in place and
+ * writes the debiased EMA weights (the inference weights) to infer_params. step is 1-based. */
+void orc_adam_ema(float* params, float* m, float* v, float* ema, float* infer_params,
+                  uint32_t step, const float* grad, float loss_scale, float lr, float beta1,
+                  float beta2, float eps, float l2_reg, float ema_decay, int64_t n);
+
+/* tcnn-style xavier-uniform initialisation (per matrix, fan_in+fan_out of the padded shapes) from
+ * a pcg32 stream; init parity with tcnn is not attainable [M], parity tests inject weights. */
+void orc_init_params(float* params, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
