@@ -122,7 +122,12 @@ nrc_status nrc_set_state(nrc_net* net, int slot, const float* host_src);
 nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
 nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 
-/* ---- test entry: the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
+/* ---- test / tuning entries ---- */
+/* Inference through a specific kernel variant (0..2, see nrc_kernels.hip) for in-process A/B timing;
+ * results are identical in meaning to nrc_infer_stream. */
+nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
+                                   hipStream_t stream);
+/* the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus

@@ -538,6 +538,17 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step) {
     });
 }
 
+nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, float* out, uint32_t n,
+                                   hipStream_t stream) {
+    return guarded([&] {
+        check_live(net);
+        if (variant < 0 || variant >= kNumInferVariants) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown variant");
+        if (n == 0) return;
+        if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+        HIP_CHECK(launch_infer_variant(variant, in, out, n, net->wf_infer, stream));
+    });
+}
+
 nrc_status nrc_encode(const float* in, float* enc, uint32_t n, hipStream_t stream) {
     return guarded([&] {
         if (n == 0) return;

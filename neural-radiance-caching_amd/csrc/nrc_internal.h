@@ -51,6 +51,9 @@ __host__ __device__ constexpr int k0_feature(int K) {
 
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
+hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
+                                hipStream_t s);
+constexpr int kNumInferVariants = 3;
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,

@@ -205,6 +205,199 @@ __global__ __launch_bounds__(kInferThreads) void infer_kernel(const float* __res
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Inference v2: VALU-lean encoding, packed-f16 ReLU, LDS-resident weights, TILES x 32 queries per
+// wave iteration (each weight fragment read from LDS feeds TILES MFMAs).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+    h2 v;
+    v[0] = (_Float16)a;
+    v[1] = (_Float16)b;
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+// OneBlob(4 bins) of one input in closed form. tcnn's formula sums 12 quartic-CDF terms;
+// at most two are unsaturated: with t = 4x, fl = floor(t), fr = t - fl the kernel mass falls into the
+// unit intervals j = fl-1, fl, fl+1 as A, B-A, 1-B (A = K(-fr), B = K(1-fr)); interval j lands in bin
+// j & 3 when -4 <= j <= 7 and in bin 3 otherwise (the period-1 wrap of the formula). Returns the four
+// bins as packed f16 pairs (bins 0,1 | bins 2,3).
+__device__ __forceinline__ void blob_fast(float x, uint32_t& lo, uint32_t& hi) {
+    const float t = x * 4.0f;
+    const float fl = floorf(t);
+    const float fr = t - fl;
+    const float fr2 = fr * fr;
+    const float A = fmaf(-fr, fmaf(fr2, fmaf(fr2, 3.0f / 16.0f, -10.0f / 16.0f), 15.0f / 16.0f), 0.5f);
+    const float w = 1.0f - fr;
+    const float w2 = w * w;
+    const float B = fmaf(w, fmaf(w2, fmaf(w2, 3.0f / 16.0f, -10.0f / 16.0f), 15.0f / 16.0f), 0.5f);
+    const float M1 = B - A, M2 = 1.0f - B;
+    const int j0 = (int)fl - 1;
+    const bool in0 = (unsigned)(j0 + 4) <= 11u;
+    const bool in1 = (unsigned)(j0 + 5) <= 11u;
+    const bool in2 = (unsigned)(j0 + 6) <= 11u;
+    const float m0 = in0 ? A : 0.0f, m1 = in1 ? M1 : 0.0f, m2 = in2 ? M2 : 0.0f;
+    const float extra = (in0 ? 0.0f : A) + (in1 ? 0.0f : M1) + (in2 ? 0.0f : M2);
+    uint64_t v = (uint64_t)pk2(m0, m1) | ((uint64_t)pk2(m2, 0.0f) << 32);
+    const uint32_t s = (uint32_t)(j0 & 3) << 4;
+    v = (v << s) | (v >> ((64u - s) & 63u));
+    lo = (uint32_t)v;
+    h2 hv = __builtin_bit_cast(h2, (uint32_t)(v >> 32));
+    hv[1] = hv[1] + (_Float16)extra;
+    hi = __builtin_bit_cast(uint32_t, hv);
+}
+
+__device__ __forceinline__ float tri_fast(float u) {
+    return fabsf(fmaf(__builtin_amdgcn_fractf(u), 2.0f, -1.0f));
+}
+
+// 40 K slots of lane half h as 20 packed f16 pairs = 5 B fragments (same slot map as encode()).
+__device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
+    uint32_t w[20];
+    const float hs = h ? 64.0f : 1.0f;
+    const float p[3] = {Q.p0 * hs, Q.p1 * hs, Q.p2 * hs};
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int k = 0; k < 6; k += 2)
+            w[(d * 6 + k) >> 1] = pk2(tri_fast(p[d] * (float)(1 << k)), tri_fast(p[d] * (float)(2 << k)));
+    blob_fast(Q.b0, w[9], w[10]);
+    blob_fast(Q.b1, w[11], w[12]);
+    blob_fast(Q.b2, w[13], w[14]);
+    w[15] = pk2(Q.i0, Q.i1);
+    w[16] = pk2(Q.i2, 1.0f);
+    w[17] = w[18] = w[19] = 0x3C003C00u;  // pad features = 1.0
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
+        x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
+__device__ __forceinline__ h8 relu_h8(const f16v& a, int base) {
+    h8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (_Float16)a[base + j];
+    const h8 z = {};
+    return __builtin_elementwise_max(r, z);
+}
+
+// Hide the LDS weight base from loop-invariant code motion so fragments are re-read per layer
+// instead of being hoisted into ~184 registers (which pins the kernel at one wave per SIMD).
+typedef __attribute__((address_space(3))) const h8 lds_h8;
+__device__ __forceinline__ lds_h8* launder(lds_h8* p) {
+    asm volatile("" : "+v"(p));
+    return p;
+}
+
+template <int TILES>
+__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][5], f16v (&o)[TILES]) {
+    h8 y[TILES][4];
+    {
+        f16v c[TILES][2];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
+        lds_h8* wl = launder(lw_lane);
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) {
+            const h8 a0 = wl[fwd_frag(0, 0, kk) * 64];
+            const h8 a1 = wl[fwd_frag(0, 1, kk) * 64];
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                c[t][0] = mfma(a0, x[t][kk], c[t][0]);
+                c[t][1] = mfma(a1, x[t][kk], c[t][1]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) {
+            y[t][0] = relu_h8(c[t][0], 0);
+            y[t][1] = relu_h8(c[t][0], 8);
+            y[t][2] = relu_h8(c[t][1], 0);
+            y[t][3] = relu_h8(c[t][1], 8);
+        }
+    }
+#pragma unroll
+    for (int l = 1; l < 5; ++l) {
+        f16v c[TILES][2];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
+        lds_h8* wl = launder(lw_lane);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const h8 a0 = wl[fwd_frag(l, 0, kk) * 64];
+            const h8 a1 = wl[fwd_frag(l, 1, kk) * 64];
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                c[t][0] = mfma(a0, y[t][kk], c[t][0]);
+                c[t][1] = mfma(a1, y[t][kk], c[t][1]);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) {
+            y[t][0] = relu_h8(c[t][0], 0);
+            y[t][1] = relu_h8(c[t][0], 8);
+            y[t][2] = relu_h8(c[t][1], 0);
+            y[t][3] = relu_h8(c[t][1], 8);
+        }
+    }
+    lds_h8* wl = launder(lw_lane);
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) o[t] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        const h8 a = wl[fwd_frag(5, 0, kk) * 64];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) o[t] = mfma(a, y[t][kk], o[t]);
+    }
+}
+
+template <int TILES, int WAVES_PER_EU>
+__global__ __launch_bounds__(kInferThreads, WAVES_PER_EU) void infer_kernel_v2(const float* __restrict__ q,
+                                                                               float* __restrict__ out, int64_t n,
+                                                                               const h8* __restrict__ wf) {
+    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    for (int i = threadIdx.x; i < kFwdFrags * 64; i += kInferThreads) lw[i] = wf[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
+    const int64_t wstride = (int64_t)gridDim.x * (kInferThreads / 64);
+    int64_t g = (int64_t)blockIdx.x * (kInferThreads / 64) + (threadIdx.x >> 6);
+    if (g >= ngroups) return;
+    const int64_t last = n - 1;
+
+    QLane Q[TILES];
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
+    for (; g < ngroups; g += wstride) {
+        h8 x[TILES][5];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) encode_fast(Q[t], h, x[t]);
+        const int64_t ng = g + wstride;
+        if (ng < ngroups) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
+        }
+        f16v o[TILES];
+        mlp_tiles<TILES>((lds_h8*)(lw + lane), x, o);
+        if (h == 0) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                const int64_t s = (g * TILES + t) * 32 + r;
+                if (s < n) {
+                    float* dst = out + s * NRC_OUTPUT_DIMS;
+                    dst[0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                    dst[1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                    dst[2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                }
+            }
+        }
+    }
+}
+
 // Standalone encoding kernel (HBM-bound; used by the parity tests of the encoding): writes the f32
 // features in canonical tcnn order, [n][80].
 __global__ void encode_kernel(const float* __restrict__ q, float* __restrict__ enc, int64_t n) {
@@ -540,25 +733,45 @@ static int num_cus() {
     return cached[dev];
 }
 
-static int infer_blocks_per_cu() {
-    static int cached = 0;
-    if (!cached) {
-        int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, infer_kernel, kInferThreads, 0) != hipSuccess || v <= 0)
-            v = 1;
-        cached = v;
+template <class K>
+static int blocks_per_cu(K kernel, int threads) {
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kernel, threads, 0) != hipSuccess || v <= 0) v = 1;
+    return v;
+}
+
+template <class K>
+static hipError_t launch_persistent_infer(K kernel, int& cache_bpc, int64_t groups, const float* queries, float* out,
+                                          int64_t n, const _Float16* wf, hipStream_t s) {
+    if (!cache_bpc) cache_bpc = blocks_per_cu(kernel, kInferThreads);
+    const int64_t want = (groups + 3) / 4;
+    const int64_t cap = (int64_t)num_cus() * cache_bpc;
+    const int grid = (int)(want < cap ? want : cap);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kInferThreads), 0, s, queries, out, n, (const h8*)wf);
+    return hipGetLastError();
+}
+
+// Inference kernel variants (A/B-able in one process through nrc_debug_infer_variant):
+//   0: v1 (weights hoisted into registers, one wave per SIMD)
+//   1: v2, 1 tile (32 queries) per wave iteration, up to 3 waves per SIMD
+//   2: v2, 2 tiles (64 queries) per wave iteration, 2 waves per SIMD
+static int g_default_infer_variant = 2;
+
+hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
+                                hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t ntiles = (n + 31) / 32;
+    static int bpc[3] = {0, 0, 0};
+    switch (variant) {
+        case 0: return launch_persistent_infer(infer_kernel, bpc[0], ntiles, queries, out, n, wf, s);
+        case 1: return launch_persistent_infer(infer_kernel_v2<1, 3>, bpc[1], ntiles, queries, out, n, wf, s);
+        case 2: return launch_persistent_infer(infer_kernel_v2<2, 2>, bpc[2], (ntiles + 1) / 2, queries, out, n, wf, s);
+        default: return hipErrorInvalidValue;
     }
-    return cached;
 }
 
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int64_t ntiles = (n + 31) / 32;
-    const int64_t want = (ntiles + 3) / 4;
-    const int64_t cap = (int64_t)num_cus() * infer_blocks_per_cu();
-    const int grid = (int)(want < cap ? want : cap);
-    hipLaunchKernelGGL(infer_kernel, dim3(grid), dim3(kInferThreads), 0, s, queries, out, n, (const h8*)wf);
-    return hipGetLastError();
+    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s);
 }
 
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s) {
@@ -593,3 +806,4 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
 }
 
 }  // namespace nrc_amd
+
