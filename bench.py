@@ -36,8 +36,8 @@ ROUND = "r01"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--queries", type=int, default=QUERIES_PER_GPU, help="queries per GPU per step")
     ap.add_argument("--train-frames", type=int, default=20, help="timed frames of 4 x 16384 training")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")

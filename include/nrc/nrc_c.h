@@ -127,6 +127,10 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
  * results are identical in meaning to nrc_infer_stream. */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
                                    hipStream_t stream);
+/* Diagnostic: the training fwd/bwd kernel with s_memtime phase stamps (16 uint64 per 128-sample block
+ * written to stamps_d); performs no optimizer step. */
+nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
+                                  uint64_t* stamps_d);
 /* the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 

@@ -549,6 +549,17 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
     });
 }
 
+nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint64_t* stamps_d) {
+    return guarded([&] {
+        check_live(net);
+        if (!in || !tgt || !stamps_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
+        const int blocks = train_blocks(b);
+        net->ensure_slabs(blocks);
+        HIP_CHECK(launch_train_stamped(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                       net->slabs, net->loss_partials, stamps_d, net->stream));
+    });
+}
+
 nrc_status nrc_encode(const float* in, float* enc, uint32_t n, hipStream_t stream) {
     return guarded([&] {
         if (n == 0) return;

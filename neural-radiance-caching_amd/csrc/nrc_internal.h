@@ -53,13 +53,17 @@ __host__ __device__ constexpr int k0_feature(int K) {
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s);
-constexpr int kNumInferVariants = 3;
+constexpr int kNumInferVariants = 14;
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,
                                 float* loss_partials, hipStream_t s);
 int train_blocks(int64_t b);
+// diagnostic: same kernel with s_memtime stamps (16 per block) — never used by the product path
+hipError_t launch_train_stamped(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                                const _Float16* wf, const _Float16* wb, float* slabs, float* loss_partials,
+                                uint64_t* stamps, hipStream_t s);
 
 enum ReduceMode { kReduceFused = 0, kReduceOnly = 1, kApplyOnly = 2, kPackOnly = 3 };
 struct OptimArgs {

@@ -164,6 +164,24 @@ __device__ __forceinline__ f16v mlp_out(const h8* __restrict__ lw, const h8 (&a5
     return o;
 }
 
+// Global -> LDS copy of a fragment image with every load in flight before the first LDS store
+// (a plain strided loop waits one round trip per iteration: ~7k cycles for 80 KiB).
+template <int THREADS, int COUNT>
+__device__ __forceinline__ void copy_to_lds(h8* __restrict__ dst, const h8* __restrict__ src) {
+    constexpr int PER = (COUNT + THREADS - 1) / THREADS;
+    h8 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + k * THREADS;
+        if (i < COUNT) v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = threadIdx.x + k * THREADS;
+        if (i < COUNT) dst[i] = v[k];
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Inference: persistent waves, 32 queries per wave-iteration.
 // ------------------------------------------------------------------------------------------------
@@ -172,7 +190,7 @@ constexpr int kInferThreads = 256;
 __global__ __launch_bounds__(kInferThreads) void infer_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                               int64_t n, const h8* __restrict__ wf) {
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
-    for (int i = threadIdx.x; i < kFwdFrags * 64; i += kInferThreads) lw[i] = wf[i];
+    copy_to_lds<kInferThreads, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -276,10 +294,12 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
     }
 }
 
+template <int ABL = 0>
 __device__ __forceinline__ h8 relu_h8(const f16v& a, int base) {
     h8 r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = (_Float16)a[base + j];
+    if (ABL & 2) return r;
     const h8 z = {};
     return __builtin_elementwise_max(r, z);
 }
@@ -292,80 +312,193 @@ __device__ __forceinline__ lds_h8* launder(lds_h8* p) {
     return p;
 }
 
-template <int TILES>
-__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][5], f16v (&o)[TILES]) {
-    h8 y[TILES][4];
-    {
-        f16v c[TILES][2];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
-        lds_h8* wl = launder(lw_lane);
-#pragma unroll
-        for (int kk = 0; kk < 5; ++kk) {
-            const h8 a0 = wl[fwd_frag(0, 0, kk) * 64];
-            const h8 a1 = wl[fwd_frag(0, 1, kk) * 64];
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) {
-                c[t][0] = mfma(a0, x[t][kk], c[t][0]);
-                c[t][1] = mfma(a1, x[t][kk], c[t][1]);
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) {
-            y[t][0] = relu_h8(c[t][0], 0);
-            y[t][1] = relu_h8(c[t][0], 8);
-            y[t][2] = relu_h8(c[t][1], 0);
-            y[t][3] = relu_h8(c[t][1], 8);
-        }
-    }
-#pragma unroll
-    for (int l = 1; l < 5; ++l) {
-        f16v c[TILES][2];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
-        lds_h8* wl = launder(lw_lane);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const h8 a0 = wl[fwd_frag(l, 0, kk) * 64];
-            const h8 a1 = wl[fwd_frag(l, 1, kk) * 64];
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) {
-                c[t][0] = mfma(a0, y[t][kk], c[t][0]);
-                c[t][1] = mfma(a1, y[t][kk], c[t][1]);
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) {
-            y[t][0] = relu_h8(c[t][0], 0);
-            y[t][1] = relu_h8(c[t][0], 8);
-            y[t][2] = relu_h8(c[t][1], 0);
-            y[t][3] = relu_h8(c[t][1], 8);
-        }
-    }
+template <int KK>
+__device__ __forceinline__ void load_frags(lds_h8* lw_lane, int layer, h8 (&a)[2][KK]) {
     lds_h8* wl = launder(lw_lane);
 #pragma unroll
-    for (int t = 0; t < TILES; ++t) o[t] = zero16();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-        const h8 a = wl[fwd_frag(5, 0, kk) * 64];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) o[t] = mfma(a, y[t][kk], o[t]);
+    for (int kk = 0; kk < KK; ++kk) {
+        a[0][kk] = wl[fwd_frag(layer, 0, kk) * 64];
+        a[1][kk] = wl[fwd_frag(layer, 1, kk) * 64];
     }
 }
 
-template <int TILES, int WAVES_PER_EU>
-__global__ __launch_bounds__(kInferThreads, WAVES_PER_EU) void infer_kernel_v2(const float* __restrict__ q,
-                                                                               float* __restrict__ out, int64_t n,
-                                                                               const h8* __restrict__ wf) {
+template <int TILES, int KK, int ABL = 0>
+__device__ __forceinline__ void layer_mfma(const h8 (&a)[2][KK], const h8 (&in)[TILES][KK], h8 (&y)[TILES][4]) {
+    f16v c[TILES][2];
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) {
+            c[t][0] = mfma(a[0][kk], in[t][kk], c[t][0]);
+            c[t][1] = mfma(a[1][kk], in[t][kk], c[t][1]);
+        }
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) {
+        y[t][0] = relu_h8<ABL>(c[t][0], 0);
+        y[t][1] = relu_h8<ABL>(c[t][0], 8);
+        y[t][2] = relu_h8<ABL>(c[t][1], 0);
+        y[t][3] = relu_h8<ABL>(c[t][1], 8);
+    }
+}
+
+// PREFETCH: issue layer l+1's weight-fragment reads before layer l's MFMAs (double-buffered
+// fragment registers) instead of at the head of layer l+1.
+template <int TILES, bool PREFETCH, int ABL = 0>
+__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][5], f16v (&o)[TILES]) {
+    h8 y[TILES][4], z[TILES][4];
+    if (PREFETCH) {
+        h8 a0[2][5];
+        load_frags<5>(lw_lane, 0, a0);
+        h8 aA[2][4], aB[2][4];
+        load_frags<4>(lw_lane, 1, aA);
+        layer_mfma<TILES, 5>(a0, x, y);
+        load_frags<4>(lw_lane, 2, aB);
+        layer_mfma<TILES, 4>(aA, y, z);
+        load_frags<4>(lw_lane, 3, aA);
+        layer_mfma<TILES, 4>(aB, z, y);
+        load_frags<4>(lw_lane, 4, aB);
+        layer_mfma<TILES, 4>(aA, y, z);
+        lds_h8* wl = launder(lw_lane);
+        h8 a5[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) a5[kk] = wl[fwd_frag(5, 0, kk) * 64];
+        layer_mfma<TILES, 4>(aB, z, y);
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) o[t] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) o[t] = mfma(a5[kk], y[t][kk], o[t]);
+    } else {
+        {
+            h8 a0[2][5];
+            load_frags<5>(lw_lane, 0, a0);
+            layer_mfma<TILES, 5, ABL>(a0, x, y);
+        }
+#pragma unroll
+        for (int l = 1; l < 5; ++l) {
+            h8 a[2][4];
+            load_frags<4>(lw_lane, l, a);
+            layer_mfma<TILES, 4, ABL>(a, y, z);
+#pragma unroll
+            for (int t = 0; t < TILES; ++t)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) y[t][kk] = z[t][kk];
+        }
+        lds_h8* wl = launder(lw_lane);
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) o[t] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const h8 a = wl[fwd_frag(5, 0, kk) * 64];
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) o[t] = mfma(a, y[t][kk], o[t]);
+        }
+    }
+}
+
+template <int TILES, int WAVES_PER_EU, int THREADS, bool PREFETCH, int ABL = 0>
+__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const float* __restrict__ q,
+                                                                         float* __restrict__ out, int64_t n,
+                                                                         const h8* __restrict__ wf) {
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
-    for (int i = threadIdx.x; i < kFwdFrags * 64; i += kInferThreads) lw[i] = wf[i];
+    copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, r = lane & 31;
     const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
-    const int64_t wstride = (int64_t)gridDim.x * (kInferThreads / 64);
-    int64_t g = (int64_t)blockIdx.x * (kInferThreads / 64) + (threadIdx.x >> 6);
+    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
+    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    if (g >= ngroups) return;
+    const int64_t last = n - 1;
+
+    QLane Q[TILES];
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
+    for (; g < ngroups; g += wstride) {
+        h8 x[TILES][5];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) {
+            if (ABL & 1) {
+                typedef float f4 __attribute__((ext_vector_type(4)));
+                const f4 a = {Q[t].p0, Q[t].p1, Q[t].b0, Q[t].b1}, b = {Q[t].b2, Q[t].i0, Q[t].i1, Q[t].i2};
+#pragma unroll
+                for (int kk = 0; kk < 5; ++kk) x[t][kk] = __builtin_bit_cast(h8, (kk & 1) ? a : b);
+            } else {
+                encode_fast(Q[t], h, x[t]);
+            }
+        }
+        const int64_t ng = g + wstride;
+        if (ng < ngroups) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
+        }
+        f16v o[TILES];
+        mlp_tiles<TILES, PREFETCH, ABL>((lds_h8*)(lw + lane), x, o);
+        if (h == 0) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                const int64_t s = (g * TILES + t) * 32 + r;
+                if (s < n) {
+                    float* dst = out + s * NRC_OUTPUT_DIMS;
+                    dst[0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                    dst[1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                    dst[2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Inference v3: weight fragments resident in registers (loaded once per wave from LDS), so the MFMA
+// stream never waits on LDS. RESIDENT = 46: every layer in registers (1 wave per SIMD, TILES
+// independent tiles interleaved for ILP); RESIDENT = 32: hidden layers 1..4 in registers, input and
+// output layers re-read from LDS (fits 2 waves per SIMD).
+// ------------------------------------------------------------------------------------------------
+template <int TILES, int KK>
+__device__ __forceinline__ void layer_regs(const h8* a0, const h8* a1, const h8 (&in)[TILES][KK],
+                                           h8 (&y)[TILES][4]) {
+    f16v c[TILES][2];
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) {
+            c[t][0] = mfma(a0[kk], in[t][kk], c[t][0]);
+            c[t][1] = mfma(a1[kk], in[t][kk], c[t][1]);
+        }
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) {
+        y[t][0] = relu_h8(c[t][0], 0);
+        y[t][1] = relu_h8(c[t][0], 8);
+        y[t][2] = relu_h8(c[t][1], 0);
+        y[t][3] = relu_h8(c[t][1], 8);
+    }
+}
+
+template <int TILES, int RESIDENT, int WAVES_PER_EU>
+__global__ __launch_bounds__(256, WAVES_PER_EU) void infer_kernel_v3(const float* __restrict__ q,
+                                                                     float* __restrict__ out, int64_t n,
+                                                                     const h8* __restrict__ wf) {
+    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    copy_to_lds<256, kFwdFrags * 64>(lw, wf);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    constexpr int F0 = RESIDENT == 46 ? 0 : 10;  // first register-resident fragment
+    h8 wr[RESIDENT];
+#pragma unroll
+    for (int f = 0; f < RESIDENT; ++f) wr[f] = lw[(F0 + f) * 64 + lane];
+
+    const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
+    const int64_t wstride = (int64_t)gridDim.x * 4;
+    int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= ngroups) return;
     const int64_t last = n - 1;
 
@@ -381,8 +514,39 @@ __global__ __launch_bounds__(kInferThreads, WAVES_PER_EU) void infer_kernel_v2(c
 #pragma unroll
             for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
         }
+        h8 y[TILES][4], z[TILES][4];
+        if (RESIDENT == 46) {
+            layer_regs<TILES, 5>(&wr[fwd_frag(0, 0, 0)], &wr[fwd_frag(0, 1, 0)], x, y);
+        } else {
+            lds_h8* wl = launder((lds_h8*)(lw + lane));
+            h8 a0[5], a1[5];
+#pragma unroll
+            for (int kk = 0; kk < 5; ++kk) {
+                a0[kk] = wl[fwd_frag(0, 0, kk) * 64];
+                a1[kk] = wl[fwd_frag(0, 1, kk) * 64];
+            }
+            layer_regs<TILES, 5>(a0, a1, x, y);
+        }
+        layer_regs<TILES, 4>(&wr[fwd_frag(1, 0, 0) - F0], &wr[fwd_frag(1, 1, 0) - F0], y, z);
+        layer_regs<TILES, 4>(&wr[fwd_frag(2, 0, 0) - F0], &wr[fwd_frag(2, 1, 0) - F0], z, y);
+        layer_regs<TILES, 4>(&wr[fwd_frag(3, 0, 0) - F0], &wr[fwd_frag(3, 1, 0) - F0], y, z);
+        layer_regs<TILES, 4>(&wr[fwd_frag(4, 0, 0) - F0], &wr[fwd_frag(4, 1, 0) - F0], z, y);
         f16v o[TILES];
-        mlp_tiles<TILES>((lds_h8*)(lw + lane), x, o);
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) o[t] = zero16();
+        h8 a5[4];
+        if (RESIDENT == 46) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) a5[kk] = wr[fwd_frag(5, 0, kk)];
+        } else {
+            lds_h8* wl = launder((lds_h8*)(lw + lane));
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) a5[kk] = wl[fwd_frag(5, 0, kk) * 64];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) o[t] = mfma(a5[kk], y[t][kk], o[t]);
         if (h == 0) {
 #pragma unroll
             for (int t = 0; t < TILES; ++t) {
@@ -536,10 +700,25 @@ __device__ __forceinline__ void bwd_chain(const h8* __restrict__ lwb, const h8 (
     mask_pack(c1, a[2], a[3], dn[2], dn[3]);
 }
 
+// STAMP (diagnostic build only): wave 0 of every block records s_memtime at phase boundaries into
+// stamps[block][16]; the product instantiation (STAMP = false) executes no stamp.
+template <bool STAMP>
 __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                        int64_t b, float n_total, float loss_scale,
                                                        const h8* __restrict__ wf, const h8* __restrict__ wb,
-                                                       float* __restrict__ slabs, float* __restrict__ loss_partials) {
+                                                       float* __restrict__ slabs, float* __restrict__ loss_partials,
+                                                       uint64_t* __restrict__ stamps) {
+    int nst = 0;
+    auto stamp = [&]() {
+        if (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t tt = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_sched_barrier(0);
+            if (threadIdx.x == 0) stamps[blockIdx.x * 16 + nst] = tt;
+            ++nst;
+        }
+    };
+    stamp();
     __shared__ __attribute__((aligned(16))) char smem[kLdsTrain];
     h8* lwf = (h8*)smem;
     h8* lwb = (h8*)(smem + kLdsWf);
@@ -548,8 +727,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     char* img_xh = img_d + kLdsImg;
     float* red = (float*)(img_xh + kLdsXhi);
 
-    for (int i = threadIdx.x; i < kFwdFrags * 64; i += 256) lwf[i] = wf[i];
-    for (int i = threadIdx.x; i < kBwdFrags * 64; i += 256) lwb[i] = wb[i];
+    copy_to_lds<256, kFwdFrags * 64>(lwf, wf);
+    copy_to_lds<256, kBwdFrags * 64>(lwb, wb);
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, r = lane & 31;
@@ -565,12 +744,32 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         tgt[2] = t[sc * 3 + 2];
     }
     h8 x[5];
-    encode(Q, h, x);
+    encode_fast(Q, h, x);
     __syncthreads();  // weights in LDS
+    stamp();
 
     h8 a[5][4];
-    mlp_hidden(lwf, x, lane, a);
+    {
+        lds_h8* wl = (lds_h8*)(lwf + lane);
+        h8 w0[2][5];
+        load_frags<5>(wl, 0, w0);
+        h8 xx[1][5] = {{x[0], x[1], x[2], x[3], x[4]}};
+        h8 yy[1][4];
+        layer_mfma<1, 5>(w0, xx, yy);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) a[0][kk] = yy[0][kk];
+#pragma unroll
+        for (int l = 1; l < 5; ++l) {
+            h8 wlay[2][4];
+            load_frags<4>(wl, l, wlay);
+            h8 in[1][4] = {{a[l - 1][0], a[l - 1][1], a[l - 1][2], a[l - 1][3]}};
+            layer_mfma<1, 4>(wlay, in, yy);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) a[l][kk] = yy[0][kk];
+        }
+    }
     const f16v o = mlp_out(lwf, a[4], lane);
+    stamp();
 
     // RelativeL2Luminance on the f16 prediction, loss-scaled f16 gradient, ReLU-masked.
     float lossv = 0.0f;
@@ -602,11 +801,13 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     write_rows64(img_a, sl, h, a[4]);
     __syncthreads();
     if (threadIdx.x == 0) loss_partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    stamp();
 
     h8 d4[4], d3[4], d2[4], d1[4], d0[4];
     // ---- layer 5
     bwd_chain<5>(lwb, g, a[4], lane, d4);
     dw_layer<5>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
     __syncthreads();
     write_rows64(img_d, sl, h, d4);
     write_rows64(img_a, sl, h, a[3]);
@@ -614,6 +815,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // ---- layer 4
     bwd_chain<4>(lwb, d4, a[3], lane, d3);
     dw_layer<4>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
     __syncthreads();
     write_rows64(img_d, sl, h, d3);
     write_rows64(img_a, sl, h, a[2]);
@@ -621,6 +823,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // ---- layer 3
     bwd_chain<3>(lwb, d3, a[2], lane, d2);
     dw_layer<3>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
     __syncthreads();
     write_rows64(img_d, sl, h, d2);
     write_rows64(img_a, sl, h, a[1]);
@@ -628,6 +831,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // ---- layer 2
     bwd_chain<2>(lwb, d2, a[1], lane, d1);
     dw_layer<2>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
     __syncthreads();
     write_rows64(img_d, sl, h, d1);
     write_rows64(img_a, sl, h, a[0]);
@@ -635,6 +839,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // ---- layer 1
     bwd_chain<1>(lwb, d1, a[0], lane, d0);
     dw_layer<1>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
     __syncthreads();
     // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a, x_hi -> img_xh)
     write_rows64(img_d, sl, h, d0);
@@ -646,17 +851,26 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     __syncthreads();
     // ---- layer 0
     dw_layer<0>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
 }
 
 // ------------------------------------------------------------------------------------------------
 // Fixed-order weight-gradient reduction + tcnn Adam + EMA + f16 fragment-image repack.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
+// Block = 64 parameters x 16 slab groups; each thread sums every 16th slab with all of its loads in
+// flight (four interleaved partial sums), the groups are combined in LDS in a fixed tree: the result is
+// bitwise reproducible for a given slab count.
+constexpr int kRedParams = 64, kRedGroups = 16, kRedThreads = kRedParams * kRedGroups;
+static_assert(NRC_NUM_PARAMS % kRedParams == 0, "parameter count must tile the reduction");
+
+__global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
                                                           const float* __restrict__ loss_partials,
                                                           float* __restrict__ grad_io, float* __restrict__ loss_out,
                                                           ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ float part[kRedGroups][kRedParams];
+    const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
+    const int p = blockIdx.x * kRedParams + pl;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
@@ -667,32 +881,38 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(int mode, const float*
             loss_out[0] = grad_io[NRC_NUM_PARAMS];
         }
     }
-    if (p >= NRC_NUM_PARAMS) return;
+    float gsum = 0.0f;
+    if (mode == kReduceFused || mode == kReduceOnly) {
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        int i = grp;
+        for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = slabs[(int64_t)(i + u * kRedGroups) * NRC_NUM_PARAMS + p];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u & 3] += v[u];
+        }
+        for (int u = 0; i < nslabs; i += kRedGroups, ++u) acc[u & 3] += slabs[(int64_t)i * NRC_NUM_PARAMS + p];
+        part[grp][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        __syncthreads();
+        if (grp != 0) return;
+        float t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][pl] + part[2 * u + 1][pl];
+        gsum = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
+        if (mode == kReduceOnly) {
+            grad_io[p] = gsum;
+            return;
+        }
+    } else {
+        if (grp != 0) return;
+        if (mode == kApplyOnly) gsum = grad_io[p];
+    }
     float w, inf;
     if (mode == kPackOnly) {
         w = mb.params[p];
         inf = mb.infer[p];
     } else {
-        float gsum;
-        if (mode == kApplyOnly) {
-            gsum = grad_io[p];
-        } else {
-            // fixed order: 4 interleaved partial sums, combined in a fixed tree
-            float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
-            int i = 0;
-            for (; i + 4 <= nslabs; i += 4) {
-                g0 += slabs[(int64_t)(i + 0) * NRC_NUM_PARAMS + p];
-                g1 += slabs[(int64_t)(i + 1) * NRC_NUM_PARAMS + p];
-                g2 += slabs[(int64_t)(i + 2) * NRC_NUM_PARAMS + p];
-                g3 += slabs[(int64_t)(i + 3) * NRC_NUM_PARAMS + p];
-            }
-            for (; i < nslabs; ++i) g0 += slabs[(int64_t)i * NRC_NUM_PARAMS + p];
-            gsum = (g0 + g1) + (g2 + g3);
-            if (mode == kReduceOnly) {
-                grad_io[p] = gsum;
-                return;
-            }
-        }
         // tcnn Adam (optimizers/adam.h); lr_t and the EMA debias come from the host in f32.
         float gradient = gsum / oa.loss_scale;
         w = mb.params[p];
@@ -741,13 +961,14 @@ static int blocks_per_cu(K kernel, int threads) {
 }
 
 template <class K>
-static hipError_t launch_persistent_infer(K kernel, int& cache_bpc, int64_t groups, const float* queries, float* out,
-                                          int64_t n, const _Float16* wf, hipStream_t s) {
-    if (!cache_bpc) cache_bpc = blocks_per_cu(kernel, kInferThreads);
-    const int64_t want = (groups + 3) / 4;
+static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc, int64_t groups, const float* queries,
+                                          float* out, int64_t n, const _Float16* wf, hipStream_t s) {
+    if (!cache_bpc) cache_bpc = blocks_per_cu(kernel, threads);
+    const int wpb = threads / 64;
+    const int64_t want = (groups + wpb - 1) / wpb;
     const int64_t cap = (int64_t)num_cus() * cache_bpc;
     const int grid = (int)(want < cap ? want : cap);
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kInferThreads), 0, s, queries, out, n, (const h8*)wf);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, queries, out, n, (const h8*)wf);
     return hipGetLastError();
 }
 
@@ -755,17 +976,35 @@ static hipError_t launch_persistent_infer(K kernel, int& cache_bpc, int64_t grou
 //   0: v1 (weights hoisted into registers, one wave per SIMD)
 //   1: v2, 1 tile (32 queries) per wave iteration, up to 3 waves per SIMD
 //   2: v2, 2 tiles (64 queries) per wave iteration, 2 waves per SIMD
+//   3: v2, 1 tile, 512-thread blocks, 4 waves per SIMD
+//   4: v2, 1 tile, next-layer fragment prefetch, 3 waves per SIMD
+//   5: v2, 1 tile, 512-thread blocks, 4 waves per SIMD, prefetch
+//   6: v2, 2 tiles, 512-thread blocks, 2 waves per SIMD, prefetch
 static int g_default_infer_variant = 2;
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
-    static int bpc[3] = {0, 0, 0};
+    static int bpc[kNumInferVariants] = {};
+    const int64_t pairs = (ntiles + 1) / 2;
     switch (variant) {
-        case 0: return launch_persistent_infer(infer_kernel, bpc[0], ntiles, queries, out, n, wf, s);
-        case 1: return launch_persistent_infer(infer_kernel_v2<1, 3>, bpc[1], ntiles, queries, out, n, wf, s);
-        case 2: return launch_persistent_infer(infer_kernel_v2<2, 2>, bpc[2], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 0: return launch_persistent_infer(infer_kernel, kInferThreads, bpc[0], ntiles, queries, out, n, wf, s);
+        case 1: return launch_persistent_infer(infer_kernel_v2<1, 3, 256, false>, 256, bpc[1], ntiles, queries, out, n, wf, s);
+        case 2: return launch_persistent_infer(infer_kernel_v2<2, 2, 256, false>, 256, bpc[2], pairs, queries, out, n, wf, s);
+        case 3: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false>, 512, bpc[3], ntiles, queries, out, n, wf, s);
+        case 4: return launch_persistent_infer(infer_kernel_v2<1, 3, 256, true>, 256, bpc[4], ntiles, queries, out, n, wf, s);
+        case 5: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, true>, 512, bpc[5], ntiles, queries, out, n, wf, s);
+        case 6: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, true>, 512, bpc[6], pairs, queries, out, n, wf, s);
+        // ablations (timing only; outputs are wrong): no encode / no ReLU max / neither
+        case 7: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 1>, 512, bpc[7], ntiles, queries, out, n, wf, s);
+        case 8: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 2>, 512, bpc[8], ntiles, queries, out, n, wf, s);
+        case 9: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 3>, 512, bpc[9], ntiles, queries, out, n, wf, s);
+        // v3: register-resident weights
+        case 10: return launch_persistent_infer(infer_kernel_v3<1, 46, 1>, 256, bpc[10], ntiles, queries, out, n, wf, s);
+        case 11: return launch_persistent_infer(infer_kernel_v3<2, 46, 1>, 256, bpc[11], pairs, queries, out, n, wf, s);
+        case 12: return launch_persistent_infer(infer_kernel_v3<1, 32, 2>, 256, bpc[12], ntiles, queries, out, n, wf, s);
+        case 13: return launch_persistent_infer(infer_kernel_v3<3, 46, 1>, 256, bpc[13], (ntiles + 2) / 3, queries, out, n, wf, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -788,8 +1027,17 @@ hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int6
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,
                                 float* loss_partials, hipStream_t s) {
     if (b <= 0) return hipSuccess;
-    hipLaunchKernelGGL(train_kernel, dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total, loss_scale,
-                       (const h8*)wf, (const h8*)wb, slabs, loss_partials);
+    hipLaunchKernelGGL(train_kernel<false>, dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
+                       loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_train_stamped(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                                const _Float16* wf, const _Float16* wb, float* slabs, float* loss_partials,
+                                uint64_t* stamps, hipStream_t s) {
+    if (b <= 0) return hipSuccess;
+    hipLaunchKernelGGL(train_kernel<true>, dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
+                       loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, stamps);
     return hipGetLastError();
 }
 
@@ -799,8 +1047,8 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
     const float step = (float)(oa.step ? oa.step : 1);
     const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
     const float ema_debias = 1.0f - powf(oa.ema_decay, step);
-    const int grid = (NRC_NUM_PARAMS + 255) / 256;
-    hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(256), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
+    const int grid = NRC_NUM_PARAMS / kRedParams;
+    hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
                        loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();
 }

@@ -149,7 +149,7 @@ def test_train_grad_parity(nrc, orc, torch, dev, net, golden, b):
     g32, _ = orc.grad(params, q_np, t_np, mode=orc.FP32)
     print(f"b={b}: grad rel vs mixed {rel(g[:nrc.NUM_PARAMS], g_ref):.2e}, vs fp32 {rel(g[:nrc.NUM_PARAMS], g32):.2e}")
     assert rel(g[:nrc.NUM_PARAMS], g_ref) <= 2e-3
-    assert abs(g[nrc.NUM_PARAMS] - loss_ref) <= 1e-4 * abs(loss_ref)
+    assert abs(g[nrc.NUM_PARAMS] - loss_ref) <= 1e-3 * abs(loss_ref)
     # padded output rows 3..15 get exactly zero data gradient
     w5 = g[21504:22528].reshape(16, 64)
     assert (w5[3:] == 0).all()
