@@ -312,8 +312,16 @@ __device__ __forceinline__ lds_h8* launder(lds_h8* p) {
     return p;
 }
 
-template <int KK>
+template <int KK, int ABL = 0>
 __device__ __forceinline__ void load_frags(lds_h8* lw_lane, int layer, h8 (&a)[2][KK]) {
+    if (ABL & 4) {
+        h8 v = {};
+        v[0] = (_Float16)(float)layer;
+        asm volatile("" : "+v"(v));
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) a[0][kk] = a[1][kk] = v;
+        return;
+    }
     lds_h8* wl = launder(lw_lane);
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
@@ -374,13 +382,13 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
     } else {
         {
             h8 a0[2][5];
-            load_frags<5>(lw_lane, 0, a0);
+            load_frags<5, ABL>(lw_lane, 0, a0);
             layer_mfma<TILES, 5, ABL>(a0, x, y);
         }
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
             h8 a[2][4];
-            load_frags<4>(lw_lane, l, a);
+            load_frags<4, ABL>(lw_lane, l, a);
             layer_mfma<TILES, 4, ABL>(a, y, z);
 #pragma unroll
             for (int t = 0; t < TILES; ++t)
@@ -560,6 +568,146 @@ __global__ __launch_bounds__(256, WAVES_PER_EU) void infer_kernel_v3(const float
             }
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Inference v4: explicit weight-fragment prefetch. Layer l+1's fragments are issued (inline-asm
+// ds_read_b128, which the scheduler cannot sink next to its consumer) before layer l's MFMAs and
+// retired by a counted s_waitcnt lgkmcnt right before layer l+1 — LDS latency hides under a whole
+// layer of MFMAs. The next tile's layer-0 fragments are issued before the output layer. The loop holds
+// no other LDS or scalar-memory traffic, so lgkmcnt counts exactly these reads (in issue order).
+// ------------------------------------------------------------------------------------------------
+template <int OFF>
+__device__ __forceinline__ void ldsrd(h8& d, uint32_t base) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(OFF * 1024));
+}
+#define NRC_RD_LAYER4(A, L)                                      \
+    ldsrd<fwd_frag(L, 0, 0)>(A[0][0], base);                      \
+    ldsrd<fwd_frag(L, 0, 1)>(A[0][1], base);                      \
+    ldsrd<fwd_frag(L, 0, 2)>(A[0][2], base);                      \
+    ldsrd<fwd_frag(L, 0, 3)>(A[0][3], base);                      \
+    ldsrd<fwd_frag(L, 1, 0)>(A[1][0], base);                      \
+    ldsrd<fwd_frag(L, 1, 1)>(A[1][1], base);                      \
+    ldsrd<fwd_frag(L, 1, 2)>(A[1][2], base);                      \
+    ldsrd<fwd_frag(L, 1, 3)>(A[1][3], base);
+#define NRC_RD_LAYER0(A)                                         \
+    ldsrd<fwd_frag(0, 0, 0)>(A[0][0], base);                      \
+    ldsrd<fwd_frag(0, 0, 1)>(A[0][1], base);                      \
+    ldsrd<fwd_frag(0, 0, 2)>(A[0][2], base);                      \
+    ldsrd<fwd_frag(0, 0, 3)>(A[0][3], base);                      \
+    ldsrd<fwd_frag(0, 0, 4)>(A[0][4], base);                      \
+    ldsrd<fwd_frag(0, 1, 0)>(A[1][0], base);                      \
+    ldsrd<fwd_frag(0, 1, 1)>(A[1][1], base);                      \
+    ldsrd<fwd_frag(0, 1, 2)>(A[1][2], base);                      \
+    ldsrd<fwd_frag(0, 1, 3)>(A[1][3], base);                      \
+    ldsrd<fwd_frag(0, 1, 4)>(A[1][4], base);
+#define NRC_RD_LAYER5(A)                                         \
+    ldsrd<fwd_frag(5, 0, 0)>(A[0], base);                         \
+    ldsrd<fwd_frag(5, 0, 1)>(A[1], base);                         \
+    ldsrd<fwd_frag(5, 0, 2)>(A[2], base);                         \
+    ldsrd<fwd_frag(5, 0, 3)>(A[3], base);
+
+// Wait until at most N LDS reads are outstanding; the "+v" ties stop the compiler from using the
+// fragments before this point, sched_barrier stops it from hoisting MFMAs above it (guide §5.4 rule 18).
+template <int N, int KK>
+__device__ __forceinline__ void lds_wait(h8 (&a)[2][KK]) {
+    if constexpr (KK == 5)
+        asm volatile("s_waitcnt lgkmcnt(%10)"
+                     : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[0][4]), "+v"(a[1][0]),
+                       "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]), "+v"(a[1][4])
+                     : "i"(N));
+    else
+        asm volatile("s_waitcnt lgkmcnt(%8)"
+                     : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]), "+v"(a[1][1]),
+                       "+v"(a[1][2]), "+v"(a[1][3])
+                     : "i"(N));
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+__device__ __forceinline__ void lds_wait5(h8 (&a)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "i"(N));
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int TILES, int THREADS, int WAVES_PER_EU>
+__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v4(const float* __restrict__ q,
+                                                                         float* __restrict__ out, int64_t n,
+                                                                         const h8* __restrict__ wf) {
+    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
+    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
+    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    if (g >= ngroups) return;
+    const int64_t last = n - 1;
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_h8*)(lw + lane);
+
+    QLane Q[TILES];
+#pragma unroll
+    for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
+    h8 w0[2][5];
+    NRC_RD_LAYER0(w0);
+    __builtin_amdgcn_sched_barrier(0);
+    for (; g < ngroups; g += wstride) {
+        h8 x[TILES][5];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) encode_fast(Q[t], h, x[t]);
+        const int64_t ng = g + wstride;
+        if (ng < ngroups) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
+        }
+        h8 wa[2][4], wb[2][4], w5[4];
+        h8 y[TILES][4], z[TILES][4];
+        __builtin_amdgcn_sched_barrier(0);
+        NRC_RD_LAYER4(wa, 1);
+        lds_wait<8>(w0);
+        layer_mfma<TILES, 5>(w0, x, y);
+        __builtin_amdgcn_sched_barrier(0);
+        NRC_RD_LAYER4(wb, 2);
+        lds_wait<8>(wa);
+        layer_mfma<TILES, 4>(wa, y, z);
+        __builtin_amdgcn_sched_barrier(0);
+        NRC_RD_LAYER4(wa, 3);
+        lds_wait<8>(wb);
+        layer_mfma<TILES, 4>(wb, z, y);
+        __builtin_amdgcn_sched_barrier(0);
+        NRC_RD_LAYER4(wb, 4);
+        lds_wait<8>(wa);
+        layer_mfma<TILES, 4>(wa, y, z);
+        __builtin_amdgcn_sched_barrier(0);
+        NRC_RD_LAYER5(w5);
+        lds_wait<4>(wb);
+        layer_mfma<TILES, 4>(wb, z, y);
+        __builtin_amdgcn_sched_barrier(0);
+        NRC_RD_LAYER0(w0);  // next tile's layer 0
+        lds_wait5<10>(w5);
+        f16v o[TILES];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) o[t] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) o[t] = mfma(w5[kk], y[t][kk], o[t]);
+        if (h == 0) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                const int64_t s = (g * TILES + t) * 32 + r;
+                if (s < n) {
+                    float* dst = out + s * NRC_OUTPUT_DIMS;
+                    dst[0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                    dst[1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                    dst[2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                }
+            }
+        }
+    }
+    // drain the speculative layer-0 reads before the wave exits
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // Standalone encoding kernel (HBM-bound; used by the parity tests of the encoding): writes the f32
@@ -1000,6 +1148,14 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 7: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 1>, 512, bpc[7], ntiles, queries, out, n, wf, s);
         case 8: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 2>, 512, bpc[8], ntiles, queries, out, n, wf, s);
         case 9: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 3>, 512, bpc[9], ntiles, queries, out, n, wf, s);
+        case 14: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 4>, 512, bpc[14], ntiles, queries, out, n, wf, s);
+        case 15: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 7>, 512, bpc[15], ntiles, queries, out, n, wf, s);
+        case 16: return launch_persistent_infer(infer_kernel_v2<2, 2, 256, false, 7>, 256, bpc[16], pairs, queries, out, n, wf, s);
+        // v4: explicit layer-ahead weight prefetch
+        case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
+        case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
+        case 19: return launch_persistent_infer(infer_kernel_v4<2, 256, 2>, 256, bpc[19], pairs, queries, out, n, wf, s);
+        case 20: return launch_persistent_infer(infer_kernel_v4<2, 512, 2>, 512, bpc[20], pairs, queries, out, n, wf, s);
         // v3: register-resident weights
         case 10: return launch_persistent_infer(infer_kernel_v3<1, 46, 1>, 256, bpc[10], ntiles, queries, out, n, wf, s);
         case 11: return launch_persistent_infer(infer_kernel_v3<2, 46, 1>, 256, bpc[11], pairs, queries, out, n, wf, s);
