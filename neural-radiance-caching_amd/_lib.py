@@ -11,7 +11,8 @@ import subprocess
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libnrc_amd.so"
+# NRC_LIB_PATH: alternate build of the same library (tuning A/B across compile flags only)
+LIB_PATH = Path(os.environ["NRC_LIB_PATH"]) if os.environ.get("NRC_LIB_PATH") else PKG_DIR / "libnrc_amd.so"
 
 NUM_PARAMS = 22528
 GRAD_FLOATS = NUM_PARAMS + 4

@@ -229,11 +229,10 @@ __global__ __launch_bounds__(kInferThreads) void infer_kernel(const float* __res
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
+typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk2(float a, float b) {
-    h2 v;
-    v[0] = (_Float16)a;
-    v[1] = (_Float16)b;
-    return __builtin_bit_cast(uint32_t, v);
+    const f2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2));  // v_cvt_pk_f16_f32 (RNE)
 }
 
 // OneBlob(4 bins) of one input in closed form. tcnn's formula sums 12 quartic-CDF terms;
@@ -270,16 +269,39 @@ __device__ __forceinline__ float tri_fast(float u) {
     return fabsf(fmaf(__builtin_amdgcn_fractf(u), 2.0f, -1.0f));
 }
 
+// 2 * frac(x) in one instruction (v_fract_f32 with the mul:2 output modifier; hipcc only folds omod when
+// f32 denormals are flushed). Non-volatile asm: freely schedulable, no hazards on VALU -> VALU.
+__device__ __forceinline__ float fract2(float x) {
+    float r;
+    asm("v_fract_f32_e64 %0, %1 mul:2" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // 40 K slots of lane half h as 20 packed f16 pairs = 5 B fragments (same slot map as encode()).
+// Triangle wave octaves by doubling: g_0 = 2 frac(u), g_{k+1} = 2 frac(g_k) = 2 frac(2^{k+1} u) (doubling
+// and frac of a value in [0, 2) are exact in f32), tri_k = |g_k - 1|.
+template <bool CHAIN = true>
 __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
     uint32_t w[20];
     const float hs = h ? 64.0f : 1.0f;
     const float p[3] = {Q.p0 * hs, Q.p1 * hs, Q.p2 * hs};
+    if (CHAIN) {
 #pragma unroll
-    for (int d = 0; d < 3; ++d)
+        for (int d = 0; d < 3; ++d) {
+            float g[6];
+            g[0] = fract2(p[d]);
 #pragma unroll
-        for (int k = 0; k < 6; k += 2)
-            w[(d * 6 + k) >> 1] = pk2(tri_fast(p[d] * (float)(1 << k)), tri_fast(p[d] * (float)(2 << k)));
+            for (int k = 1; k < 6; ++k) g[k] = fract2(g[k - 1]);
+#pragma unroll
+            for (int k = 0; k < 6; k += 2) w[(d * 6 + k) >> 1] = pk2(fabsf(g[k] - 1.0f), fabsf(g[k + 1] - 1.0f));
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int k = 0; k < 6; k += 2)
+                w[(d * 6 + k) >> 1] = pk2(tri_fast(p[d] * (float)(1 << k)), tri_fast(p[d] * (float)(2 << k)));
+    }
     blob_fast(Q.b0, w[9], w[10]);
     blob_fast(Q.b1, w[11], w[12]);
     blob_fast(Q.b2, w[13], w[14]);
@@ -1128,7 +1150,7 @@ static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc,
 //   4: v2, 1 tile, next-layer fragment prefetch, 3 waves per SIMD
 //   5: v2, 1 tile, 512-thread blocks, 4 waves per SIMD, prefetch
 //   6: v2, 2 tiles, 512-thread blocks, 2 waves per SIMD, prefetch
-static int g_default_infer_variant = 2;
+static int g_default_infer_variant = 3;
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s) {
