@@ -133,6 +133,8 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const flo
                                   uint64_t* stamps_d);
 /* the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
+/* the encoder the MLP kernels actually run (closed-form OneBlob, f16-rounded), same output format */
+nrc_status nrc_debug_encode_fast(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 
 #ifdef __cplusplus
 }

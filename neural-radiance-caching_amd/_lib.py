@@ -32,7 +32,7 @@ EXPORTS = [
     "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_get_state", "nrc_set_state", "nrc_get_step", "nrc_set_step",
-    "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps",
+    "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_encode_fast",
 ]
 
 
@@ -97,6 +97,7 @@ def lib() -> ctypes.CDLL:
         "nrc_encode": (st, [fp, fp, u32, vp]),
         "nrc_debug_infer_variant": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_train_stamps": (st, [vp, fp, fp, u32, vp]),
+        "nrc_debug_encode_fast": (st, [fp, fp, u32, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

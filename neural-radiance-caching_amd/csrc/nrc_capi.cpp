@@ -568,4 +568,12 @@ nrc_status nrc_encode(const float* in, float* enc, uint32_t n, hipStream_t strea
     });
 }
 
+nrc_status nrc_debug_encode_fast(const float* in, float* enc, uint32_t n, hipStream_t stream) {
+    return guarded([&] {
+        if (n == 0) return;
+        if (!in || !enc) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
+        HIP_CHECK(launch_encode_fast(in, enc, n, stream));
+    });
+}
+
 }  // extern "C"

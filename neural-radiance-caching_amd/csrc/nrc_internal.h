@@ -55,6 +55,7 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
                                 hipStream_t s);
 constexpr int kNumInferVariants = 21;
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
+hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,

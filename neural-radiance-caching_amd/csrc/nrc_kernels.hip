@@ -269,8 +269,7 @@ __device__ __forceinline__ float tri_fast(float u) {
     return fabsf(fmaf(__builtin_amdgcn_fractf(u), 2.0f, -1.0f));
 }
 
-// 2 * frac(x) in one instruction (v_fract_f32 with the mul:2 output modifier; hipcc only folds omod when
-// f32 denormals are flushed). Non-volatile asm: freely schedulable, no hazards on VALU -> VALU.
+// 2 * frac(x) via v_fract_f32's mul:2 output modifier — does NOT give 2*frac(x) on gfx950 (see CHAIN).
 __device__ __forceinline__ float fract2(float x) {
     float r;
     asm("v_fract_f32_e64 %0, %1 mul:2" : "=v"(r) : "v"(x));
@@ -278,9 +277,9 @@ __device__ __forceinline__ float fract2(float x) {
 }
 
 // 40 K slots of lane half h as 20 packed f16 pairs = 5 B fragments (same slot map as encode()).
-// Triangle wave octaves by doubling: g_0 = 2 frac(u), g_{k+1} = 2 frac(g_k) = 2 frac(2^{k+1} u) (doubling
-// and frac of a value in [0, 2) are exact in f32), tri_k = |g_k - 1|.
-template <bool CHAIN = true>
+// CHAIN (experimental, off): triangle-wave octaves by doubling through v_fract's mul:2 output modifier —
+// wrong on gfx950 hardware (caught by test_encode_fast_parity); the direct form is used.
+template <bool CHAIN = false>
 __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
     uint32_t w[20];
     const float hs = h ? 64.0f : 1.0f;
@@ -746,6 +745,27 @@ __global__ void encode_kernel(const float* __restrict__ q, float* __restrict__ e
     for (int k = 0; k < 40; ++k) enc[s * NRC_ENC_WIDTH + slot_feature(k, h)] = v[k];
 }
 
+// The production encoder (encode_fast: f16 B fragments) unpacked to canonical order as f32 — lets the
+// parity tests check the exact code path the MLP kernels run.
+__global__ void encode_fast_kernel(const float* __restrict__ q, float* __restrict__ enc, int64_t n) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = gid >> 1;
+    const int h = (int)(gid & 1);
+    if (s >= n) return;
+    const QLane Q = load_q(q, s, h);
+    h8 x[5];
+    encode_fast(Q, h, x);
+#pragma unroll
+    for (int k = 0; k < 40; ++k) enc[s * NRC_ENC_WIDTH + slot_feature(k, h)] = (float)x[k >> 3][k & 7];
+}
+
+hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int grid = (int)((2 * n + 255) / 256);
+    hipLaunchKernelGGL(encode_fast_kernel, dim3(grid), dim3(256), 0, s, queries, enc, n);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Training: one block = 4 waves = 128 samples.
 // ------------------------------------------------------------------------------------------------
@@ -804,7 +824,7 @@ constexpr int kLdsWf = kFwdHalves * 2;   // 47104
 constexpr int kLdsWb = kBwdHalves * 2;   // 34816
 constexpr int kLdsImg = 128 * 128;       // 16384
 constexpr int kLdsXhi = 128 * 32;        // 4096
-constexpr int kLdsTrain = kLdsWf + kLdsWb + 2 * kLdsImg + kLdsXhi + 16;
+constexpr int kLdsTrain = kLdsWf + kLdsWb + 4 * kLdsImg + kLdsXhi + 16;
 
 // dW output block (mb, nb) of layer L: A = delta image (features = output rows), B = activation image.
 template <int L>
@@ -892,13 +912,25 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     __shared__ __attribute__((aligned(16))) char smem[kLdsTrain];
     h8* lwf = (h8*)smem;
     h8* lwb = (h8*)(smem + kLdsWf);
-    char* img_a = smem + kLdsWf + kLdsWb;
-    char* img_d = img_a + kLdsImg;
-    char* img_xh = img_d + kLdsImg;
+    // double-buffered [sample][feature] images: buffer p holds (delta_l, a_l) for layers l with l & 1 == p
+    char* img_a[2] = {smem + kLdsWf + kLdsWb, smem + kLdsWf + kLdsWb + kLdsImg};
+    char* img_d[2] = {smem + kLdsWf + kLdsWb + 2 * kLdsImg, smem + kLdsWf + kLdsWb + 3 * kLdsImg};
+    char* img_xh = smem + kLdsWf + kLdsWb + 4 * kLdsImg;
     float* red = (float*)(img_xh + kLdsXhi);
 
-    copy_to_lds<256, kFwdFrags * 64>(lwf, wf);
-    copy_to_lds<256, kBwdFrags * 64>(lwb, wb);
+    // weight images: issue every global load first, encode while they fly, then store to LDS
+    constexpr int PF = (kFwdFrags * 64 + 255) / 256, PB = (kBwdFrags * 64 + 255) / 256;
+    h8 vf[PF], vb[PB];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < kFwdFrags * 64) vf[k] = wf[i];
+    }
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < kBwdFrags * 64) vb[k] = wb[i];
+    }
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, r = lane & 31;
@@ -915,6 +947,16 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     }
     h8 x[5];
     encode_fast(Q, h, x);
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < kFwdFrags * 64) lwf[i] = vf[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < kBwdFrags * 64) lwb[i] = vb[k];
+    }
     __syncthreads();  // weights in LDS
     stamp();
 
@@ -965,62 +1007,53 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 
     float* slab = slabs + (int64_t)blockIdx.x * NRC_NUM_PARAMS;
 
-    // images for layer 5: delta_5 = g (16 rows, k-step 0 only), a_5
+    // layer 5 operands (buffer 1): delta_5 = g (16 rows, k-step 0 only), a_5
 #pragma unroll
-    for (int jg = 0; jg < 2; ++jg) store_h4(img_d, img_off(sl, acc_row(0, h, 4 * jg)), g[0], 4 * jg);
-    write_rows64(img_a, sl, h, a[4]);
+    for (int jg = 0; jg < 2; ++jg) store_h4(img_d[1], img_off(sl, acc_row(0, h, 4 * jg)), g[0], 4 * jg);
+    write_rows64(img_a[1], sl, h, a[4]);
     __syncthreads();
     if (threadIdx.x == 0) loss_partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
     stamp();
 
+    // One barrier per layer: step l reads buffer l&1 and writes layer l-1's operands into the other
+    // buffer, whose previous readers (step l+1) all passed the barrier that ended step l+1.
     h8 d4[4], d3[4], d2[4], d1[4], d0[4];
-    // ---- layer 5
     bwd_chain<5>(lwb, g, a[4], lane, d4);
-    dw_layer<5>(img_d, img_a, img_xh, wave, lane, slab);
+    write_rows64(img_d[0], sl, h, d4);
+    write_rows64(img_a[0], sl, h, a[3]);
+    dw_layer<5>(img_d[1], img_a[1], img_xh, wave, lane, slab);
+    __syncthreads();
     stamp();
-    __syncthreads();
-    write_rows64(img_d, sl, h, d4);
-    write_rows64(img_a, sl, h, a[3]);
-    __syncthreads();
-    // ---- layer 4
     bwd_chain<4>(lwb, d4, a[3], lane, d3);
-    dw_layer<4>(img_d, img_a, img_xh, wave, lane, slab);
+    write_rows64(img_d[1], sl, h, d3);
+    write_rows64(img_a[1], sl, h, a[2]);
+    dw_layer<4>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    __syncthreads();
     stamp();
-    __syncthreads();
-    write_rows64(img_d, sl, h, d3);
-    write_rows64(img_a, sl, h, a[2]);
-    __syncthreads();
-    // ---- layer 3
     bwd_chain<3>(lwb, d3, a[2], lane, d2);
-    dw_layer<3>(img_d, img_a, img_xh, wave, lane, slab);
+    write_rows64(img_d[0], sl, h, d2);
+    write_rows64(img_a[0], sl, h, a[1]);
+    dw_layer<3>(img_d[1], img_a[1], img_xh, wave, lane, slab);
+    __syncthreads();
     stamp();
-    __syncthreads();
-    write_rows64(img_d, sl, h, d2);
-    write_rows64(img_a, sl, h, a[1]);
-    __syncthreads();
-    // ---- layer 2
     bwd_chain<2>(lwb, d2, a[1], lane, d1);
-    dw_layer<2>(img_d, img_a, img_xh, wave, lane, slab);
+    write_rows64(img_d[1], sl, h, d1);
+    write_rows64(img_a[1], sl, h, a[0]);
+    dw_layer<2>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    __syncthreads();
     stamp();
-    __syncthreads();
-    write_rows64(img_d, sl, h, d1);
-    write_rows64(img_a, sl, h, a[0]);
-    __syncthreads();
-    // ---- layer 1
     bwd_chain<1>(lwb, d1, a[0], lane, d0);
-    dw_layer<1>(img_d, img_a, img_xh, wave, lane, slab);
-    stamp();
-    __syncthreads();
-    // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a, x_hi -> img_xh)
-    write_rows64(img_d, sl, h, d0);
+    // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a[0], x_hi -> img_xh)
+    write_rows64(img_d[0], sl, h, d0);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int jg = 0; jg < 2; ++jg) store_h4(img_a, img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
+        for (int jg = 0; jg < 2; ++jg) store_h4(img_a[0], img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
     *(h8*)(img_xh + sl * 32 + 16 * h) = x[4];
+    dw_layer<1>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     __syncthreads();
-    // ---- layer 0
-    dw_layer<0>(img_d, img_a, img_xh, wave, lane, slab);
+    stamp();
+    dw_layer<0>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     stamp();
 }
 

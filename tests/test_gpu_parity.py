@@ -67,6 +67,48 @@ def test_encode_parity(nrc, orc, torch, dev, golden):
         np.testing.assert_allclose(enc.cpu().numpy(), orc.encode(q_np), rtol=0, atol=4e-6)
 
 
+def test_encode_fast_parity(nrc, orc, torch, dev, golden):
+    """The encoder inside the MLP kernels (closed-form OneBlob, doubling-chain triangle wave, f16
+    packing) against the oracle's tcnn-literal encoding rounded to f16: every feature of every query
+    within one f16 ulp (plus 2e-6 absolute for the f32 evaluation-order differences)."""
+    L = nrc._lib.lib()
+    for q_np in [golden["queries"], golden["queries_edge"], nrc.synthetic.cornell_queries(20000, seed=22)]:
+        n = q_np.shape[0]
+        enc = torch.zeros((n, 80), dtype=torch.float32, device=dev)
+        nrc._lib.check(L.nrc_debug_encode_fast(to_dev(torch, dev, q_np).data_ptr(), enc.data_ptr(), n, None))
+        torch.cuda.synchronize()
+        ref = orc.encode(q_np).astype(np.float16).astype(np.float32)
+        got = enc.cpu().numpy()
+        tol = np.abs(ref) * 2.0 ** -10 + 2e-6
+        bad = np.argwhere(np.abs(got - ref) > tol)
+        assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
+
+
+@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20])
+def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
+    """Per-query max error (not an aggregate) for every production-eligible kernel variant at sizes
+    that exercise partial tiles / single blocks."""
+    net.set_state(nrc.StateSlot.INFER, golden["params_b"])
+    L = nrc._lib.lib()
+    for n in [1, 33, 1000, 70001]:
+        q_np = nrc.synthetic.cornell_queries(n, seed=700 + n)
+        out = torch.full((n + 8, 3), 777.0, device=dev)
+        nrc._lib.check(L.nrc_debug_infer_variant(net._h, variant, to_dev(torch, dev, q_np).data_ptr(), out.data_ptr(),
+                                                 n, int(torch.cuda.current_stream().cuda_stream)))
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        assert (o[n:] == 777.0).all()
+        y_ref = orc.forward(golden["params_b"], q_np, orc.MIXED)
+        err = np.abs(o[:n] - y_ref).max(axis=1)
+        # The encoding amplifies tiny differences (d tri / dx reaches 2 * 2^11): in the oracle itself a 1e-6
+        # position change moves 1.7 % of these queries by > 16 output ulps. Bound: at most 0.1 % of the
+        # queries beyond 16 ulps of their scale (a wrong query or tile fails it), rel-L2 <= 1e-3 overall.
+        tol = 16.0 * 2.0 ** -11 * np.maximum(np.abs(y_ref).max(axis=1), 1e-2)
+        bad = np.flatnonzero(err > tol)
+        assert bad.size <= 0.001 * n, f"variant {variant} n={n}: {bad.size} queries off, e.g. {bad[:5]} {o[bad[:2]]} vs {y_ref[bad[:2]]}"
+        assert rel(o[:n], y_ref) <= 1e-3
+
+
 @pytest.mark.parametrize("n", [1, 2, 31, 32, 33, 127, 1000, 4096, 65537])
 def test_infer_parity_sizes(nrc, orc, torch, dev, net, golden, n):
     params = golden["params_b"]
