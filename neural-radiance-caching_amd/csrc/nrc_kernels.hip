@@ -820,6 +820,14 @@ __device__ __forceinline__ void write_rows64(char* img, int sl, int h, const h8 
         for (int jg = 0; jg < 2; ++jg) store_h4(img, img_off(sl, acc_row(kk, h, 4 * jg)), f[kk], 4 * jg);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt) but not for its
+// outstanding global stores (the weight-gradient slab writes drain in the background) — __syncthreads()
+// would emit s_waitcnt vmcnt(0) first. The asm "memory" clobber keeps the compiler's memory ops on
+// their side of the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 constexpr int kLdsWf = kFwdHalves * 2;   // 47104
 constexpr int kLdsWb = kBwdHalves * 2;   // 34816
 constexpr int kLdsImg = 128 * 128;       // 16384
@@ -858,7 +866,7 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
     for (int reg = 0; reg < 16; ++reg) {
         const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         if (L == 5 && row >= NRC_OUT_PADDED) continue;
-        slab[off + row * in_dim + fcol] = acc[reg];
+        __builtin_nontemporal_store(acc[reg], &slab[off + row * in_dim + fcol]);  // streamed, read once
     }
 }
 
@@ -957,7 +965,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         const int i = threadIdx.x + k * 256;
         if (i < kBwdFrags * 64) lwb[i] = vb[k];
     }
-    __syncthreads();  // weights in LDS
+    lds_barrier();  // weights in LDS
     stamp();
 
     h8 a[5][4];
@@ -1011,7 +1019,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 #pragma unroll
     for (int jg = 0; jg < 2; ++jg) store_h4(img_d[1], img_off(sl, acc_row(0, h, 4 * jg)), g[0], 4 * jg);
     write_rows64(img_a[1], sl, h, a[4]);
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) loss_partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
     stamp();
 
@@ -1022,25 +1030,25 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     write_rows64(img_d[0], sl, h, d4);
     write_rows64(img_a[0], sl, h, a[3]);
     dw_layer<5>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    __syncthreads();
+    lds_barrier();
     stamp();
     bwd_chain<4>(lwb, d4, a[3], lane, d3);
     write_rows64(img_d[1], sl, h, d3);
     write_rows64(img_a[1], sl, h, a[2]);
     dw_layer<4>(img_d[0], img_a[0], img_xh, wave, lane, slab);
-    __syncthreads();
+    lds_barrier();
     stamp();
     bwd_chain<3>(lwb, d3, a[2], lane, d2);
     write_rows64(img_d[0], sl, h, d2);
     write_rows64(img_a[0], sl, h, a[1]);
     dw_layer<3>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    __syncthreads();
+    lds_barrier();
     stamp();
     bwd_chain<2>(lwb, d2, a[1], lane, d1);
     write_rows64(img_d[1], sl, h, d1);
     write_rows64(img_a[1], sl, h, a[0]);
     dw_layer<2>(img_d[0], img_a[0], img_xh, wave, lane, slab);
-    __syncthreads();
+    lds_barrier();
     stamp();
     bwd_chain<1>(lwb, d1, a[0], lane, d0);
     // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a[0], x_hi -> img_xh)
@@ -1051,7 +1059,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         for (int jg = 0; jg < 2; ++jg) store_h4(img_a[0], img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
     *(h8*)(img_xh + sl * 32 + 16 * h) = x[4];
     dw_layer<1>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    __syncthreads();
+    lds_barrier();
     stamp();
     dw_layer<0>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     stamp();
@@ -1064,53 +1072,12 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 // flight (four interleaved partial sums), the groups are combined in LDS in a fixed tree: the result is
 // bitwise reproducible for a given slab count.
 constexpr int kRedParams = 64, kRedGroups = 16, kRedThreads = kRedParams * kRedGroups;
-static_assert(NRC_NUM_PARAMS % kRedParams == 0, "parameter count must tile the reduction");
+constexpr int kRedVec = 4;  // floats per thread: one 16-byte load per slab
+static_assert(NRC_NUM_PARAMS % (kRedParams * 4) == 0, "parameter count must tile the reduction");
 
-__global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
-                                                          const float* __restrict__ loss_partials,
-                                                          float* __restrict__ grad_io, float* __restrict__ loss_out,
-                                                          ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+__device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const ModelBuffers& mb, const OptimArgs& oa,
+                                              float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
-    __shared__ float part[kRedGroups][kRedParams];
-    const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
-    const int p = blockIdx.x * kRedParams + pl;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (mode == kReduceFused || mode == kReduceOnly) {
-            float L = 0.0f;
-            for (int i = 0; i < nslabs; ++i) L += loss_partials[i];
-            if (mode == kReduceOnly) grad_io[NRC_NUM_PARAMS] = L;
-            else if (loss_out) loss_out[0] = L;
-        } else if (mode == kApplyOnly && loss_out) {
-            loss_out[0] = grad_io[NRC_NUM_PARAMS];
-        }
-    }
-    float gsum = 0.0f;
-    if (mode == kReduceFused || mode == kReduceOnly) {
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        int i = grp;
-        for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = slabs[(int64_t)(i + u * kRedGroups) * NRC_NUM_PARAMS + p];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u & 3] += v[u];
-        }
-        for (int u = 0; i < nslabs; i += kRedGroups, ++u) acc[u & 3] += slabs[(int64_t)i * NRC_NUM_PARAMS + p];
-        part[grp][pl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-        __syncthreads();
-        if (grp != 0) return;
-        float t8[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][pl] + part[2 * u + 1][pl];
-        gsum = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
-        if (mode == kReduceOnly) {
-            grad_io[p] = gsum;
-            return;
-        }
-    } else {
-        if (grp != 0) return;
-        if (mode == kApplyOnly) gsum = grad_io[p];
-    }
     float w, inf;
     if (mode == kPackOnly) {
         w = mb.params[p];
@@ -1138,6 +1105,69 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
     mb.wf_infer[fp] = (_Float16)inf;
     const int bp = mb.bwd_pos[p];
     if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
+}
+
+// Block = 256 parameters (64 lanes x float4) x 16 slab groups; each thread sums every 16th slab with
+// all of its 16-byte loads in flight (two interleaved partial sums), the groups are combined in LDS in
+// a fixed tree: bitwise reproducible for a given slab count.
+__global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
+                                                          const float* __restrict__ loss_partials,
+                                                          float* __restrict__ grad_io, float* __restrict__ loss_out,
+                                                          ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+#pragma clang fp contract(off)
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ f4 part[kRedGroups][kRedParams];
+    const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
+    const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (mode == kReduceFused || mode == kReduceOnly) {
+            float L = 0.0f;
+            for (int i = 0; i < nslabs; ++i) L += loss_partials[i];
+            if (mode == kReduceOnly) grad_io[NRC_NUM_PARAMS] = L;
+            else if (loss_out) loss_out[0] = L;
+        } else if (mode == kApplyOnly && loss_out) {
+            loss_out[0] = grad_io[NRC_NUM_PARAMS];
+        }
+    }
+    if (mode == kReduceFused || mode == kReduceOnly) {
+        f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        int i = grp;
+        for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
+            f4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v[u] = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)(i + u * kRedGroups) * NRC_NUM_PARAMS + p0]);
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                a0 += v[u];
+                a1 += v[u + 1];
+            }
+        }
+        for (int u = 0; i < nslabs; i += kRedGroups, ++u) {
+            const f4 v = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)i * NRC_NUM_PARAMS + p0]);
+            if (u & 1) a1 += v;
+            else a0 += v;
+        }
+        part[grp][pl] = a0 + a1;
+        __syncthreads();
+        // one parameter per thread for the combine + Adam (threads 0..255 of the block)
+        if (threadIdx.x >= kRedParams * kRedVec) return;
+        const int lp = threadIdx.x / kRedVec, comp = threadIdx.x % kRedVec;
+        float t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][lp][comp] + part[2 * u + 1][lp][comp];
+        const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
+        const int p = blockIdx.x * kRedParams * kRedVec + threadIdx.x;
+        if (mode == kReduceOnly) {
+            grad_io[p] = g1;
+            return;
+        }
+        adam_pack_one(mode, p, g1, mb, oa, lr_t, ema_debias);
+        return;
+    }
+    if (threadIdx.x >= kRedParams * kRedVec) return;
+    const int p = blockIdx.x * kRedParams * kRedVec + threadIdx.x;
+    adam_pack_one(mode, p, mode == kApplyOnly ? grad_io[p] : 0.0f, mb, oa, lr_t, ema_debias);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1258,7 +1288,7 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
     const float step = (float)(oa.step ? oa.step : 1);
     const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
     const float ema_debias = 1.0f - powf(oa.ema_decay, step);
-    const int grid = NRC_NUM_PARAMS / kRedParams;
+    const int grid = NRC_NUM_PARAMS / (kRedParams * kRedVec);
     hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
                        loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();
