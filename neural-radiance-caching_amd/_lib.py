@@ -26,13 +26,16 @@ STATUS_NAMES = {
     4: "NRC_ERR_HIP", 5: "NRC_ERR_UNSUPPORTED", 6: "NRC_ERR_OUT_OF_MEMORY", 7: "NRC_ERR_INTERNAL",
 }
 
-# Every symbol include/nrc/nrc_c.h declares (checked by tests/test_abi.py).
+# Every symbol include/nrc/*.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "nrc_version", "nrc_last_error", "nrc_default_config", "nrc_create", "nrc_free", "nrc_init", "nrc_destroy",
     "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_get_state", "nrc_set_state", "nrc_get_step", "nrc_set_step",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_encode_fast",
+    # include/nrc/frame.h (bound in frame.py)
+    "nrc_accumulate_render_radiance", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
+    "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame",
 ]
 
 

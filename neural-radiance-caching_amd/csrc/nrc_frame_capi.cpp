@@ -1,0 +1,157 @@
+// nrc_frame_capi.cpp — C-ABI of the per-frame steps around the network (include/nrc/frame.h) and the
+// frame driver nrc_process_frame, which replays Device::render's post-trace NRC sequence
+// (/root/reference/nrc/src/Device.cpp:2493-2515) on the handle's stream.
+#include <algorithm>
+#include <cstdint>
+
+#include "nrc/frame.h"
+#include "nrc_guard.h"
+#include "nrc_internal.h"
+
+using namespace nrc_amd;
+
+namespace {
+
+void require(bool ok, const char* msg) {
+    if (!ok) throw ApiError(NRC_ERR_INVALID_ARGUMENT, msg);
+}
+
+void check(nrc_status st) {
+    if (st != NRC_OK) throw ApiError(st, nrc_last_error());
+}
+
+bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+float accumulation_weight(uint32_t iteration_index) {
+    return 1.0f / (float)(iteration_index + 1u);  // nrc_helpers.cu:98
+}
+
+bool valid_mode(int mode) { return mode >= NRC_RENDER_FULL && mode <= NRC_RENDER_DEBUG_THROUGHPUT_ONLY; }
+
+constexpr uint32_t kMaxPermute = 1u << 26;  // 18 dwords per record stay inside a 32-bit grid index
+
+}  // namespace
+
+extern "C" {
+
+nrc_status nrc_accumulate_render_radiance(const nrc_float3* rad, const nrc_float3* thr, float* rgba, uint32_t n,
+                                          int mode, uint32_t iteration_index, hipStream_t stream) {
+    return guarded([&] {
+        require(valid_mode(mode), "unknown render mode");
+        if (n == 0 || mode == NRC_RENDER_NO_CACHE || mode == NRC_RENDER_CACHE_FIRST_VERTEX) return;
+        require(rgba && aligned(rgba, 16), "output_rgba must be a 16-byte aligned float4 buffer");
+        require(mode == NRC_RENDER_DEBUG_THROUGHPUT_ONLY || rad, "radiance buffer is NULL");
+        require(mode == NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION || thr, "throughput buffer is NULL");
+        require(aligned(rad, 4) && aligned(thr, 4), "float3 buffers must be 4-byte aligned");
+        HIP_CHECK(launch_accumulate(reinterpret_cast<const float*>(rad), reinterpret_cast<const float*>(thr), rgba, n,
+                                    mode, accumulation_weight(iteration_index), stream));
+    });
+}
+
+nrc_status nrc_copy_radiance_to_output(const nrc_float3* rad, float* rgba, uint32_t n, hipStream_t stream) {
+    return nrc_accumulate_render_radiance(rad, nullptr, rgba, n, NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0,
+                                          stream);
+}
+
+nrc_status nrc_propagate_train_radiance(const nrc_train_suffix_end_vertex* ends, const nrc_float3* end_rad,
+                                        uint32_t tiles, const nrc_training_record* records, nrc_float3* targets,
+                                        uint32_t nrec, hipStream_t stream) {
+    return guarded([&] {
+        if (tiles == 0 || nrec == 0) return;
+        require(ends && end_rad && records && targets, "NULL buffer");
+        require(aligned(ends, 4) && aligned(end_rad, 4) && aligned(records, 4) && aligned(targets, 4),
+                "buffers must be 4-byte aligned");
+        require(nrec <= (uint32_t)INT32_MAX, "num_records too large");
+        HIP_CHECK(launch_propagate(ends, reinterpret_cast<const float*>(end_rad), tiles, records,
+                                   reinterpret_cast<float*>(targets), nrec, stream));
+    });
+}
+
+nrc_status nrc_generate_train_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n,
+                                          hipStream_t stream) {
+    return guarded([&] {
+        if (n == 0) return;
+        require(perm != nullptr && aligned(perm, 4), "permutation buffer must be non-NULL and 4-byte aligned");
+        require(n <= (1u << 30), "n must be <= 2^30");
+        HIP_CHECK(launch_permutation(seed, frame, perm, n, stream));
+    });
+}
+
+nrc_status nrc_permute_train_data(const float* qs, const nrc_float3* ts, const int32_t* perm, uint64_t seed,
+                                  uint32_t frame, int32_t num_records, float* qd, nrc_float3* td, uint32_t n_out,
+                                  hipStream_t stream) {
+    return guarded([&] {
+        const uint32_t nrec = (uint32_t)std::min<int64_t>(num_records, (int64_t)n_out);  // nrc_helpers.cu:236
+        if (num_records <= 0 || n_out == 0) return;                                      // :237
+        require(n_out <= kMaxPermute, "n_out must be <= 2^26");
+        require(qs && ts && qd && td, "NULL buffer");
+        require(aligned(qs, 4) && aligned(ts, 4) && aligned(qd, 4) && aligned(td, 4) && aligned(perm, 4),
+                "buffers must be 4-byte aligned");
+        HIP_CHECK(launch_permute(qs, reinterpret_cast<const float*>(ts), perm, seed, frame, nrec, qd,
+                                 reinterpret_cast<float*>(td), n_out, stream));
+    });
+}
+
+nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_params* p, float* loss_h) {
+    return guarded([&] {
+        require(net && fb && p, "NULL argument");
+        require(valid_mode(p->render_mode), "unknown render mode");
+        hipStream_t s = nullptr;
+        check(nrc_get_stream(net, &s));
+        if (loss_h) *loss_h = 0.0f;
+        const uint32_t screen = p->screen_size, tiles = p->num_tiles;
+        const int mode = p->render_mode;
+
+        // Device::nrcInferRadiance (Device.cpp:1272-1301): render queries are skipped for NoCache / CacheFirstVertex
+        const bool skip_render = mode == NRC_RENDER_NO_CACHE || mode == NRC_RENDER_CACHE_FIRST_VERTEX;
+        const float* q = fb->queries_inference_d;
+        nrc_float3* r = fb->results_inference_d;
+        uint64_t nq = (uint64_t)screen + tiles;
+        if (skip_render) {
+            q += (size_t)screen * NRC_INPUT_DIMS;
+            r += screen;
+            nq = tiles;
+        }
+        require(nq <= UINT32_MAX, "screen_size + num_tiles overflows");
+        if (nq > 0) {
+            require(fb->queries_inference_d && fb->results_inference_d, "inference buffers are NULL");
+            check(nrc_infer_stream(net, q, reinterpret_cast<float*>(r), (uint32_t)nq, s));
+        }
+        // Device::nrcAccumulateRadiance (Device.cpp:1310-1337)
+        if (!skip_render)
+            check(nrc_accumulate_render_radiance(fb->results_inference_d, fb->last_render_throughput_d,
+                                                 fb->output_rgba_d, screen, mode, p->iteration_index, s));
+        // Device::nrcVisualizeFirstRadiance (Device.cpp:1339-1370)
+        if (mode == NRC_RENDER_CACHE_FIRST_VERTEX && screen > 0) {
+            require(fb->queries_cache_vis_d && fb->results_cache_vis_d, "cache-vis buffers are NULL");
+            check(nrc_infer_stream(net, fb->queries_cache_vis_d, reinterpret_cast<float*>(fb->results_cache_vis_d),
+                                   screen, s));
+            check(nrc_copy_radiance_to_output(fb->results_cache_vis_d, fb->output_rgba_d, screen, s));
+        }
+
+        // Training (Device.cpp:2505-2512): only when the trace produced records
+        const int32_t nrec = std::min(p->num_training_records, (int32_t)NRC_NUM_TRAINING_RECORDS_PER_FRAME);
+        if (!p->train || nrec <= 0) return;
+        require(fb->train_queries_d[0] && fb->train_queries_d[1] && fb->train_targets_d[0] && fb->train_targets_d[1],
+                "training double buffers are NULL");
+        // Device::nrcPropagateRadiance (Device.cpp:1382-1419): end radiance = results after the render part
+        check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
+                                           fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
+        // Device::nrcShuffleTrainingData (Device.cpp:1427-1469)
+        check(nrc_permute_train_data(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d,
+                                     p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],
+                                     fb->train_targets_d[1], NRC_NUM_TRAINING_RECORDS_PER_FRAME, s));
+        // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss
+        float total = 0.0f;
+        for (int b = 0; b < NRC_NUM_BATCHES; ++b) {
+            float l = 0.0f;
+            check(nrc_train_stream(net, fb->train_queries_d[1] + (size_t)b * NRC_BATCH_SIZE * NRC_INPUT_DIMS,
+                                   reinterpret_cast<const float*>(fb->train_targets_d[1] + (size_t)b * NRC_BATCH_SIZE),
+                                   s, loss_h ? &l : nullptr));
+            total += l;
+        }
+        if (loss_h) *loss_h = total * (1.0f / NRC_NUM_BATCHES);
+    });
+}
+
+}  // extern "C"

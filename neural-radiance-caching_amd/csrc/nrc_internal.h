@@ -80,4 +80,13 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);
 
+// ---- per-frame kernels around the network (nrc_frame.hip, include/nrc/frame.h)
+hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,
+                             hipStream_t s);
+hipError_t launch_propagate(const void* ends, const float* end_rad, uint32_t tiles, const void* records,
+                            float* targets, uint32_t nrec, hipStream_t s);
+hipError_t launch_permutation(uint64_t seed, uint32_t frame, int* perm, uint32_t n, hipStream_t s);
+hipError_t launch_permute(const float* qs, const float* ts, const int* perm, uint64_t seed, uint32_t frame,
+                          uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s);
+
 }  // namespace nrc_amd

@@ -81,3 +81,73 @@ def cornell_targets(n: int, seed: int = SEED) -> np.ndarray:
 
 def cornell_batch(n: int, seed: int = SEED) -> tuple[np.ndarray, np.ndarray]:
     return cornell_queries(n, seed), cornell_targets(n, seed)
+
+
+# ---- one frame of the renderer's NRC buffers (stands in for the OptiX trace) --------------------------------
+class SyntheticFrame:
+    """Host arrays of one frame, in the reference's layouts (neural_radiance_caching.h:57-187).
+
+    Emulates what the trace leaves behind (hit.cu:975-1027, miss.cu:140-160, raygeneration.cu:122-136):
+    one training path per full tile; each non-Dirac vertex of it atomically allocates a TrainingRecord
+    (bounce-major order, shuffled within a bounce like concurrent atomics) linked by ``prop_to`` to the
+    previous one; once the 65,536-record buffer is full the path ends there by self-training; other paths
+    end self-training (mask 1) or, with probability TRAIN_UNBIASED_RATIO = 1/16, unbiased (mask 0).
+    ``num_training_records`` is the raw atomic counter, so it can exceed the capacity.
+    """
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def cornell_frame(width: int = 64, height: int = 48, tile: tuple[int, int] = (4, 4), seed: int = SEED,
+                  frame_index: int = 0, capacity: int = 65536, mean_records: float = 2.0,
+                  max_records_per_path: int = 8) -> SyntheticFrame:
+    from .frame import END_VERTEX_DTYPE, TRAINING_RECORD_DTYPE
+
+    rng = np.random.default_rng([seed, frame_index, 0x4E5243])
+    tx, ty = tile
+    tiles_x, tiles_y = width // tx, height // ty  # boundary tiles are discarded (raygeneration.cu:122-129)
+    screen, tiles = width * height, tiles_x * tiles_y
+
+    n_vert = np.minimum(rng.geometric(1.0 / (mean_records + 1.0), size=tiles) - 1, max_records_per_path)
+    last = np.full(tiles, -1, dtype=np.int64)
+    full = np.zeros(tiles, dtype=bool)
+    recs = np.zeros(capacity, dtype=TRAINING_RECORD_DTYPE)
+    counter = 0
+    for b in range(int(n_vert.max(initial=0))):
+        t = np.flatnonzero((n_vert > b) & ~full)
+        t = rng.permutation(t)
+        idx = counter + np.arange(len(t))
+        counter += len(t)
+        ok = idx < capacity
+        full[t[~ok]] = True
+        t, idx = t[ok], idx[ok]
+        recs["prop_to"][idx] = last[t]
+        recs["local_throughput"][idx] = rng.uniform(0.05, 0.9, size=(len(t), 3)).astype(np.float32)
+        recs["tile_index"][idx] = t
+        recs["pixel_index"][idx] = (t // tiles_x) * ty * width + (t % tiles_x) * tx
+        recs["prop_length"][idx] = b + 1
+        last[t] = idx
+    allocated = min(counter, capacity)
+
+    ends = np.zeros(tiles, dtype=END_VERTEX_DTYPE)
+    ends["start_train_record"] = last
+    unbiased = (rng.random(tiles) < 1.0 / 16.0) & ~full
+    ends["radiance_mask"] = np.where(unbiased, 0.0, 1.0).astype(np.float32)
+    ends["tile_index"] = np.arange(tiles)
+
+    train_q = np.zeros((capacity, 15), dtype=np.float32)
+    train_q[:allocated] = cornell_queries(allocated, seed=int(rng.integers(1 << 31)))
+    train_t = np.zeros((capacity, 3), dtype=np.float32)
+    lit = np.flatnonzero(rng.random(allocated) < 0.1)  # emission / env hits added during the trace
+    train_t[lit] = rng.lognormal(-1.0, 1.5, size=(len(lit), 3)).astype(np.float32)
+
+    thr = rng.uniform(0.0, 1.0, size=(screen, 3)).astype(np.float32)
+    thr[rng.random(screen) < 0.05] = 0.0  # paths that missed early (miss.cu:150-155)
+    return SyntheticFrame(
+        width=width, height=height, tile=tile, screen_size=screen, num_tiles=tiles,
+        num_training_records=counter, frame_index=frame_index,
+        queries_inference=cornell_queries(screen + tiles, seed=int(rng.integers(1 << 31))),
+        last_render_throughput=thr,
+        queries_cache_vis=cornell_queries(screen, seed=int(rng.integers(1 << 31))),
+        end_vertices=ends, train_records=recs, train_queries=train_q, train_targets=train_t)

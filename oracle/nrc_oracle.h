@@ -59,6 +59,17 @@ void orc_adam_ema(float* params, float* m, float* v, float* ema, float* infer_pa
  * a pcg32 stream; init parity with tcnn is not attainable [M], parity tests inject weights. */
 void orc_init_params(float* params, uint64_t seed);
 
+
+/* ---- per-frame kernels around the network (nrc_frame_oracle.c) ---- */
+void orc_accumulate(const float* radiance, const float* throughput, float* rgba, int64_t n, int mode,
+                    uint32_t iteration_index);
+void orc_propagate(const void* end_vertices, const float* end_radiance, int64_t num_tiles, const void* records,
+                   float* targets, int64_t num_records);
+void orc_feistel_keys(uint64_t seed, uint32_t frame, uint32_t keys[4]);
+void orc_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n);
+void orc_permute(const float* q_src, const float* t_src, const int32_t* perm, uint64_t seed, uint32_t frame,
+                 int32_t num_records, float* q_dst, float* t_dst, uint32_t n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,6 +44,12 @@ def lib() -> ctypes.CDLL:
                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int64]
         L.orc_init_params.argtypes = [fp, ctypes.c_uint64]
+        vp, u32, u64, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64
+        L.orc_accumulate.argtypes = [vp, vp, vp, i64, ctypes.c_int, u32]
+        L.orc_propagate.argtypes = [vp, vp, i64, vp, vp, i64]
+        L.orc_feistel_keys.argtypes = [u64, u32, vp]
+        L.orc_permutation.argtypes = [u64, u32, vp, u32]
+        L.orc_permute.argtypes = [vp, vp, vp, u64, u32, ctypes.c_int32, vp, vp, u32]
         _lib = L
     return _lib
 
@@ -119,3 +125,52 @@ def init_params(seed: int = 1337) -> np.ndarray:
 
 def f16_round(x: float) -> float:
     return lib().orc_f16_round(x)
+
+
+# ---- per-frame kernels around the network (oracle/nrc_frame_oracle.c) -----------------------------
+def _v(a: np.ndarray) -> int:
+    assert a.flags.c_contiguous
+    return a.ctypes.data
+
+
+def accumulate(radiance: np.ndarray, throughput: np.ndarray, rgba: np.ndarray, mode: int,
+               iteration_index: int) -> np.ndarray:
+    """accumulate_render_radiance (nrc_helpers.cu:77-129); returns an updated copy of rgba [n, 4]."""
+    r = np.ascontiguousarray(radiance, dtype=np.float32)
+    t = np.ascontiguousarray(throughput, dtype=np.float32)
+    o = np.array(rgba, dtype=np.float32, order="C")
+    lib().orc_accumulate(_v(r), _v(t), _v(o), o.shape[0], int(mode), int(iteration_index))
+    return o
+
+
+def propagate(end_vertices: np.ndarray, end_radiance: np.ndarray, records: np.ndarray, targets: np.ndarray,
+              num_records: int) -> np.ndarray:
+    """propagate_train_radiance (nrc_helpers.cu:131-224); end_vertices / records are the structured
+    dtypes of nrc_amd.frame (16 B / 28 B). Returns an updated copy of targets [n, 3]."""
+    ev = np.ascontiguousarray(end_vertices)
+    er = np.ascontiguousarray(end_radiance, dtype=np.float32)
+    rec = np.ascontiguousarray(records)
+    assert ev.dtype.itemsize == 16 and rec.dtype.itemsize == 28
+    t = np.array(targets, dtype=np.float32, order="C")
+    lib().orc_propagate(_v(ev), _v(er), ev.shape[0], _v(rec), _v(t), int(num_records))
+    return t
+
+
+def permutation(seed: int, frame: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.int32)
+    if n:
+        lib().orc_permutation(int(seed), int(frame), _v(out), int(n))
+    return out
+
+
+def permute(q_src: np.ndarray, t_src: np.ndarray, perm, seed: int, frame: int, num_records: int, n_out: int,
+            q_dst: np.ndarray | None = None, t_dst: np.ndarray | None = None):
+    """permute_train_data (nrc_helpers.cu:226-249); perm None = the Feistel permutation of (seed, frame)."""
+    qs = np.ascontiguousarray(q_src, dtype=np.float32)
+    ts = np.ascontiguousarray(t_src, dtype=np.float32)
+    qd = np.zeros((n_out, 15), np.float32) if q_dst is None else np.array(q_dst, dtype=np.float32, order="C")
+    td = np.zeros((n_out, 3), np.float32) if t_dst is None else np.array(t_dst, dtype=np.float32, order="C")
+    pp = None if perm is None else np.ascontiguousarray(perm, dtype=np.int32)
+    lib().orc_permute(_v(qs), _v(ts), None if pp is None else _v(pp), int(seed), int(frame), int(num_records),
+                      _v(qd), _v(td), int(n_out))
+    return qd, td

@@ -14,3 +14,11 @@ void frame(nrc::Network& net, hipStream_t stream, float* queries, float* results
     (void)net.getLearningRate();
     net.destroy();                                                // Device.cpp:429
 }
+
+// include/nrc/frame.h: the reference's record layouts byte for byte (neural_radiance_caching.h:57-94) and the
+// struct sizes the ctypes mirror in neural-radiance-caching_amd/frame.py assumes.
+#include "nrc/frame.h"
+static_assert(sizeof(nrc_training_record) == 28, "TrainingRecord");
+static_assert(sizeof(nrc_train_suffix_end_vertex) == 16, "TrainingSuffixEndVertex");
+static_assert(sizeof(nrc_frame_buffers) == 13 * sizeof(void*), "nrc_frame_buffers");
+static_assert(sizeof(nrc_frame_params) == 40, "nrc_frame_params");

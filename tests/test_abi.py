@@ -1,4 +1,4 @@
-"""The C-ABI library loads and exports every symbol include/nrc/nrc_c.h declares; host-only entry
+"""The C-ABI library loads and exports every symbol include/nrc/*.h declares; host-only entry
 points behave; the C++ shim and the header compile. No GPU compute calls."""
 import ctypes
 import re
@@ -8,13 +8,15 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
-HEADER = ROOT / "include" / "nrc" / "nrc_c.h"
+HEADERS = sorted((ROOT / "include" / "nrc").glob("*.h"))
 
 
 def header_functions() -> list[str]:
-    text = HEADER.read_text()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(nrc_[a-z_]+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"\b(nrc_[a-z_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_the_binding_list(nrc):
@@ -82,3 +84,11 @@ def test_layout_header_matches_python_constants(nrc):
     assert "#define NRC_NUM_PARAMS" in text
     assert nrc.NUM_PARAMS == 64 * 80 + 4 * 64 * 64 + 16 * 64 == 22528
     assert nrc.BATCH_SIZE == 65536 // 4
+
+
+def test_frame_struct_layouts(nrc):
+    """ctypes mirrors of include/nrc/frame.h structs have the C sizes (static_asserts in tests/cpp/shim_compile.cpp)."""
+    F = nrc.frame
+    assert ctypes.sizeof(F.NrcFrameBuffers) == 13 * 8
+    assert ctypes.sizeof(F.NrcFrameParams) == 40
+    assert F.TRAINING_RECORD_DTYPE.itemsize == 28 and F.END_VERTEX_DTYPE.itemsize == 16

@@ -1,0 +1,237 @@
+"""GPU parity of the per-frame kernels around the network (include/nrc/frame.h) against the C oracle
+(oracle/nrc_frame_oracle.c). Integer / copy / fma work: bit-exact. The frame driver's training leg is
+checked against the oracle's training at the fp16 tolerance of the network tests."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("n", [1, 257, 100_003])
+def test_accumulate_bitwise(nrc, orc, dev, mode, n):
+    import torch
+    rng = np.random.default_rng(n + mode)
+    L = rng.lognormal(-1, 1.5, (n, 3)).astype(np.float32)
+    T = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    O = rng.uniform(0, 2, (n, 4)).astype(np.float32)
+    for it in (0, 13):
+        out = _t(O, dev)
+        nrc.frame.accumulate_render_radiance(_t(L, dev), _t(T, dev), out, n, mode, it)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), orc.accumulate(L, T, O, mode, it))
+
+
+def test_accumulate_tail_untouched_and_errors(nrc, dev):
+    import torch
+    n = 1000
+    out = torch.full((n + 64, 4), -7.0, device=dev)
+    L = torch.ones((n, 3), device=dev)
+    nrc.frame.accumulate_render_radiance(L, L, out, n, nrc.frame.RenderMode.CacheOnly, 0)
+    torch.cuda.synchronize()
+    assert torch.all(out[n:] == -7.0) and torch.all(out[:n] == 1.0)
+    with pytest.raises(nrc.NrcError):
+        nrc.frame.accumulate_render_radiance(L, L, out, n, 9, 0)
+    with pytest.raises(nrc.NrcError):  # float4 frame buffer must be 16-byte aligned
+        nrc.frame.accumulate_render_radiance(L, L, int(out.data_ptr()) + 4, n, 0, 0)
+
+
+def test_copy_radiance_to_output(nrc, dev):
+    import torch
+    L = torch.rand((777, 3), device=dev)
+    out = torch.zeros((777, 4), device=dev)
+    nrc.frame.copy_radiance_to_output(L, out, 777)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :3], L) and torch.all(out[:, 3] == 1)
+
+
+@pytest.mark.parametrize("shape", [(64, 48, (4, 4), 512), (1920, 1080, (8, 8), 65536), (640, 480, (2, 2), 65536)])
+def test_propagate_bitwise(nrc, orc, dev, shape):
+    import torch
+    w, h, tile, cap = shape
+    f = nrc.synthetic.cornell_frame(w, h, tile, seed=11, capacity=cap)
+    nrec = min(f.num_training_records, cap)
+    rng = np.random.default_rng(4)
+    end_rad = rng.lognormal(-1, 1, (f.num_tiles, 3)).astype(np.float32)
+    tg = _t(f.train_targets, dev)
+    nrc.frame.propagate_train_radiance(nrc.frame.records_to_device(f.end_vertices, dev), _t(end_rad, dev),
+                                       f.num_tiles, nrc.frame.records_to_device(f.train_records, dev), tg, nrec)
+    torch.cuda.synchronize()
+    want = orc.propagate(f.end_vertices, end_rad, f.train_records, f.train_targets, nrec)
+    np.testing.assert_array_equal(tg.cpu().numpy(), want)
+
+
+def test_propagate_hardening(nrc, orc, dev):
+    """Cyclic and out-of-range links neither hang nor fault; results match the oracle."""
+    import torch
+    F = nrc.frame
+    recs = np.zeros(4, dtype=F.TRAINING_RECORD_DTYPE)
+    recs["prop_to"] = [1, 1, 99, -1]
+    recs["local_throughput"] = 0.5
+    ends = np.zeros(5, dtype=F.END_VERTEX_DTYPE)
+    ends["start_train_record"] = [0, 2, 7, F.TRAIN_RECORD_INDEX_BUFFER_FULL, F.TRAIN_RECORD_INDEX_NONE]
+    ends["radiance_mask"] = 1.0
+    er = np.ones((5, 3), np.float32)
+    tg = torch.zeros((4, 3), device=dev)
+    F.propagate_train_radiance(F.records_to_device(ends, dev), _t(er, dev), 5, F.records_to_device(recs, dev), tg, 4)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(tg.cpu().numpy(), orc.propagate(ends, er, recs, np.zeros((4, 3), np.float32), 4))
+
+
+@pytest.mark.parametrize("n", [1, 3, 1000, 65536, 100_003, 1 << 22])
+def test_permutation_bitwise(nrc, orc, dev, n):
+    import torch
+    p = torch.empty(n, dtype=torch.int32, device=dev)
+    nrc.frame.generate_train_permutation(0xDEADBEEF12345, 5, p, n)
+    torch.cuda.synchronize()
+    got = p.cpu().numpy()
+    np.testing.assert_array_equal(got, orc.permutation(0xDEADBEEF12345, 5, n))
+    assert np.array_equal(np.sort(got), np.arange(n))
+
+
+@pytest.mark.parametrize("num_records", [65536, 40000, 1, 70000, 0, -3])
+@pytest.mark.parametrize("explicit", [False, True])
+def test_permute_bitwise(nrc, orc, dev, num_records, explicit):
+    import torch
+    n_out = 65536
+    rng = np.random.default_rng(num_records & 0xFFFF)
+    qs = rng.normal(size=(n_out, 15)).astype(np.float32)
+    ts = rng.normal(size=(n_out, 3)).astype(np.float32)
+    perm = rng.permutation(n_out).astype(np.int32) if explicit else None
+    qd = torch.full((n_out, 15), 3.0, device=dev)
+    td = torch.full((n_out, 3), 3.0, device=dev)
+    nrc.frame.permute_train_data(_t(qs, dev), _t(ts, dev), None if perm is None else _t(perm, dev), 77, 9,
+                                 num_records, qd, td, n_out)
+    torch.cuda.synchronize()
+    wq, wt = orc.permute(qs, ts, perm, 77, 9, num_records, n_out, q_dst=np.full((n_out, 15), 3.0, np.float32),
+                         t_dst=np.full((n_out, 3), 3.0, np.float32))
+    np.testing.assert_array_equal(qd.cpu().numpy(), wq)
+    np.testing.assert_array_equal(td.cpu().numpy(), wt)
+
+
+# ---- the frame driver ---------------------------------------------------------------------------------------------
+def _device_frame(nrc, f, dev, with_perm=None):
+    import torch
+    F = nrc.frame
+    cap = F.NUM_TRAINING_RECORDS_PER_FRAME
+    tq0 = np.zeros((cap, 15), np.float32)
+    tq0[: len(f.train_queries)] = f.train_queries[:cap]
+    tt0 = np.zeros((cap, 3), np.float32)
+    tt0[: len(f.train_targets)] = f.train_targets[:cap]
+    rec = np.zeros(cap, F.TRAINING_RECORD_DTYPE)
+    rec[: len(f.train_records)] = f.train_records[:cap]
+    return F.FrameBuffers(
+        queries_inference=_t(f.queries_inference, dev),
+        results_inference=torch.zeros((f.screen_size + f.num_tiles, 3), device=dev),
+        last_render_throughput=_t(f.last_render_throughput, dev),
+        output_rgba=torch.zeros((f.screen_size, 4), device=dev),
+        queries_cache_vis=_t(f.queries_cache_vis, dev),
+        results_cache_vis=torch.zeros((f.screen_size, 3), device=dev),
+        end_vertices=F.records_to_device(f.end_vertices, dev),
+        train_records=F.records_to_device(rec, dev),
+        train_queries=[_t(tq0, dev), torch.zeros((cap, 15), device=dev)],
+        train_targets=[_t(tt0, dev), torch.zeros((cap, 3), device=dev)],
+        permutation=None if with_perm is None else _t(with_perm, dev)), tq0, tt0, rec
+
+
+def test_process_frame_matches_oracle_pipeline(nrc, orc, dev):
+    """One full frame (infer -> accumulate -> propagate -> shuffle -> 4 x train) against the oracle's steps."""
+    import torch
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(320, 240, (4, 4), seed=21, frame_index=3)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    params = orc.init_params(1337) * np.float32(1.6)
+    for slot in (nrc.StateSlot.PARAMS, nrc.StateSlot.INFER):
+        net.set_state(slot, params)
+    fb, tq0, tt0, rec = _device_frame(nrc, f, dev)
+    out0 = np.random.default_rng(0).uniform(0, 1, (f.screen_size, 4)).astype(np.float32)
+    fb.output_rgba.copy_(_t(out0, dev))
+    fp = F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records, F.RenderMode.Full, iteration_index=2,
+                       frame_index=3, shuffle_seed=99)
+    loss = F.process_frame(net, fb, fp)
+    torch.cuda.synchronize()
+
+    # infer: the network's own per-query tolerance is covered by test_gpu_parity; here the downstream steps are
+    # checked bit-exactly given the GPU's radiance.
+    res = fb.results_inference.cpu().numpy()
+    y_ref = orc.forward(params, f.queries_inference, orc.MIXED)
+    assert np.linalg.norm(res - y_ref) / np.linalg.norm(y_ref) < 1e-3
+    np.testing.assert_array_equal(fb.output_rgba.cpu().numpy(),
+                                  orc.accumulate(res[: f.screen_size], f.last_render_throughput, out0, 0, 2))
+    nrec = min(f.num_training_records, 65536)
+    tt_prop = orc.propagate(f.end_vertices, res[f.screen_size:], rec, tt0, nrec)
+    np.testing.assert_array_equal(fb.train_targets[0].cpu().numpy(), tt_prop)
+    qd, td = orc.permute(tq0, tt_prop, None, 99, 3, nrec, 65536)
+    np.testing.assert_array_equal(fb.train_queries[1].cpu().numpy(), qd)
+    np.testing.assert_array_equal(fb.train_targets[1].cpu().numpy(), td)
+
+    # training: 4 oracle steps on the same shuffled batches
+    st = orc.AdamEmaState(params)
+    losses = []
+    for b in range(4):
+        s = slice(b * 16384, (b + 1) * 16384)
+        g, lb = orc.grad(st.params, qd[s], td[s])
+        st.apply(g)
+        losses.append(lb)
+    # same tolerances as test_gpu_parity.test_train_step_matches_oracle_and_learns (fp16 network)
+    assert abs(loss - np.mean(losses)) <= 2e-2 * abs(np.mean(losses))
+    assert net.step == 4
+    p_gpu = net.get_state(nrc.StateSlot.PARAMS)
+    assert np.linalg.norm(p_gpu - st.params) / np.linalg.norm(st.params) <= 1e-3
+    net.destroy()
+
+
+def test_process_frame_modes(nrc, orc, dev):
+    import torch
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(128, 64, (4, 4), seed=2)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    params = net.get_state(nrc.StateSlot.INFER)
+
+    # NoCache: render queries are not inferred, the frame buffer is untouched, training still runs
+    fb, *_ = _device_frame(nrc, f, dev)
+    fb.results_inference.fill_(-1.0)
+    fb.output_rgba.fill_(5.0)
+    loss = F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records,
+                                                  F.RenderMode.NoCache))
+    torch.cuda.synchronize()
+    assert torch.all(fb.results_inference[: f.screen_size] == -1.0)
+    assert torch.all(fb.results_inference[f.screen_size:] != -1.0)
+    assert torch.all(fb.output_rgba == 5.0)
+    assert np.isfinite(loss) and net.step == 4
+
+    # CacheFirstVertex: output = radiance at the first non-specular vertex
+    net.init(stream=torch.cuda.current_stream())
+    net.set_state(nrc.StateSlot.INFER, params)
+    fb, *_ = _device_frame(nrc, f, dev)
+    loss = F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records,
+                                                  F.RenderMode.CacheFirstVertex, train=False))
+    torch.cuda.synchronize()
+    assert loss == 0.0 and net.step == 0
+    vis = fb.results_cache_vis.cpu().numpy()
+    assert np.linalg.norm(vis - orc.forward(params, f.queries_cache_vis, orc.MIXED)) / np.linalg.norm(vis) < 1e-3
+    np.testing.assert_array_equal(fb.output_rgba.cpu().numpy()[:, :3], vis)
+
+    # no records: no training (Device.cpp:2507)
+    fb, *_ = _device_frame(nrc, f, dev)
+    assert F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, 0)) == 0.0
+    assert net.step == 0
+
+    # explicit (caller-made) permutation: shuffled buffers follow it exactly
+    perm = np.random.default_rng(5).permutation(65536).astype(np.int32)
+    fb, tq0, tt0, rec = _device_frame(nrc, f, dev, with_perm=perm)
+    F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records), loss=False)
+    torch.cuda.synchronize()
+    nrec = min(f.num_training_records, 65536)
+    np.testing.assert_array_equal(fb.train_queries[1].cpu().numpy(), tq0[perm % nrec])
+
+    net.destroy()
+    with pytest.raises(nrc.NrcError):
+        F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records))
