@@ -5,6 +5,6 @@ This package is the host-side mirror of the reference interface plus the synthet
 stream and the data-parallel sharding. The directory name contains hyphens, so it is loaded as the
 module ``nrc_amd`` by ``load()`` in __graft_entry__.py / tests/conftest.py / bench.py.
 """
-from . import _lib, dp, frame, synthetic  # noqa: F401
+from . import _lib, dp, frame, stream, synthetic  # noqa: F401
 from ._lib import BATCH_SIZE, GRAD_FLOATS, NUM_PARAMS, NrcError  # noqa: F401
 from .network import HyperParams, InputEncoding, Network, StateSlot, current_stream, default_config, encode  # noqa: F401

@@ -36,6 +36,9 @@ EXPORTS = [
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame",
+    # include/nrc/stream.h (bound in stream.py)
+    "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_open", "nrc_stream_close",
+    "nrc_stream_write_frame", "nrc_stream_next_frame", "nrc_stream_read_section",
 ]
 
 
