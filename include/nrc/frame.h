@@ -62,6 +62,16 @@ nrc_status nrc_accumulate_render_radiance(const nrc_float3* end_render_radiance_
                                           uint32_t num_pixels, int mode, uint32_t iteration_index,
                                           hipStream_t stream);
 
+/* infer() with accumulate_render_radiance fused into the inference epilogue:
+ * queries [0, num_pixels) are the render queries — their radiance goes straight into output_rgba exactly as
+ * nrc_accumulate_render_radiance would put it (bit-identical) and is NOT written to results_d; queries
+ * [num_pixels, n) (the train-suffix ends) are written to results_d as infer() does. mode: Full or CacheOnly
+ * (other modes: NRC_ERR_INVALID_ARGUMENT — use nrc_infer + nrc_accumulate_render_radiance). Saves the 24 B/pixel
+ * radiance round trip through HBM and one launch. Uses the inference (EMA) weights, the handle's stream. */
+nrc_status nrc_infer_accumulate(nrc_net* net, const float* queries_d, float* results_d, uint32_t n,
+                                const nrc_float3* end_render_throughput_d, float* output_rgba_d, uint32_t num_pixels,
+                                int mode, uint32_t iteration_index);
+
 /* copy_radiance_to_output_buffer (nrc_helpers.cu:54-73): out = (radiance, 1) for n pixels. */
 nrc_status nrc_copy_radiance_to_output(const nrc_float3* radiance_d, float* output_rgba_d, uint32_t num_pixels,
                                        hipStream_t stream);
@@ -119,11 +129,14 @@ typedef struct nrc_frame_params {
     uint32_t frame_index;         /* shuffle key */
     uint64_t shuffle_seed;
     int32_t train;                /* 0: inference/accumulation only */
+    int32_t keep_render_results;  /* 1: also write the render queries' radiance to results_inference (unfused
+                                     infer + accumulate, e.g. for the reference's debug dump); 0: fused */
 } nrc_frame_params;
 
-/* Runs, on the handle's stream: infer -> accumulate (or cache-vis) -> [if records] propagate -> shuffle ->
- * NUM_BATCHES x train. loss_h (optional) receives the mean of the NUM_BATCHES minibatch losses
- * (Device.cpp:1503-1511) and makes the call block; 0 if the frame did not train. */
+/* Runs, on the handle's stream: infer -> accumulate (fused into infer for Full / CacheOnly unless
+ * keep_render_results; cache-vis for CacheFirstVertex) -> [if records] propagate -> shuffle -> NUM_BATCHES x train.
+ * loss_h (optional) receives the mean of the NUM_BATCHES minibatch losses (Device.cpp:1503-1511) and makes the call
+ * block once at the end (the reference blocks after every minibatch); 0 if the frame did not train. */
 nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* buffers, const nrc_frame_params* params,
                              float* loss_h);
 

@@ -90,6 +90,9 @@ nrc_status nrc_train_stream(nrc_net* net, const float* inputs_d, const float* ta
                             float* loss_h);
 /* Extension: a step on any batch size b >= 1 (the reference fixes b = 16384). */
 nrc_status nrc_train_batch(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b, float* loss_h);
+/* Extension (the asynchronous loss read-back SURVEY.md §8(b) allows): one step on b samples on the handle's
+ * stream whose minibatch loss is written to device memory loss_d (may be NULL); never blocks. */
+nrc_status nrc_train_async(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b, float* loss_d);
 
 /* infer(in, out, n) / infer(in, out, n, stream) (NRCNetwork.h:49-51). Processes exactly n queries
  * (the reference rounds n up to 256 and reads/writes past n, NRCNetwork.cu:147-148; this one never

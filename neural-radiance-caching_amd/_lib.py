@@ -29,12 +29,12 @@ STATUS_NAMES = {
 # Every symbol include/nrc/*.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "nrc_version", "nrc_last_error", "nrc_default_config", "nrc_create", "nrc_free", "nrc_init", "nrc_destroy",
-    "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
+    "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_train_async", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_get_state", "nrc_set_state", "nrc_get_step", "nrc_set_step",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_encode_fast",
     # include/nrc/frame.h (bound in frame.py)
-    "nrc_accumulate_render_radiance", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
+    "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame",
     # include/nrc/stream.h (bound in stream.py)
     "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_open", "nrc_stream_close",
@@ -86,6 +86,7 @@ def lib() -> ctypes.CDLL:
         "nrc_train": (st, [vp, fp, fp, ctypes.POINTER(ctypes.c_float)]),
         "nrc_train_stream": (st, [vp, fp, fp, vp, ctypes.POINTER(ctypes.c_float)]),
         "nrc_train_batch": (st, [vp, fp, fp, u32, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_train_async": (st, [vp, fp, fp, u32, fp]),
         "nrc_infer": (st, [vp, fp, fp, u32]),
         "nrc_infer_stream": (st, [vp, fp, fp, u32, vp]),
         "nrc_set_stream": (st, [vp, vp]),

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "nrc/frame.h"
 #include "nrc/nrc_c.h"
 #include "nrc_guard.h"
 #include "nrc_internal.h"
@@ -203,7 +204,7 @@ void repack(nrc_net* net, hipStream_t s) {
     HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
 }
 
-void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h) {
+void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h, float* loss_d = nullptr) {
     check_live(net);
     if (b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "batch size must be >= 1");
     if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
@@ -212,8 +213,8 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                    net->slabs, net->loss_partials, net->stream));
     net->step += 1;
-    HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr, net->loss_dev,
-                                 net->buffers(), net->optim(net->step), net->stream));
+    HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
+                                 loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
     if (loss_h) {
         HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
         HIP_CHECK(hipStreamSynchronize(net->stream));
@@ -233,6 +234,11 @@ float* slot_ptr(nrc_net* net, int slot) {
 }
 
 }  // namespace
+
+nrc_loss_slots nrc_amd::net_loss_slots(nrc_net* net) {
+    check_live(net);
+    return {net->loss_dev, net->loss_host};
+}
 
 extern "C" {
 
@@ -347,6 +353,31 @@ nrc_status nrc_train_stream(nrc_net* net, const float* in, const float* tgt, hip
 
 nrc_status nrc_train_batch(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h) {
     return guarded([&] { do_train(net, in, tgt, b, loss_h); });
+}
+
+nrc_status nrc_train_async(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_d) {
+    return guarded([&] {
+        check_live(net);
+        // loss_d == NULL: the loss still lands in the handle's own slot
+        do_train(net, in, tgt, b, nullptr, loss_d);
+    });
+}
+
+nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint32_t n, const nrc_float3* thr,
+                                float* rgba, uint32_t num_pixels, int mode, uint32_t iteration_index) {
+    return guarded([&] {
+        check_live(net);
+        if (mode != NRC_RENDER_FULL && mode != NRC_RENDER_CACHE_ONLY)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "fused accumulation supports RenderMode Full and CacheOnly only");
+        if (num_pixels > n) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "num_pixels > n");
+        if (n == 0) return;
+        if (!in || (num_pixels < n && !out)) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null query/result pointer");
+        if (num_pixels > 0 && (!thr || !rgba || (reinterpret_cast<uintptr_t>(rgba) & 15)))
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "throughput / 16-byte aligned float4 frame buffer required");
+        const float w = 1.0f / (float)(iteration_index + 1u);  // nrc_helpers.cu:98
+        HIP_CHECK(launch_infer_accumulate(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba,
+                                          num_pixels, mode, w, net->stream));
+    });
 }
 
 nrc_status nrc_infer(nrc_net* net, const float* in, float* out, uint32_t n) {

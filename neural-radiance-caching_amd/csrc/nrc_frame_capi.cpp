@@ -113,12 +113,20 @@ nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nr
             nq = tiles;
         }
         require(nq <= UINT32_MAX, "screen_size + num_tiles overflows");
+        // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion)
+        const bool fuse = !skip_render && !p->keep_render_results &&
+                          (mode == NRC_RENDER_FULL || mode == NRC_RENDER_CACHE_ONLY);
         if (nq > 0) {
             require(fb->queries_inference_d && fb->results_inference_d, "inference buffers are NULL");
-            check(nrc_infer_stream(net, q, reinterpret_cast<float*>(r), (uint32_t)nq, s));
+            if (fuse)
+                check(nrc_infer_accumulate(net, q, reinterpret_cast<float*>(r), (uint32_t)nq,
+                                           fb->last_render_throughput_d, fb->output_rgba_d, screen, mode,
+                                           p->iteration_index));
+            else
+                check(nrc_infer_stream(net, q, reinterpret_cast<float*>(r), (uint32_t)nq, s));
         }
         // Device::nrcAccumulateRadiance (Device.cpp:1310-1337)
-        if (!skip_render)
+        if (!skip_render && !fuse)
             check(nrc_accumulate_render_radiance(fb->results_inference_d, fb->last_render_throughput_d,
                                                  fb->output_rgba_d, screen, mode, p->iteration_index, s));
         // Device::nrcVisualizeFirstRadiance (Device.cpp:1339-1370)
@@ -141,16 +149,21 @@ nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nr
         check(nrc_permute_train_data(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d,
                                      p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],
                                      fb->train_targets_d[1], NRC_NUM_TRAINING_RECORDS_PER_FRAME, s));
-        // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss
-        float total = 0.0f;
-        for (int b = 0; b < NRC_NUM_BATCHES; ++b) {
-            float l = 0.0f;
-            check(nrc_train_stream(net, fb->train_queries_d[1] + (size_t)b * NRC_BATCH_SIZE * NRC_INPUT_DIMS,
-                                   reinterpret_cast<const float*>(fb->train_targets_d[1] + (size_t)b * NRC_BATCH_SIZE),
-                                   s, loss_h ? &l : nullptr));
-            total += l;
+        // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss. The minibatch losses
+        // land in device slots and are read back with one copy + one sync at the end (the reference syncs after
+        // every minibatch, Device.cpp:1504); summed in the same order, so the mean is the same float.
+        const nrc_loss_slots slots = net_loss_slots(net);
+        for (int b = 0; b < NRC_NUM_BATCHES; ++b)
+            check(nrc_train_async(net, fb->train_queries_d[1] + (size_t)b * NRC_BATCH_SIZE * NRC_INPUT_DIMS,
+                                  reinterpret_cast<const float*>(fb->train_targets_d[1] + (size_t)b * NRC_BATCH_SIZE),
+                                  NRC_BATCH_SIZE, slots.dev + b));
+        if (loss_h) {
+            HIP_CHECK(hipMemcpyAsync(slots.host, slots.dev, sizeof(float) * NRC_NUM_BATCHES, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            float total = 0.0f;
+            for (int b = 0; b < NRC_NUM_BATCHES; ++b) total += slots.host[b];
+            *loss_h = total * (1.0f / NRC_NUM_BATCHES);
         }
-        if (loss_h) *loss_h = total * (1.0f / NRC_NUM_BATCHES);
     });
 }
 

@@ -53,7 +53,10 @@ __host__ __device__ constexpr int k0_feature(int K) {
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s);
-constexpr int kNumInferVariants = 21;
+constexpr int kNumInferVariants = 22;
+// inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
+hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
+                                   float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
@@ -79,6 +82,17 @@ struct ModelBuffers {
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);
+
+// ---- per-handle scratch used by the frame driver (nrc_capi.cpp): NRC_NUM_BATCHES loss slots on the device and a
+// pinned host mirror
+struct nrc_loss_slots {
+    float* dev;
+    float* host;
+};
+}  // namespace nrc_amd
+struct nrc_net;
+namespace nrc_amd {
+nrc_loss_slots net_loss_slots(nrc_net* net);
 
 // ---- per-frame kernels around the network (nrc_frame.hip, include/nrc/frame.h)
 hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,

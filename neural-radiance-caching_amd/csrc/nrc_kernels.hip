@@ -428,16 +428,29 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
     }
 }
 
-template <int TILES, int WAVES_PER_EU, int THREADS, bool PREFETCH, int ABL = 0>
-__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const float* __restrict__ q,
-                                                                         float* __restrict__ out, int64_t n,
-                                                                         const h8* __restrict__ wf) {
+// Optional epilogue: accumulate_render_radiance (nrc_helpers.cu:77-129) fused into inference for the render
+// queries [0, n_acc) (EPI = RenderMode Full 0 / CacheOnly 2); their radiance is consumed in registers and never
+// written. Queries [n_acc, n) (the train-suffix ends) are written to out as usual. Same float operations as
+// accumulate_kernel (nrc_frame.hip), so the frame buffer is bit-identical to the unfused path.
+struct InferEpilogue {
+    const float* thr;  // [n_acc] float3 lastRenderThroughput
+    float4* rgba;      // [n_acc] frame buffer
+    int64_t n_acc;
+    float w;           // 1 / (iterationIndex + 1)
+};
+
+template <int TILES, int THREADS, bool PREFETCH, int ABL, int EPI>
+__device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float* __restrict__ out, int64_t n,
+                                              const h8* __restrict__ wf, const InferEpilogue& epi) {
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    // ABL & 8: per-wave staging of a tile's 32 x 12-B results so they leave as 24 contiguous 16-B stores
+    __shared__ __attribute__((aligned(16))) float ostage[(ABL & 8) ? THREADS / 64 : 1][96];
     copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, r = lane & 31;
+    const bool out16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
     const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
     int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
@@ -465,21 +478,91 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
 #pragma unroll
             for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
         }
+        // epilogue operands are fetched before the MLP so their latency hides under the MFMAs
+        float tr[TILES][3];
+        float4 acc[TILES];
+        if constexpr (EPI >= 0) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                const int64_t s = (g * TILES + t) * 32 + r;
+                if (h == 0 && s < epi.n_acc) {
+                    const float* T = epi.thr + s * 3;
+                    tr[t][0] = T[0];
+                    tr[t][1] = T[1];
+                    tr[t][2] = T[2];
+                    if constexpr (EPI == 0) acc[t] = epi.rgba[s];
+                }
+            }
+        }
         f16v o[TILES];
-        mlp_tiles<TILES, PREFETCH, ABL>((lds_h8*)(lw + lane), x, o);
+        mlp_tiles<TILES, PREFETCH, ABL & 7>((lds_h8*)(lw + lane), x, o);
+        if constexpr ((ABL & 8) && EPI < 0) {
+            const int64_t s0 = g * TILES * 32;
+            if (out16 && s0 + TILES * 32 <= n) {
+                float* st = ostage[threadIdx.x >> 6];
+#pragma unroll
+                for (int t = 0; t < TILES; ++t) {
+                    if (h == 0) {
+                        st[3 * r + 0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                        st[3 * r + 1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                        st[3 * r + 2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                    }
+                    __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler in order too
+                    if (lane < 24)
+                        reinterpret_cast<float4*>(out + (s0 + t * 32) * NRC_OUTPUT_DIMS)[lane] =
+                            reinterpret_cast<const float4*>(st)[lane];
+                    __builtin_amdgcn_wave_barrier();
+                }
+                continue;
+            }
+        }
         if (h == 0) {
 #pragma unroll
             for (int t = 0; t < TILES; ++t) {
                 const int64_t s = (g * TILES + t) * 32 + r;
                 if (s < n) {
-                    float* dst = out + s * NRC_OUTPUT_DIMS;
-                    dst[0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
-                    dst[1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
-                    dst[2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                    const float L0 = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                    const float L1 = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                    const float L2 = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                    if (EPI >= 0 && s < epi.n_acc) {
+                        float4 v;
+                        if constexpr (EPI == 0) {  // Full: dst += (T * L) * w
+                            v = acc[t];
+                            v.x = __builtin_fmaf(tr[t][0] * L0, epi.w, v.x);
+                            v.y = __builtin_fmaf(tr[t][1] * L1, epi.w, v.y);
+                            v.z = __builtin_fmaf(tr[t][2] * L2, epi.w, v.z);
+                        } else {  // CacheOnly
+                            v.x = L0 * tr[t][0];
+                            v.y = L1 * tr[t][1];
+                            v.z = L2 * tr[t][2];
+                        }
+                        v.w = 1.0f;
+                        epi.rgba[s] = v;
+                    } else {
+                        float* dst = out + s * NRC_OUTPUT_DIMS;
+                        dst[0] = L0;
+                        dst[1] = L1;
+                        dst[2] = L2;
+                    }
                 }
             }
         }
     }
+}
+
+template <int TILES, int WAVES_PER_EU, int THREADS, bool PREFETCH, int ABL = 0>
+__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const float* __restrict__ q,
+                                                                         float* __restrict__ out, int64_t n,
+                                                                         const h8* __restrict__ wf) {
+    infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, InferEpilogue{});
+}
+
+// the default inference configuration (variant 3) with the accumulation epilogue
+template <int EPI>
+__global__ __launch_bounds__(512, 4) void infer_accumulate_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                                  int64_t n, const h8* __restrict__ wf,
+                                                                  InferEpilogue epi) {
+    infer_v2_body<1, 512, false, 0, EPI>(q, out, n, wf, epi);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1193,15 +1276,15 @@ static int blocks_per_cu(K kernel, int threads) {
     return v;
 }
 
-template <class K>
+template <class K, class... Extra>
 static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc, int64_t groups, const float* queries,
-                                          float* out, int64_t n, const _Float16* wf, hipStream_t s) {
+                                          float* out, int64_t n, const _Float16* wf, hipStream_t s, Extra... extra) {
     if (!cache_bpc) cache_bpc = blocks_per_cu(kernel, threads);
     const int wpb = threads / 64;
     const int64_t want = (groups + wpb - 1) / wpb;
     const int64_t cap = (int64_t)num_cus() * cache_bpc;
     const int grid = (int)(want < cap ? want : cap);
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, queries, out, n, (const h8*)wf);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, queries, out, n, (const h8*)wf, extra...);
     return hipGetLastError();
 }
 
@@ -1236,6 +1319,8 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 14: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 4>, 512, bpc[14], ntiles, queries, out, n, wf, s);
         case 15: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 7>, 512, bpc[15], ntiles, queries, out, n, wf, s);
         case 16: return launch_persistent_infer(infer_kernel_v2<2, 2, 256, false, 7>, 256, bpc[16], pairs, queries, out, n, wf, s);
+        // v2 variant 3 with LDS-staged coalesced 16-B result stores
+        case 21: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 8>, 512, bpc[21], ntiles, queries, out, n, wf, s);
         // v4: explicit layer-ahead weight prefetch
         case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
         case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
@@ -1252,6 +1337,19 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
 
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s);
+}
+
+hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
+                                   float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t ntiles = (n + 31) / 32;
+    static int bpc[2] = {};
+    const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
+    switch (mode) {
+        case 0: return launch_persistent_infer(infer_accumulate_kernel<0>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_accumulate_kernel<2>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s) {

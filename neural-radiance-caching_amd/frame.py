@@ -82,6 +82,7 @@ def _sigs():
     for name, args in {
         "nrc_accumulate_render_radiance": [vp, vp, vp, u32, ctypes.c_int, u32, vp],
         "nrc_copy_radiance_to_output": [vp, vp, u32, vp],
+        "nrc_infer_accumulate": [vp, vp, vp, u32, vp, vp, u32, ctypes.c_int, u32],
         "nrc_propagate_train_radiance": [vp, vp, u32, vp, vp, u32, vp],
         "nrc_generate_train_permutation": [u64, u32, vp, u32, vp],
         "nrc_permute_train_data": [vp, vp, vp, u64, u32, i32, vp, vp, u32, vp],
@@ -108,7 +109,7 @@ class NrcFrameParams(ctypes.Structure):
     _fields_ = [("screen_size", ctypes.c_uint32), ("num_tiles", ctypes.c_uint32),
                 ("num_training_records", ctypes.c_int32), ("render_mode", ctypes.c_int32),
                 ("iteration_index", ctypes.c_uint32), ("frame_index", ctypes.c_uint32),
-                ("shuffle_seed", ctypes.c_uint64), ("train", ctypes.c_int32)]
+                ("shuffle_seed", ctypes.c_uint64), ("train", ctypes.c_int32), ("keep_render_results", ctypes.c_int32)]
 
 
 def accumulate_render_radiance(radiance, throughput, output_rgba, num_pixels: int, mode: RenderMode,
@@ -116,6 +117,15 @@ def accumulate_render_radiance(radiance, throughput, output_rgba, num_pixels: in
     check(_sigs().nrc_accumulate_render_radiance(_ptr(radiance, "radiance"), _ptr(throughput, "throughput"),
                                                  _ptr(output_rgba, "output_rgba"), int(num_pixels), int(mode),
                                                  int(iteration_index), _stream(stream)))
+
+
+def infer_accumulate(net, queries, results, n: int, throughput, output_rgba, num_pixels: int, mode: RenderMode,
+                     iteration_index: int) -> None:
+    """infer() with accumulate_render_radiance fused into its epilogue for the render queries [0, num_pixels)
+    (their radiance is not written to ``results``); on the network's stream."""
+    check(_sigs().nrc_infer_accumulate(net._h, _ptr(queries, "queries"), _ptr(results, "results"), int(n),
+                                       _ptr(throughput, "throughput"), _ptr(output_rgba, "output_rgba"),
+                                       int(num_pixels), int(mode), int(iteration_index)))
 
 
 def copy_radiance_to_output(radiance, output_rgba, num_pixels: int, stream=None) -> None:
@@ -199,11 +209,12 @@ class FrameParams:
     frame_index: int = 0
     shuffle_seed: int = 0
     train: bool = True
+    keep_render_results: bool = False
 
     def as_struct(self) -> NrcFrameParams:
         return NrcFrameParams(int(self.screen_size), int(self.num_tiles), int(self.num_training_records),
                               int(self.render_mode), int(self.iteration_index), int(self.frame_index),
-                              int(self.shuffle_seed), int(bool(self.train)))
+                              int(self.shuffle_seed), int(bool(self.train)), int(bool(self.keep_render_results)))
 
 
 def process_frame(net, buffers: FrameBuffers, params: FrameParams, loss: bool = True):

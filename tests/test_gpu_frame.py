@@ -153,7 +153,7 @@ def test_process_frame_matches_oracle_pipeline(nrc, orc, dev):
     out0 = np.random.default_rng(0).uniform(0, 1, (f.screen_size, 4)).astype(np.float32)
     fb.output_rgba.copy_(_t(out0, dev))
     fp = F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records, F.RenderMode.Full, iteration_index=2,
-                       frame_index=3, shuffle_seed=99)
+                       frame_index=3, shuffle_seed=99, keep_render_results=True)
     loss = F.process_frame(net, fb, fp)
     torch.cuda.synchronize()
 
@@ -235,3 +235,58 @@ def test_process_frame_modes(nrc, orc, dev):
     net.destroy()
     with pytest.raises(nrc.NrcError):
         F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records))
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("n,n_acc", [(100_003, 90_001), (4096, 4096), (777, 0), (2_097_152 + 32_400, 2_097_152)])
+def test_infer_accumulate_fused_bitwise(nrc, dev, mode, n, n_acc):
+    """Fused inference epilogue == nrc_infer + nrc_accumulate_render_radiance, bit for bit; render radiance is not
+    written, train-suffix radiance is."""
+    import torch
+    F = nrc.frame
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    q = _t(nrc.synthetic.cornell_queries(n, seed=n), dev)
+    rng = np.random.default_rng(n_acc)
+    thr = _t(rng.uniform(0, 1, (max(n_acc, 1), 3)).astype(np.float32), dev)
+    rgba0 = _t(rng.uniform(0, 1, (max(n_acc, 1), 4)).astype(np.float32), dev)
+    ref_res = torch.empty((n, 3), device=dev)
+    net.infer(q, ref_res, n)
+    ref_rgba = rgba0.clone()
+    F.accumulate_render_radiance(ref_res, thr, ref_rgba, n_acc, mode, 5)
+    res = torch.full((n, 3), -3.0, device=dev)
+    rgba = rgba0.clone()
+    F.infer_accumulate(net, q, res, n, thr, rgba, n_acc, mode, 5)
+    torch.cuda.synchronize()
+    assert torch.equal(rgba, ref_rgba)
+    assert torch.equal(res[n_acc:], ref_res[n_acc:])
+    assert torch.all(res[:n_acc] == -3.0)
+    with pytest.raises(nrc.NrcError):
+        F.infer_accumulate(net, q, res, n, thr, rgba, n_acc, F.RenderMode.DebugThroughputOnly, 0)
+    net.destroy()
+
+
+def test_process_frame_fused_equals_unfused(nrc, dev):
+    """The default (fused, one loss sync) frame == the reference-shaped unfused frame: same frame buffer, same
+    train-suffix radiance, same losses and weights."""
+    import torch
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(256, 192, (4, 4), seed=8, frame_index=1)
+    out = []
+    for keep in (False, True):
+        net = nrc.Network()
+        net.init(stream=torch.cuda.current_stream())
+        fb, *_ = _device_frame(nrc, f, dev)
+        fb.output_rgba.fill_(0.25)
+        losses = [F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records,
+                                                         F.RenderMode.Full, iteration_index=it, frame_index=it,
+                                                         keep_render_results=keep)) for it in range(3)]
+        torch.cuda.synchronize()
+        out.append((losses, fb.output_rgba.cpu().numpy(), fb.results_inference[f.screen_size:].cpu().numpy(),
+                    net.get_state(nrc.StateSlot.INFER)))
+        net.destroy()
+    (l0, o0, r0, w0), (l1, o1, r1, w1) = out
+    assert l0 == l1
+    np.testing.assert_array_equal(o0, o1)
+    np.testing.assert_array_equal(r0, r1)
+    np.testing.assert_array_equal(w0, w1)
