@@ -138,6 +138,9 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const flo
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* the encoder the MLP kernels actually run (closed-form OneBlob, f16-rounded), same output format */
 nrc_status nrc_debug_encode_fast(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
+/* encoder variants: 0 = production (as nrc_debug_encode_fast), 1 = omod doubling-chain triangle wave */
+nrc_status nrc_debug_encode_fast_variant(int variant, const float* inputs_d, float* encoded_d, uint32_t n,
+                                         hipStream_t stream);
 
 #ifdef __cplusplus
 }

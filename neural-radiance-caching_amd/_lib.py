@@ -33,6 +33,7 @@ EXPORTS = [
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_get_state", "nrc_set_state", "nrc_get_step", "nrc_set_step",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_encode_fast",
+    "nrc_debug_encode_fast_variant",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame",
@@ -105,6 +106,7 @@ def lib() -> ctypes.CDLL:
         "nrc_debug_infer_variant": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_train_stamps": (st, [vp, fp, fp, u32, vp]),
         "nrc_debug_encode_fast": (st, [fp, fp, u32, vp]),
+        "nrc_debug_encode_fast_variant": (st, [ctypes.c_int, fp, fp, u32, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

@@ -566,4 +566,13 @@ nrc_status nrc_debug_encode_fast(const float* in, float* enc, uint32_t n, hipStr
     });
 }
 
+nrc_status nrc_debug_encode_fast_variant(int variant, const float* in, float* enc, uint32_t n, hipStream_t stream) {
+    return guarded([&] {
+        if (variant != 0 && variant != 1) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "encoder variant must be 0 or 1");
+        if (n == 0) return;
+        if (!in || !enc) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
+        HIP_CHECK(launch_encode_fast(in, enc, n, stream, variant == 1));
+    });
+}
+
 }  // extern "C"

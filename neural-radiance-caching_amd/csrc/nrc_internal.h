@@ -53,12 +53,12 @@ __host__ __device__ constexpr int k0_feature(int K) {
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s);
-constexpr int kNumInferVariants = 22;
+constexpr int kNumInferVariants = 23;
 // inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
-hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s);
+hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, bool chain = false);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,

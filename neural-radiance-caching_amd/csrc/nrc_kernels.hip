@@ -269,16 +269,35 @@ __device__ __forceinline__ float tri_fast(float u) {
     return fabsf(fmaf(__builtin_amdgcn_fractf(u), 2.0f, -1.0f));
 }
 
-// 2 * frac(x) via v_fract_f32's mul:2 output modifier — does NOT give 2*frac(x) on gfx950 (see CHAIN).
+// Output modifiers (omod mul:2) are ignored by the hardware while MODE.IEEE is set or f32 output denormals are
+// enabled (both are the HIP kernel defaults), which is why the CHAIN encoder failed on hardware. A kernel that
+// uses it first clears MODE.IEEE (bit 9) and switches MODE.FP_DENORM[f32] (bits 5:4) to "allow input denormals,
+// flush output denormals". Inference results are unchanged: every f32 value that could be flushed (< 1.2e-38)
+// becomes the same f16 anyway, and the only min/max in the kernel (v_pk_max_f16 ReLU against 0) returns the
+// non-NaN operand for a quiet NaN in both modes.
+__device__ __forceinline__ void fp32_flush_output_denorms() {
+    __builtin_amdgcn_s_setreg((1 << 11) | (4 << 6) | 1 /* hwreg(HW_REG_MODE, 4, 2) */, 1u);
+    __builtin_amdgcn_s_setreg((0 << 11) | (9 << 6) | 1 /* hwreg(HW_REG_MODE, 9, 1) = IEEE */, 0u);
+}
+
+// 2 * frac(x) via v_fract_f32's mul:2 output modifier (needs fp32_flush_output_denorms, see above).
 __device__ __forceinline__ float fract2(float x) {
     float r;
     asm("v_fract_f32_e64 %0, %1 mul:2" : "=v"(r) : "v"(x));
     return r;
 }
+// 2 * frac(|x|): the triangle wave is even, tri(-u) = tri(u), and frac of a non-negative value is exact, so the
+// doubling chain started from |x| is exact in every octave (frac(x) of a negative x rounds x + 1, and doubling
+// would amplify that rounding 2^5-fold).
+__device__ __forceinline__ float fract2_abs(float x) {
+    float r;
+    asm("v_fract_f32_e64 %0, |%1| mul:2" : "=v"(r) : "v"(x));
+    return r;
+}
 
 // 40 K slots of lane half h as 20 packed f16 pairs = 5 B fragments (same slot map as encode()).
-// CHAIN (experimental, off): triangle-wave octaves by doubling through v_fract's mul:2 output modifier —
-// wrong on gfx950 hardware (caught by test_encode_fast_parity); the direct form is used.
+// CHAIN: triangle-wave octaves by doubling through v_fract's mul:2 output modifier (1 VALU per octave instead
+// of mul + fract + half an fma); only valid after fp32_flush_output_denorms().
 template <bool CHAIN = false>
 __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
     uint32_t w[20];
@@ -288,7 +307,7 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             float g[6];
-            g[0] = fract2(p[d]);
+            g[0] = fract2_abs(p[d]);
 #pragma unroll
             for (int k = 1; k < 6; ++k) g[k] = fract2(g[k - 1]);
 #pragma unroll
@@ -428,6 +447,9 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
     }
 }
 
+// Encoder option of the production kernels: 16 = omod doubling-chain triangle wave (variant 22).
+constexpr int kDefaultAbl = 16;
+
 // Optional epilogue: accumulate_render_radiance (nrc_helpers.cu:77-129) fused into inference for the render
 // queries [0, n_acc) (EPI = RenderMode Full 0 / CacheOnly 2); their radiance is consumed in registers and never
 // written. Queries [n_acc, n) (the train-suffix ends) are written to out as usual. Same float operations as
@@ -445,6 +467,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
     // ABL & 8: per-wave staging of a tile's 32 x 12-B results so they leave as 24 contiguous 16-B stores
     __shared__ __attribute__((aligned(16))) float ostage[(ABL & 8) ? THREADS / 64 : 1][96];
+    if constexpr ((ABL & 16) != 0) fp32_flush_output_denorms();
     copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
@@ -470,7 +493,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
 #pragma unroll
                 for (int kk = 0; kk < 5; ++kk) x[t][kk] = __builtin_bit_cast(h8, (kk & 1) ? a : b);
             } else {
-                encode_fast(Q[t], h, x[t]);
+                encode_fast<(ABL & 16) != 0>(Q[t], h, x[t]);
             }
         }
         const int64_t ng = g + wstride;
@@ -557,12 +580,12 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
     infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, InferEpilogue{});
 }
 
-// the default inference configuration (variant 3) with the accumulation epilogue
+// the default inference configuration (variant 22) with the accumulation epilogue
 template <int EPI>
 __global__ __launch_bounds__(512, 4) void infer_accumulate_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                                   int64_t n, const h8* __restrict__ wf,
                                                                   InferEpilogue epi) {
-    infer_v2_body<1, 512, false, 0, EPI>(q, out, n, wf, epi);
+    infer_v2_body<1, 512, false, kDefaultAbl, EPI>(q, out, n, wf, epi);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -830,22 +853,27 @@ __global__ void encode_kernel(const float* __restrict__ q, float* __restrict__ e
 
 // The production encoder (encode_fast: f16 B fragments) unpacked to canonical order as f32 — lets the
 // parity tests check the exact code path the MLP kernels run.
+template <bool CHAIN>
 __global__ void encode_fast_kernel(const float* __restrict__ q, float* __restrict__ enc, int64_t n) {
+    if (CHAIN) fp32_flush_output_denorms();
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t s = gid >> 1;
     const int h = (int)(gid & 1);
     if (s >= n) return;
     const QLane Q = load_q(q, s, h);
     h8 x[5];
-    encode_fast(Q, h, x);
+    encode_fast<CHAIN>(Q, h, x);
 #pragma unroll
     for (int k = 0; k < 40; ++k) enc[s * NRC_ENC_WIDTH + slot_feature(k, h)] = (float)x[k >> 3][k & 7];
 }
 
-hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s) {
+hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, bool chain) {
     if (n <= 0) return hipSuccess;
     const int grid = (int)((2 * n + 255) / 256);
-    hipLaunchKernelGGL(encode_fast_kernel, dim3(grid), dim3(256), 0, s, queries, enc, n);
+    if (chain)
+        hipLaunchKernelGGL(encode_fast_kernel<true>, dim3(grid), dim3(256), 0, s, queries, enc, n);
+    else
+        hipLaunchKernelGGL(encode_fast_kernel<false>, dim3(grid), dim3(256), 0, s, queries, enc, n);
     return hipGetLastError();
 }
 
@@ -1296,7 +1324,9 @@ static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc,
 //   4: v2, 1 tile, next-layer fragment prefetch, 3 waves per SIMD
 //   5: v2, 1 tile, 512-thread blocks, 4 waves per SIMD, prefetch
 //   6: v2, 2 tiles, 512-thread blocks, 2 waves per SIMD, prefetch
-static int g_default_infer_variant = 3;
+//   7-9, 14-16: ablations (timing only); 10-13: v3 register-resident weights; 17-20: v4 asm prefetch
+//   21: variant 3 + LDS-staged 16-B result stores;  22: variant 3 + omod doubling-chain encoder (default)
+static int g_default_infer_variant = 22;  // variant 3 + omod doubling-chain encoder (A/B: 91.4 vs 93.7 us)
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s) {
@@ -1321,6 +1351,8 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 16: return launch_persistent_infer(infer_kernel_v2<2, 2, 256, false, 7>, 256, bpc[16], pairs, queries, out, n, wf, s);
         // v2 variant 3 with LDS-staged coalesced 16-B result stores
         case 21: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 8>, 512, bpc[21], ntiles, queries, out, n, wf, s);
+        // v2 variant 3 with the omod doubling-chain triangle wave (f32 output denormals flushed)
+        case 22: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 16>, 512, bpc[22], ntiles, queries, out, n, wf, s);
         // v4: explicit layer-ahead weight prefetch
         case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
         case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);

@@ -114,9 +114,9 @@ class Network:
         if h is not None and h.value:
             try:
                 self._lib.nrc_free(h)
-            except Exception:
+                self._h = ctypes.c_void_p()
+            except Exception:  # interpreter shutdown: module globals may already be gone
                 pass
-            self._h = ctypes.c_void_p()
 
     # ---- hot path ----------------------------------------------------------------------------
     def train(self, inputs, targets, stream=None, loss: bool = False):

@@ -22,3 +22,27 @@ static_assert(sizeof(nrc_training_record) == 28, "TrainingRecord");
 static_assert(sizeof(nrc_train_suffix_end_vertex) == 16, "TrainingSuffixEndVertex");
 static_assert(sizeof(nrc_frame_buffers) == 13 * sizeof(void*), "nrc_frame_buffers");
 static_assert(sizeof(nrc_frame_params) == 40, "nrc_frame_params");
+
+// the one-call frame and the recorder at the reference's dump point, as a renderer writes them.
+#include "nrc/stream.h"
+float frame_call(nrc::Network& net, const nrc_frame_buffers& fb, uint32_t screen, uint32_t tiles, int32_t records,
+                 nrc_stream* recorder, hipStream_t stream) {
+    const void* sec[NRC_SEC_COUNT] = {};
+    sec[NRC_SEC_QUERIES_INFERENCE] = fb.queries_inference_d;
+    sec[NRC_SEC_END_VERTICES] = fb.end_vertices_d;
+    sec[NRC_SEC_TRAIN_RECORDS] = fb.train_records_d;
+    nrc_stream_frame_header h{};
+    h.screen_size = screen;
+    h.num_tiles = tiles;
+    h.num_training_records = records;
+    (void)nrc_stream_write_frame(recorder, &h, sec, stream);
+    nrc_frame_params p{};
+    p.screen_size = screen;
+    p.num_tiles = tiles;
+    p.num_training_records = records;
+    p.render_mode = NRC_RENDER_FULL;
+    p.train = 1;
+    float loss = 0.0f;
+    (void)nrc_process_frame(net.handle(), &fb, &p, &loss);
+    return loss;
+}

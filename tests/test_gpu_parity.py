@@ -67,15 +67,17 @@ def test_encode_parity(nrc, orc, torch, dev, golden):
         np.testing.assert_allclose(enc.cpu().numpy(), orc.encode(q_np), rtol=0, atol=4e-6)
 
 
-def test_encode_fast_parity(nrc, orc, torch, dev, golden):
-    """The encoder inside the MLP kernels (closed-form OneBlob, doubling-chain triangle wave, f16
-    packing) against the oracle's tcnn-literal encoding rounded to f16: every feature of every query
+@pytest.mark.parametrize("encoder", [0, 1])
+def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
+    """The encoder inside the MLP kernels (closed-form OneBlob, direct (0) or omod doubling-chain (1) triangle
+    wave, f16 packing) against the oracle's tcnn-literal encoding rounded to f16: every feature of every query
     within one f16 ulp (plus 2e-6 absolute for the f32 evaluation-order differences)."""
     L = nrc._lib.lib()
     for q_np in [golden["queries"], golden["queries_edge"], nrc.synthetic.cornell_queries(20000, seed=22)]:
         n = q_np.shape[0]
         enc = torch.zeros((n, 80), dtype=torch.float32, device=dev)
-        nrc._lib.check(L.nrc_debug_encode_fast(to_dev(torch, dev, q_np).data_ptr(), enc.data_ptr(), n, None))
+        nrc._lib.check(L.nrc_debug_encode_fast_variant(encoder, to_dev(torch, dev, q_np).data_ptr(), enc.data_ptr(),
+                                                       n, None))
         torch.cuda.synchronize()
         ref = orc.encode(q_np).astype(np.float16).astype(np.float32)
         got = enc.cpu().numpy()
@@ -84,7 +86,7 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21, 22])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every production-eligible kernel variant at sizes
     that exercise partial tiles / single blocks."""
