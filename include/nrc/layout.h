@@ -79,6 +79,33 @@ typedef struct nrc_float3 { float x, y, z; } nrc_float3;
 #define NRC_W5_OFFSET   (NRC_W4_OFFSET + NRC_WIDTH * NRC_WIDTH)       /* 21504 */
 #define NRC_NUM_PARAMS  (NRC_W5_OFFSET + NRC_OUT_PADDED * NRC_WIDTH)  /* 22528 */
 
+/* ---- Hash-config model shape (NRCNetworkConfigs.h:84-128) ----
+ * Composite encoding: HashGrid(dims 0-2: 16 levels x 2 features, log2 hashmap 15, base resolution 16,
+ * per-level scale 2) -> 32, OneBlob(dims 3-8, 4 bins) -> 24, Identity(dims 9-14) -> 6; 62 features padded
+ * with 1.0 to 64. Level l: scale = 16 * 2^l - 1, resolution = 16 * 2^l; entries = min(resolution^3, 2^15)
+ * (levels 0, 1 dense: 4096 and 32768 entries; levels 2..15 hashed: 32768 each). */
+#define NRC_HASH_LEVELS        16
+#define NRC_HASH_FEATURES      2
+#define NRC_HASH_LOG2_T        15
+#define NRC_HASH_T             (1 << NRC_HASH_LOG2_T)
+#define NRC_HASH_BASE_RES      16
+#define NRC_HASH_ENC_REAL      (NRC_HASH_LEVELS * NRC_HASH_FEATURES + NRC_BLOB_DIMS * NRC_BLOB_BINS + NRC_IDENT_DIMS) /* 62 */
+#define NRC_HASH_ENC_WIDTH     64
+#define NRC_HASH_ENTRIES       (4096 + (NRC_HASH_LEVELS - 1) * NRC_HASH_T)          /* 495616 */
+#define NRC_HASH_GRID_PARAMS   (NRC_HASH_ENTRIES * NRC_HASH_FEATURES)               /* 991232 */
+/* parameter blob of the Hash config: MLP W0[64][64], W1..W4[64][64], W5[16][64] (matrix params, Adam with
+ * l2), then the grid table [entry][feature] (non-matrix params: sparse Adam, no l2) */
+#define NRC_HASH_W0_OFFSET     0
+#define NRC_HASH_W1_OFFSET     (NRC_HASH_W0_OFFSET + NRC_WIDTH * NRC_HASH_ENC_WIDTH)  /* 4096  */
+#define NRC_HASH_W5_OFFSET     (NRC_HASH_W1_OFFSET + 4 * NRC_WIDTH * NRC_WIDTH)       /* 20480 */
+#define NRC_HASH_MLP_PARAMS    (NRC_HASH_W5_OFFSET + NRC_OUT_PADDED * NRC_WIDTH)      /* 21504 */
+#define NRC_HASH_GRID_OFFSET   NRC_HASH_MLP_PARAMS
+#define NRC_HASH_NUM_PARAMS    (NRC_HASH_MLP_PARAMS + NRC_HASH_GRID_PARAMS)           /* 1012736 */
+/* first table entry of level l */
+#define NRC_HASH_LEVEL_ENTRY_OFFSET(l) ((l) == 0 ? 0 : 4096 + ((l) - 1) * NRC_HASH_T)
+#define NRC_HASH_PRIME1 2654435761u /* tcnn coherent prime hash: x * 1 ^ y * 2654435761 ^ z * 805459861 */
+#define NRC_HASH_PRIME2 805459861u
+
 /* tcnn defaults used by the Frequency config (survey Appendix A.7-A.8). */
 #define NRC_LOSS_SCALE     128.0f
 #define NRC_ADAM_BETA1     0.9f

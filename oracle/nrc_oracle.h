@@ -70,6 +70,18 @@ void orc_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n);
 void orc_permute(const float* q_src, const float* t_src, const int32_t* perm, uint64_t seed, uint32_t frame,
                  int32_t num_records, float* q_dst, float* t_dst, uint32_t n_out);
 
+/* ---- InputEncoding::Hash model (nrc_hash_oracle.c; NRCNetworkConfigs.h:84-128) ----
+ * params: NRC_HASH_NUM_PARAMS f32 = MLP (W0[64][64] ...) then the grid table [entry][2]. */
+void orc_hash_encode(const float* params, const float* queries, int64_t n, int mode, float* enc /* n x 64 */);
+void orc_hash_forward(const float* params, const float* queries, int64_t n, int mode, float* out, int nthreads);
+double orc_hash_grad(const float* params, const float* queries, const float* targets, int64_t b, double n_total,
+                     float loss_scale, int mode, float* grad, int nthreads);
+void orc_hash_adam_ema(float* params, float* m, float* v, float* ema, float* infer_params, uint32_t* grid_steps,
+                       uint32_t step, const float* grad, float loss_scale, float lr, float beta1, float beta2,
+                       float eps, float l2_reg, float ema_decay);
+void orc_hash_init_params(float* params, uint64_t seed);
+void orc_hash_corners(const float* q, int level, uint32_t* entries, float* weights);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,13 @@ def lib() -> ctypes.CDLL:
         L.orc_feistel_keys.argtypes = [u64, u32, vp]
         L.orc_permutation.argtypes = [u64, u32, vp, u32]
         L.orc_permute.argtypes = [vp, vp, vp, u64, u32, ctypes.c_int32, vp, vp, u32]
+        L.orc_hash_encode.argtypes = [vp, vp, i64, ctypes.c_int, vp]
+        L.orc_hash_forward.argtypes = [vp, vp, i64, ctypes.c_int, vp, ctypes.c_int]
+        L.orc_hash_grad.restype = ctypes.c_double
+        L.orc_hash_grad.argtypes = [vp, vp, vp, i64, ctypes.c_double, ctypes.c_float, ctypes.c_int, vp, ctypes.c_int]
+        L.orc_hash_adam_ema.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp] + [ctypes.c_float] * 7
+        L.orc_hash_init_params.argtypes = [vp, u64]
+        L.orc_hash_corners.argtypes = [vp, ctypes.c_int, vp, vp]
         _lib = L
     return _lib
 
@@ -174,3 +181,75 @@ def permute(q_src: np.ndarray, t_src: np.ndarray, perm, seed: int, frame: int, n
     lib().orc_permute(_v(qs), _v(ts), None if pp is None else _v(pp), int(seed), int(frame), int(num_records),
                       _v(qd), _v(td), int(n_out))
     return qd, td
+
+
+# ---- InputEncoding::Hash model (oracle/nrc_hash_oracle.c) --------------------------------------------
+HASH_MLP_PARAMS = 21504
+HASH_GRID_PARAMS = 991232
+HASH_NUM_PARAMS = HASH_MLP_PARAMS + HASH_GRID_PARAMS
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def hash_init_params(seed: int = 1337) -> np.ndarray:
+    p = np.empty(HASH_NUM_PARAMS, dtype=np.float32)
+    lib().orc_hash_init_params(_v(p), seed)
+    return p
+
+
+def hash_encode(params, queries, mode: int = MIXED) -> np.ndarray:
+    q, p = _f32(queries), _f32(params)
+    out = np.zeros((q.shape[0], 64), np.float32)
+    if q.shape[0]:
+        lib().orc_hash_encode(_v(p), _v(q), q.shape[0], mode, _v(out))
+    return out
+
+
+def hash_forward(params, queries, mode: int = MIXED, threads: int | None = None) -> np.ndarray:
+    q, p = _f32(queries), _f32(params)
+    out = np.zeros((q.shape[0], 3), np.float32)
+    if q.shape[0]:
+        lib().orc_hash_forward(_v(p), _v(q), q.shape[0], mode, _v(out), threads or default_threads())
+    return out
+
+
+def hash_grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, threads=None):
+    q, t, p = _f32(queries), _f32(targets), _f32(params)
+    b = q.shape[0]
+    g = np.zeros(HASH_NUM_PARAMS, np.float32)
+    loss = lib().orc_hash_grad(_v(p), _v(q), _v(t), b, float(3.0 * b if n_total is None else n_total),
+                               float(loss_scale), mode, _v(g), threads or default_threads())
+    return g, float(loss)
+
+
+def hash_corners(query, level: int):
+    q = _f32(query).reshape(15)
+    e = np.zeros(8, np.uint32)
+    w = np.zeros(8, np.float32)
+    lib().orc_hash_corners(_v(q), level, _v(e), _v(w))
+    return e, w
+
+
+class HashAdamEmaState:
+    """tcnn Adam (matrix part with l2, sparse non-matrix grid part with per-entry steps) + EMA."""
+
+    def __init__(self, params, lr=1e-2, beta1=0.9, beta2=0.999, eps=1e-15, l2_reg=1e-6, ema_decay=0.99,
+                 loss_scale=128.0):
+        self.params = np.array(params, dtype=np.float32)
+        self.m = np.zeros_like(self.params)
+        self.v = np.zeros_like(self.params)
+        self.ema = np.zeros_like(self.params)
+        self.infer = self.params.copy()
+        self.grid_steps = np.zeros(HASH_GRID_PARAMS, np.uint32)
+        self.step = 0
+        self.hp = (lr, beta1, beta2, eps, l2_reg, ema_decay)
+        self.loss_scale = loss_scale
+
+    def apply(self, g) -> None:
+        self.step += 1
+        g = _f32(g)
+        lr, b1, b2, eps, l2, dec = self.hp
+        lib().orc_hash_adam_ema(_v(self.params), _v(self.m), _v(self.v), _v(self.ema), _v(self.infer),
+                                _v(self.grid_steps), self.step, _v(g), self.loss_scale, lr, b1, b2, eps, l2, dec)
