@@ -119,7 +119,10 @@ nrc_status nrc_train_grad(nrc_net* net, const float* inputs_d, const float* targ
                           uint32_t global_b, float* grad_d);
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h);
 
-/* ---- state access (host buffers of NRC_NUM_PARAMS f32; synchronous) ---- */
+/* ---- state access (host buffers of nrc_get_num_params() f32; synchronous) ----
+ * Frequency: NRC_NUM_PARAMS (layout.h canonical blob). Hash: NRC_HASH_NUM_PARAMS = MLP blob then the grid table
+ * [entry][2] (the grid's per-entry Adam step counters are internal). */
+nrc_status nrc_get_num_params(const nrc_net* net, uint64_t* n);
 nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst);
 nrc_status nrc_set_state(nrc_net* net, int slot, const float* host_src);
 nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
@@ -138,6 +141,9 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const flo
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* the encoder the MLP kernels actually run (closed-form OneBlob, f16-rounded), same output format */
 nrc_status nrc_debug_encode_fast(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
+/* InputEncoding::Hash: the production Composite{HashGrid, OneBlob, Identity} encoder with the inference (EMA)
+ * grid table, f32 [n][64] canonical order */
+nrc_status nrc_debug_encode_hash(nrc_net* net, const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* encoder variants: 0 = production (as nrc_debug_encode_fast), 1 = omod doubling-chain triangle wave */
 nrc_status nrc_debug_encode_fast_variant(int variant, const float* inputs_d, float* encoded_d, uint32_t n,
                                          hipStream_t stream);

@@ -54,10 +54,32 @@ void init_params(std::vector<float>& p, uint64_t seed) {
     }
 }
 
+// Hash config (oracle/nrc_hash_oracle.c orc_hash_init_params): the same xavier stream over the 64-wide layer 0,
+// grid uniform in [-1e-4, 1e-4] from a second pcg32 stream [M].
+void init_params_hash(std::vector<float>& p, uint64_t seed) {
+    const int in[NRC_NUM_LAYERS] = {NRC_HASH_ENC_WIDTH, 64, 64, 64, 64, 64};
+    const int off[NRC_NUM_LAYERS] = {NRC_HASH_W0_OFFSET, NRC_HASH_W1_OFFSET, NRC_HASH_W1_OFFSET + 4096,
+                                     NRC_HASH_W1_OFFSET + 8192, NRC_HASH_W1_OFFSET + 12288, NRC_HASH_W5_OFFSET};
+    Pcg32 rng(seed, 0xda3e39cb94b95bdbULL);
+    for (int l = 0; l < NRC_NUM_LAYERS; ++l) {
+        const float scale = std::sqrt(6.0f / (float)(in[l] + kLayerOut[l]));
+        for (int i = 0; i < in[l] * kLayerOut[l]; ++i) p[off[l] + i] = (rng.next_float() * 2.0f - 1.0f) * scale;
+    }
+    Pcg32 g(seed, 0x9e3779b97f4a7c15ULL);
+    for (int i = 0; i < NRC_HASH_GRID_PARAMS; ++i) p[NRC_HASH_GRID_OFFSET + i] = (g.next_float() * 2.0f - 1.0f) * 1e-4f;
+}
+
 // Position of every canonical parameter inside the forward / backward MFMA fragment images.
-void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd) {
-    fwd.assign(NRC_NUM_PARAMS, -1);
-    bwd.assign(NRC_NUM_PARAMS, -1);
+void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd, int encoding) {
+    const bool hash = encoding == NRC_ENCODING_HASH;
+    const int n = hash ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS;
+    const int in0 = hash ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH;
+    int off[NRC_NUM_LAYERS];
+    for (int l = 0; l < NRC_NUM_LAYERS; ++l)
+        off[l] = hash ? (l == 0 ? NRC_HASH_W0_OFFSET : l <= 4 ? NRC_HASH_W1_OFFSET + (l - 1) * 4096 : NRC_HASH_W5_OFFSET)
+                      : kLayerOff[l];
+    fwd.assign(n, -1);
+    bwd.assign(n, -1);
     // inverse of acc_row over (kk, h, j) for a 64-feature axis
     int row_kk[64], row_h[64], row_j[64];
     for (int kk = 0; kk < 4; ++kk)
@@ -70,26 +92,31 @@ void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd) {
             }
     int f_kk[NRC_ENC_WIDTH], f_h[NRC_ENC_WIDTH], f_j[NRC_ENC_WIDTH];
     for (int h = 0; h < 2; ++h)
-        for (int n = 0; n < 40; ++n) {
-            const int f = slot_feature(n, h);
-            f_kk[f] = n / 8;
+        for (int sn = 0; sn < (hash ? 32 : 40); ++sn) {
+            const int f = hash ? hash_slot_feature(sn, h) : slot_feature(sn, h);
+            f_kk[f] = sn / 8;
             f_h[f] = h;
-            f_j[f] = n % 8;
+            f_j[f] = sn % 8;
         }
     auto pos = [](int frag, int lane, int j) { return frag * kFragHalves + lane * 8 + j; };
     for (int o = 0; o < 64; ++o)
-        for (int f = 0; f < NRC_ENC_WIDTH; ++f)
-            fwd[NRC_W0_OFFSET + o * NRC_ENC_WIDTH + f] = pos(fwd_frag(0, o / 32, f_kk[f]), o % 32 + 32 * f_h[f], f_j[f]);
+        for (int f = 0; f < in0; ++f) {
+            const int p = off[0] + o * in0 + f;
+            fwd[p] = pos(fwd_frag(0, o / 32, f_kk[f]), o % 32 + 32 * f_h[f], f_j[f]);
+            // Hash: W0^T for the 32 grid features, rows permuted (hash_dx_row), k order = delta_0's acc_row order
+            if (hash && f < 2 * NRC_HASH_LEVELS)
+                bwd[p] = pos(kBwdFrags + row_kk[o], hash_dx_row(f) + 32 * row_h[o], row_j[o]);
+        }
     for (int l = 1; l <= 4; ++l)
         for (int o = 0; o < 64; ++o)
             for (int i = 0; i < 64; ++i) {
-                const int p = kLayerOff[l] + o * 64 + i;
+                const int p = off[l] + o * 64 + i;
                 fwd[p] = pos(fwd_frag(l, o / 32, row_kk[i]), o % 32 + 32 * row_h[i], row_j[i]);
                 bwd[p] = pos(bwd_frag(l, i / 32, row_kk[o]), i % 32 + 32 * row_h[o], row_j[o]);
             }
     for (int o = 0; o < NRC_OUT_PADDED; ++o)
         for (int i = 0; i < 64; ++i) {
-            const int p = NRC_W5_OFFSET + o * 64 + i;
+            const int p = off[5] + o * 64 + i;
             fwd[p] = pos(fwd_frag(5, 0, row_kk[i]), o + 32 * row_h[i], row_j[i]);
             // W5^T: rows acc_row(0, h, j) in [0,16) index the output neuron o
             bwd[p] = pos(bwd_frag(5, i / 32, 0), i % 32 + 32 * row_h[o], row_j[o]);
@@ -143,6 +170,14 @@ struct nrc_net {
     float* grad = nullptr;  // kGradFloats scratch for the fused path
     float* loss_dev = nullptr;
     float* loss_host = nullptr;  // pinned
+    // InputEncoding::Hash: grid part of the model arrays starts at n_mlp
+    int n_mlp = NRC_NUM_PARAMS, n_grid = 0;
+    float* grid_grad = nullptr;
+    uint32_t* grid_steps = nullptr;
+    _Float16 *table_train = nullptr, *table_infer = nullptr;
+
+    bool hash() const { return encoding == NRC_ENCODING_HASH; }
+    size_t n_total() const { return (size_t)n_mlp + (size_t)n_grid; }
 
     void release() {
         auto f = [](void* p) {
@@ -152,6 +187,10 @@ struct nrc_net {
         f(wf_train); f(wb_train); f(wf_infer);
         f(fwd_pos); f(bwd_pos);
         f(slabs); f(loss_partials); f(grad); f(loss_dev);
+        f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
+        grid_grad = nullptr;
+        grid_steps = nullptr;
+        table_train = table_infer = nullptr;
         if (loss_host) (void)hipHostFree(loss_host);
         params = m = v = ema = infer = nullptr;
         wf_train = wb_train = wf_infer = nullptr;
@@ -166,7 +205,16 @@ struct nrc_net {
         b.params = params; b.m = m; b.v = v; b.ema = ema; b.infer = infer;
         b.wf_train = wf_train; b.wb_train = wb_train; b.wf_infer = wf_infer;
         b.fwd_pos = fwd_pos; b.bwd_pos = bwd_pos;
+        b.n_mlp = n_mlp;
         return b;
+    }
+    GridBuffers grid_buffers() const {
+        GridBuffers g;
+        g.params = params + n_mlp; g.m = m + n_mlp; g.v = v + n_mlp; g.ema = ema + n_mlp; g.infer = infer + n_mlp;
+        g.grad = grid_grad; g.steps = grid_steps;
+        g.table_train = table_train; g.table_infer = table_infer;
+        g.n = n_grid;
+        return g;
     }
     OptimArgs optim(uint32_t s) const {
         OptimArgs o;
@@ -181,7 +229,7 @@ struct nrc_net {
         slabs = nullptr;
         loss_partials = nullptr;
         slab_blocks = 0;
-        HIP_CHECK(hipMalloc(&slabs, sizeof(float) * (size_t)blocks * NRC_NUM_PARAMS));
+        HIP_CHECK(hipMalloc(&slabs, sizeof(float) * (size_t)blocks * n_mlp));
         HIP_CHECK(hipMalloc(&loss_partials, sizeof(float) * (size_t)blocks));
         slab_blocks = blocks;
     }
@@ -196,12 +244,13 @@ void check_live(const nrc_net* net) {
 }
 
 void upload_all(nrc_net* net, const std::vector<float>& params, const std::vector<float>& infer) {
-    HIP_CHECK(hipMemcpy(net->params, params.data(), sizeof(float) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
-    HIP_CHECK(hipMemcpy(net->infer, infer.data(), sizeof(float) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(net->params, params.data(), sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(net->infer, infer.data(), sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
 }
 
 void repack(nrc_net* net, hipStream_t s) {
     HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
+    if (net->hash()) HIP_CHECK(launch_grid_adam(kPackOnly, net->grid_buffers(), net->optim(1), s));
 }
 
 void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h, float* loss_d = nullptr) {
@@ -210,16 +259,32 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
     const int blocks = train_blocks(b);
     net->ensure_slabs(blocks);
-    HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                   net->slabs, net->loss_partials, net->stream));
+    if (net->hash())
+        HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                    net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream));
+    else
+        HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                       net->slabs, net->loss_partials, net->stream));
     net->step += 1;
     HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
                                  loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
+    if (net->hash()) HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
     if (loss_h) {
         HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
         HIP_CHECK(hipStreamSynchronize(net->stream));
         *loss_h = *net->loss_host;
     }
+}
+
+hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
+    if (net->hash())
+        return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
+    return launch_infer(in, out, n, net->wf_infer, net->stream);
+}
+
+void require_frequency(const nrc_net* net, const char* what) {
+    if (net->hash())
+        throw ApiError(NRC_ERR_UNSUPPORTED, std::string(what) + " is implemented for InputEncoding::Frequency only");
 }
 
 float* slot_ptr(nrc_net* net, int slot) {
@@ -281,8 +346,6 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
         if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
-        if (encoding == NRC_ENCODING_HASH)
-            throw ApiError(NRC_ERR_UNSUPPORTED, "InputEncoding::Hash is not implemented yet (SURVEY §8(f) row 3)");
         net->release();
         net->stream = stream;
         net->encoding = encoding;
@@ -290,17 +353,28 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         net->destroyed = false;
         net->step = 0;
         HIP_CHECK(hipGetDevice(&net->device));
-        const size_t pb = sizeof(float) * NRC_NUM_PARAMS;
+        net->n_mlp = net->hash() ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS;
+        net->n_grid = net->hash() ? NRC_HASH_GRID_PARAMS : 0;
+        const size_t pb = sizeof(float) * net->n_total();
         HIP_CHECK(hipMalloc(&net->params, pb));
         HIP_CHECK(hipMalloc(&net->m, pb));
         HIP_CHECK(hipMalloc(&net->v, pb));
         HIP_CHECK(hipMalloc(&net->ema, pb));
         HIP_CHECK(hipMalloc(&net->infer, pb));
         HIP_CHECK(hipMalloc(&net->wf_train, sizeof(_Float16) * kFwdHalves));
-        HIP_CHECK(hipMalloc(&net->wb_train, sizeof(_Float16) * kBwdHalves));
+        HIP_CHECK(hipMalloc(&net->wb_train, sizeof(_Float16) * kBwdHalvesHash));
         HIP_CHECK(hipMalloc(&net->wf_infer, sizeof(_Float16) * kFwdHalves));
-        HIP_CHECK(hipMalloc(&net->fwd_pos, sizeof(int) * NRC_NUM_PARAMS));
-        HIP_CHECK(hipMalloc(&net->bwd_pos, sizeof(int) * NRC_NUM_PARAMS));
+        HIP_CHECK(hipMalloc(&net->fwd_pos, sizeof(int) * net->n_mlp));
+        HIP_CHECK(hipMalloc(&net->bwd_pos, sizeof(int) * net->n_mlp));
+        if (net->hash()) {
+            const size_t ng = (size_t)net->n_grid;
+            HIP_CHECK(hipMalloc(&net->grid_grad, sizeof(float) * ng));
+            HIP_CHECK(hipMalloc(&net->grid_steps, sizeof(uint32_t) * ng));
+            HIP_CHECK(hipMalloc(&net->table_train, sizeof(_Float16) * ng));
+            HIP_CHECK(hipMalloc(&net->table_infer, sizeof(_Float16) * ng));
+            HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(float) * ng));
+            HIP_CHECK(hipMemset(net->grid_steps, 0, sizeof(uint32_t) * ng));
+        }
         HIP_CHECK(hipMalloc(&net->grad, sizeof(float) * kGradFloats));
         HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
         HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
@@ -308,15 +382,16 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemset(net->v, 0, pb));
         HIP_CHECK(hipMemset(net->ema, 0, pb));
         HIP_CHECK(hipMemset(net->wf_train, 0, sizeof(_Float16) * kFwdHalves));
-        HIP_CHECK(hipMemset(net->wb_train, 0, sizeof(_Float16) * kBwdHalves));
+        HIP_CHECK(hipMemset(net->wb_train, 0, sizeof(_Float16) * kBwdHalvesHash));
         HIP_CHECK(hipMemset(net->wf_infer, 0, sizeof(_Float16) * kFwdHalves));
         HIP_CHECK(hipMemset(net->loss_dev, 0, sizeof(float) * 4));
         std::vector<int> fwd, bwd;
-        build_scatter_maps(fwd, bwd);
-        HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
-        HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
-        std::vector<float> p(NRC_NUM_PARAMS);
-        init_params(p, net->cfg.seed);
+        build_scatter_maps(fwd, bwd, net->encoding);
+        HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
+        std::vector<float> p(net->n_total());
+        if (net->hash()) init_params_hash(p, net->cfg.seed);
+        else init_params(p, net->cfg.seed);
         upload_all(net, p, p);  // before the first step inference uses the initial weights
         net->initialized = true;
         repack(net, nullptr);
@@ -375,8 +450,12 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
         if (num_pixels > 0 && (!thr || !rgba || (reinterpret_cast<uintptr_t>(rgba) & 15)))
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "throughput / 16-byte aligned float4 frame buffer required");
         const float w = 1.0f / (float)(iteration_index + 1u);  // nrc_helpers.cu:98
-        HIP_CHECK(launch_infer_accumulate(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba,
-                                          num_pixels, mode, w, net->stream));
+        if (net->hash())
+            HIP_CHECK(launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, reinterpret_cast<const float*>(thr),
+                                        rgba, num_pixels, mode, w, net->stream));
+        else
+            HIP_CHECK(launch_infer_accumulate(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba,
+                                              num_pixels, mode, w, net->stream));
     });
 }
 
@@ -385,7 +464,7 @@ nrc_status nrc_infer(nrc_net* net, const float* in, float* out, uint32_t n) {
         check_live(net);
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
-        HIP_CHECK(launch_infer(in, out, n, net->wf_infer, net->stream));
+        HIP_CHECK(infer_any(net, in, out, n));
     });
 }
 
@@ -395,7 +474,7 @@ nrc_status nrc_infer_stream(nrc_net* net, const float* in, float* out, uint32_t 
         net->stream = stream;
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
-        HIP_CHECK(launch_infer(in, out, n, net->wf_infer, net->stream));
+        HIP_CHECK(infer_any(net, in, out, n));
     });
 }
 
@@ -458,6 +537,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
                           float* grad_d) {
     return guarded([&] {
         check_live(net);
+        require_frequency(net, "nrc_train_grad");
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
         if (b == 0) {
@@ -477,6 +557,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
     return guarded([&] {
         check_live(net);
+        require_frequency(net, "nrc_train_apply");
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         net->step += 1;
         HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
@@ -495,7 +576,7 @@ nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst) {
         if (!host_dst) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null destination");
         float* src = slot_ptr(net, slot);
         HIP_CHECK(hipStreamSynchronize(net->stream));
-        HIP_CHECK(hipMemcpy(host_dst, src, sizeof(float) * NRC_NUM_PARAMS, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(host_dst, src, sizeof(float) * net->n_total(), hipMemcpyDeviceToHost));
     });
 }
 
@@ -505,11 +586,29 @@ nrc_status nrc_set_state(nrc_net* net, int slot, const float* host_src) {
         if (!host_src) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null source");
         float* dst = slot_ptr(net, slot);
         HIP_CHECK(hipStreamSynchronize(net->stream));
-        HIP_CHECK(hipMemcpy(dst, host_src, sizeof(float) * NRC_NUM_PARAMS, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy(dst, host_src, sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
         if (slot == NRC_STATE_PARAMS || slot == NRC_STATE_INFER) {
             repack(net, net->stream);
             HIP_CHECK(hipStreamSynchronize(net->stream));
         }
+    });
+}
+
+nrc_status nrc_get_num_params(const nrc_net* net, uint64_t* n) {
+    return guarded([&] {
+        check_live(net);
+        if (!n) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output pointer");
+        *n = net->n_total();
+    });
+}
+
+nrc_status nrc_debug_encode_hash(nrc_net* net, const float* in, float* enc, uint32_t n, hipStream_t stream) {
+    return guarded([&] {
+        check_live(net);
+        if (!net->hash()) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "network is not configured with InputEncoding::Hash");
+        if (n == 0) return;
+        if (!in || !enc) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
+        HIP_CHECK(launch_encode_hash(in, net->table_infer, enc, n, stream));
     });
 }
 
@@ -532,6 +631,7 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
                                    hipStream_t stream) {
     return guarded([&] {
         check_live(net);
+        require_frequency(net, "nrc_debug_infer_variant");
         if (variant < 0 || variant >= kNumInferVariants) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown variant");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
@@ -542,6 +642,7 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint64_t* stamps_d) {
     return guarded([&] {
         check_live(net);
+        require_frequency(net, "nrc_debug_train_stamps");
         if (!in || !tgt || !stamps_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);

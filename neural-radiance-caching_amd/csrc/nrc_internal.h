@@ -44,6 +44,26 @@ __host__ __device__ constexpr int slot_feature(int n, int h) {
            : n < 33 ? 60 + 3 * h + (n - 30)
                     : 66 + (n - 33) + 7 * h;
 }
+// Hash config (64-wide input): 32 slots per lane half: 16 HashGrid features (levels 8h..8h+7), 12 OneBlob
+// (dims 3+3h..5+3h), 3 Identity, 1 pad.
+__host__ __device__ constexpr int hash_slot_feature(int n, int h) {
+    return n < 16   ? 16 * h + n
+           : n < 28 ? 32 + (3 * h + (n - 16) / 4) * 4 + (n - 16) % 4
+           : n < 31 ? 56 + 3 * h + (n - 28)
+                    : 62 + h;
+}
+__host__ __device__ constexpr int hash_k0_feature(int K) {
+    return hash_slot_feature(8 * (K >> 4) + (K & 7), (K >> 3) & 1);
+}
+// Backward image of the Hash config: 4 extra fragments (kBwdFrags .. +3) hold W0^T for the 32 grid features,
+// M rows permuted so that accumulator register r of lane half h is grid feature 16h + r:
+// row m <-> feature 16*((m>>2)&1) + 4*(m>>3) + (m&3).
+constexpr int kBwdFragsHash = kBwdFrags + 4;
+constexpr int kBwdHalvesHash = kBwdFragsHash * kFragHalves;
+__host__ __device__ constexpr int hash_dx_row(int feature) {
+    return (feature & 3) + 4 * (feature >> 4) + 8 * ((feature >> 2) & 3);
+}
+
 // K index (column of the layer-0 MFMA, 0..79) -> canonical feature.
 __host__ __device__ constexpr int k0_feature(int K) {
     return slot_feature(8 * (K >> 4) + (K & 7), (K >> 3) & 1);
@@ -57,6 +77,10 @@ constexpr int kNumInferVariants = 23;
 // inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
+// InputEncoding::Hash inference (mode -1: plain; 0 / 2: fused accumulation for queries [0, n_acc))
+hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
+                             const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
+hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, bool chain = false);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
@@ -78,7 +102,20 @@ struct ModelBuffers {
     float *params, *m, *v, *ema, *infer;  // f32 master / Adam / EMA / debiased EMA (inference)
     _Float16 *wf_train, *wb_train, *wf_infer;
     const int *fwd_pos, *bwd_pos;
+    int n_mlp;  // MLP (matrix) parameter count = slab stride: 22528 Frequency, 21504 Hash
 };
+// HashGrid parameters (the grid part of the model arrays) and their optimizer state
+struct GridBuffers {
+    float *params, *m, *v, *ema, *infer;
+    float* grad;      // f32 [n], accumulated by the training kernel, zeroed by grid_adam_kernel
+    uint32_t* steps;  // per-entry Adam step counters
+    _Float16 *table_train, *table_infer;
+    int n;
+};
+hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
+hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                             const _Float16* wf, const _Float16* wb, const _Float16* grid, float* grid_grad,
+                             float* slabs, float* loss_partials, hipStream_t s);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);

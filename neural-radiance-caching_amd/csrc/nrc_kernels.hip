@@ -334,6 +334,96 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// HashGrid (InputEncoding::Hash, NRCNetworkConfigs.h:94-103; spec in oracle/nrc_hash_oracle.c): lane half h
+// encodes levels 8h..8h+7 of its query. Table: f16 [entry][2] (one 4-B half2 gather per corner).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+struct HashCorners {
+    uint32_t entry[8];  // global table entries
+    float w[8];         // trilinear weights, tcnn order ((1 * wx) * wy) * wz
+};
+
+// tcnn pos_fract + grid_index for level l. DENSE_OK: the level may be dense (l <= 1 possible); dense = l <= 1.
+template <bool DENSE_OK>
+__device__ __forceinline__ void hash_corners(float px, float py, float pz, int l, HashCorners& C) {
+    const float scale = (float)(16 << l) - 1.0f;  // exact: 16 * 2^l - 1 < 2^24
+    const uint32_t res = 16u << l;
+    const float xs[3] = {px, py, pz};
+    float fr[3];
+    uint32_t cell[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float pos = __builtin_fmaf(scale, xs[d], 0.5f);
+        const float fl = floorf(pos);
+        cell[d] = (uint32_t)(int)fl;
+        fr[d] = pos - fl;
+    }
+    const bool dense = DENSE_OK && l <= 1;
+    const uint32_t mask = l == 0 ? 4095u : 32767u;
+    const uint32_t off = l == 0 ? 0u : 4096u + (uint32_t)(l - 1) * 32768u;
+    // per-dimension corner terms: dense x + y*res + z*res^2, hashed x ^ y*P1 ^ z*P2 (uint32 wrap-around)
+    const uint32_t ym = dense ? res : NRC_HASH_PRIME1, zm = dense ? res * res : NRC_HASH_PRIME2;
+    const uint32_t X[2] = {cell[0], cell[0] + 1u};
+    const uint32_t Y[2] = {cell[1] * ym, cell[1] * ym + ym};
+    const uint32_t Z[2] = {cell[2] * zm, cell[2] * zm + zm};
+    const float wx[2] = {1.0f - fr[0], fr[0]}, wy[2] = {1.0f - fr[1], fr[1]}, wz[2] = {1.0f - fr[2], fr[2]};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+        uint32_t i;
+        if (DENSE_OK)
+            i = dense ? X[bx] + Y[by] + Z[bz] : X[bx] ^ Y[by] ^ Z[bz];
+        else
+            i = X[bx] ^ Y[by] ^ Z[bz];
+        C.entry[c] = (i & mask) + off;
+        C.w[c] = (wx[bx] * wy[by]) * wz[bz];
+    }
+}
+
+// One level's two features as a packed half2: tcnn kernel_grid result = fma((half)w, value, result), corners 0..7.
+template <bool DENSE_OK>
+__device__ __forceinline__ uint32_t hash_level_feature(float px, float py, float pz, int l,
+                                                        const uint32_t* __restrict__ table) {
+    HashCorners C;
+    hash_corners<DENSE_OK>(px, py, pz, l, C);
+    uint32_t v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = table[C.entry[c]];
+    h2v acc = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        // (half)weight must be rounded before the FMA: the launder stops the compiler from folding the f32->f16
+        // conversion into a mixed-precision v_fma_mix (which would skip that rounding)
+        uint32_t w2 = pk2(C.w[c], C.w[c]);
+        asm volatile("" : "+v"(w2));
+        acc = __builtin_elementwise_fma(__builtin_bit_cast(h2v, w2), __builtin_bit_cast(h2v, v[c]), acc);
+    }
+    return __builtin_bit_cast(uint32_t, acc);
+}
+
+// 32 K slots of lane half h (see hash_slot_feature): 8 hash levels (16 features), 3 OneBlob dims, 3 identity,
+// one pad; as 4 B fragments.
+__device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_t* __restrict__ table, h8 (&x)[4]) {
+    uint32_t w[16];
+    w[0] = hash_level_feature<true>(Q.p0, Q.p1, Q.p2, 8 * h + 0, table);
+    w[1] = hash_level_feature<true>(Q.p0, Q.p1, Q.p2, 8 * h + 1, table);
+#pragma unroll
+    for (int i = 2; i < 8; ++i) w[i] = hash_level_feature<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, table);
+    blob_fast(Q.b0, w[8], w[9]);
+    blob_fast(Q.b1, w[10], w[11]);
+    blob_fast(Q.b2, w[12], w[13]);
+    w[14] = pk2(Q.i0, Q.i1);
+    w[15] = pk2(Q.i2, 1.0f);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
+        x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
 template <int ABL = 0>
 __device__ __forceinline__ h8 relu_h8(const f16v& a, int base) {
     h8 r;
@@ -393,10 +483,11 @@ __device__ __forceinline__ void layer_mfma(const h8 (&a)[2][KK], const h8 (&in)[
 
 // PREFETCH: issue layer l+1's weight-fragment reads before layer l's MFMAs (double-buffered
 // fragment registers) instead of at the head of layer l+1.
-template <int TILES, bool PREFETCH, int ABL = 0>
-__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][5], f16v (&o)[TILES]) {
+template <int TILES, bool PREFETCH, int ABL = 0, int KK0 = 5>
+__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][KK0], f16v (&o)[TILES]) {
+    static_assert(KK0 == 5 || !PREFETCH, "the prefetch schedule is written for the 80-wide input layer");
     h8 y[TILES][4], z[TILES][4];
-    if (PREFETCH) {
+    if constexpr (PREFETCH) {
         h8 a0[2][5];
         load_frags<5>(lw_lane, 0, a0);
         h8 aA[2][4], aB[2][4];
@@ -421,9 +512,9 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
             for (int t = 0; t < TILES; ++t) o[t] = mfma(a5[kk], y[t][kk], o[t]);
     } else {
         {
-            h8 a0[2][5];
-            load_frags<5, ABL>(lw_lane, 0, a0);
-            layer_mfma<TILES, 5, ABL>(a0, x, y);
+            h8 a0[2][KK0];
+            load_frags<KK0, ABL>(lw_lane, 0, a0);
+            layer_mfma<TILES, KK0, ABL>(a0, x, y);
         }
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
@@ -461,9 +552,12 @@ struct InferEpilogue {
     float w;           // 1 / (iterationIndex + 1)
 };
 
-template <int TILES, int THREADS, bool PREFETCH, int ABL, int EPI>
+// ENC: 0 = Frequency composite (80-wide input), 1 = Hash composite (64-wide; grid = f16x2 table)
+template <int TILES, int THREADS, bool PREFETCH, int ABL, int EPI, int ENC = 0>
 __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float* __restrict__ out, int64_t n,
-                                              const h8* __restrict__ wf, const InferEpilogue& epi) {
+                                              const h8* __restrict__ wf, const InferEpilogue& epi,
+                                              const uint32_t* __restrict__ grid = nullptr) {
+    constexpr int KK0 = ENC == 1 ? 4 : 5;
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
     // ABL & 8: per-wave staging of a tile's 32 x 12-B results so they leave as 24 contiguous 16-B stores
     __shared__ __attribute__((aligned(16))) float ostage[(ABL & 8) ? THREADS / 64 : 1][96];
@@ -484,10 +578,12 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
 #pragma unroll
     for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
     for (; g < ngroups; g += wstride) {
-        h8 x[TILES][5];
+        h8 x[TILES][KK0];
 #pragma unroll
         for (int t = 0; t < TILES; ++t) {
-            if (ABL & 1) {
+            if constexpr (ENC == 1) {
+                encode_hash(Q[t], h, grid, x[t]);
+            } else if constexpr ((ABL & 1) != 0) {
                 typedef float f4 __attribute__((ext_vector_type(4)));
                 const f4 a = {Q[t].p0, Q[t].p1, Q[t].b0, Q[t].b1}, b = {Q[t].b2, Q[t].i0, Q[t].i1, Q[t].i2};
 #pragma unroll
@@ -518,7 +614,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             }
         }
         f16v o[TILES];
-        mlp_tiles<TILES, PREFETCH, ABL & 7>((lds_h8*)(lw + lane), x, o);
+        mlp_tiles<TILES, PREFETCH, ABL & 7, KK0>((lds_h8*)(lw + lane), x, o);
         if constexpr ((ABL & 8) && EPI < 0) {
             const int64_t s0 = g * TILES * 32;
             if (out16 && s0 + TILES * 32 <= n) {
@@ -586,6 +682,28 @@ __global__ __launch_bounds__(512, 4) void infer_accumulate_kernel(const float* _
                                                                   int64_t n, const h8* __restrict__ wf,
                                                                   InferEpilogue epi) {
     infer_v2_body<1, 512, false, kDefaultAbl, EPI>(q, out, n, wf, epi);
+}
+
+// InputEncoding::Hash inference (EPI -1: plain infer; 0 / 2: fused accumulation as above)
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                            int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
+                                                            const uint32_t* __restrict__ grid) {
+    infer_v2_body<1, 512, false, 0, EPI, 1>(q, out, n, wf, epi, grid);
+}
+
+// The production hash encoder unpacked to canonical order as f32 (parity tests): [n][64].
+__global__ void encode_hash_kernel(const float* __restrict__ q, const uint32_t* __restrict__ grid,
+                                   float* __restrict__ enc, int64_t n) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = gid >> 1;
+    const int h = (int)(gid & 1);
+    if (s >= n) return;
+    const QLane Q = load_q(q, s, h);
+    h8 x[4];
+    encode_hash(Q, h, grid, x);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) enc[s * NRC_HASH_ENC_WIDTH + hash_slot_feature(k, h)] = (float)x[k >> 3][k & 7];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -940,13 +1058,25 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 constexpr int kLdsWf = kFwdHalves * 2;   // 47104
-constexpr int kLdsWb = kBwdHalves * 2;   // 34816
+constexpr int kLdsWb = kBwdHalvesHash * 2;  // 38912 (the Frequency config uses the first 34816)
 constexpr int kLdsImg = 128 * 128;       // 16384
 constexpr int kLdsXhi = 128 * 32;        // 4096
 constexpr int kLdsTrain = kLdsWf + kLdsWb + 4 * kLdsImg + kLdsXhi + 16;
 
+// canonical offset of W_L in the parameter blob of encoding ENC (layout.h)
+template <int L, int ENC>
+__host__ __device__ constexpr int w_offset() {
+    return ENC == 1 ? (L == 0 ? NRC_HASH_W0_OFFSET : L <= 4 ? NRC_HASH_W1_OFFSET + (L - 1) * 4096 : NRC_HASH_W5_OFFSET)
+                    : (L == 0   ? NRC_W0_OFFSET
+                       : L == 1 ? NRC_W1_OFFSET
+                       : L == 2 ? NRC_W2_OFFSET
+                       : L == 3 ? NRC_W3_OFFSET
+                       : L == 4 ? NRC_W4_OFFSET
+                                : NRC_W5_OFFSET);
+}
+
 // dW output block (mb, nb) of layer L: A = delta image (features = output rows), B = activation image.
-template <int L>
+template <int L, int ENC = 0>
 __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, const char* img_xh, int mb, int nb,
                                          int lane, float* __restrict__ slab) {
     f16v acc = zero16();
@@ -956,22 +1086,21 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
         h8 A = tr_frag(img_d, mb, kk, lane);
         if (zero_a) A = h8{};
         h8 B;
-        if (L == 0 && nb == 2) B = tr_frag_xhi(img_xh, kk, lane);
+        if (ENC == 0 && L == 0 && nb == 2) B = tr_frag_xhi(img_xh, kk, lane);
         else B = tr_frag(img_a, nb, kk, lane);
         acc = mfma(A, B, acc);
     }
     const int h = lane >> 5, col = 32 * nb + (lane & 31);
-    constexpr int in_dim = (L == 0) ? NRC_ENC_WIDTH : NRC_WIDTH;
-    constexpr int off = L == 0 ? NRC_W0_OFFSET
-                        : L == 1 ? NRC_W1_OFFSET
-                        : L == 2 ? NRC_W2_OFFSET
-                        : L == 3 ? NRC_W3_OFFSET
-                        : L == 4 ? NRC_W4_OFFSET
-                                 : NRC_W5_OFFSET;
+    constexpr int in_dim = (L == 0) ? (ENC == 1 ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH) : NRC_WIDTH;
+    constexpr int off = w_offset<L, ENC>();
     int fcol = col;
     if (L == 0) {
-        if (col >= NRC_ENC_WIDTH) return;
-        fcol = k0_feature(col);
+        if (ENC == 1) {
+            fcol = hash_k0_feature(col);
+        } else {
+            if (col >= NRC_ENC_WIDTH) return;
+            fcol = k0_feature(col);
+        }
     }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -981,16 +1110,16 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
     }
 }
 
-template <int L>
+template <int L, int ENC = 0>
 __device__ __forceinline__ void dw_layer(const char* img_d, const char* img_a, const char* img_xh, int wave, int lane,
                                          float* __restrict__ slab) {
     if (L == 5) {
-        if (wave < 2) dw_block<5>(img_d, img_a, img_xh, 0, wave, lane, slab);
-    } else if (L == 0) {
+        if (wave < 2) dw_block<5, ENC>(img_d, img_a, img_xh, 0, wave, lane, slab);
+    } else if (L == 0 && ENC == 0) {
         dw_block<0>(img_d, img_a, img_xh, wave / 3, wave % 3, lane, slab);
         if (wave < 2) dw_block<0>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane, slab);
     } else {
-        dw_block<L>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane, slab);
+        dw_block<L, ENC>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane, slab);
     }
 }
 
@@ -1011,12 +1140,19 @@ __device__ __forceinline__ void bwd_chain(const h8* __restrict__ lwb, const h8 (
 
 // STAMP (diagnostic build only): wave 0 of every block records s_memtime at phase boundaries into
 // stamps[block][16]; the product instantiation (STAMP = false) executes no stamp.
-template <bool STAMP>
+// ENC 1 (InputEncoding::Hash): 64-wide layer 0, grid table `grid` (f16x2, training weights); the grid-feature
+// gradient W0^T delta_0 is scattered into grid_grad (f32 [entry][2]) with atomics.
+template <bool STAMP, int ENC = 0>
 __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                        int64_t b, float n_total, float loss_scale,
                                                        const h8* __restrict__ wf, const h8* __restrict__ wb,
                                                        float* __restrict__ slabs, float* __restrict__ loss_partials,
-                                                       uint64_t* __restrict__ stamps) {
+                                                       uint64_t* __restrict__ stamps,
+                                                       const uint32_t* __restrict__ grid = nullptr,
+                                                       float* __restrict__ grid_grad = nullptr) {
+    constexpr int KK0 = ENC == 1 ? 4 : 5;
+    constexpr int NBF = ENC == 1 ? kBwdFragsHash : kBwdFrags;
+    constexpr int SLAB = ENC == 1 ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS;
     int nst = 0;
     auto stamp = [&]() {
         if (STAMP) {
@@ -1038,7 +1174,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     float* red = (float*)(img_xh + kLdsXhi);
 
     // weight images: issue every global load first, encode while they fly, then store to LDS
-    constexpr int PF = (kFwdFrags * 64 + 255) / 256, PB = (kBwdFrags * 64 + 255) / 256;
+    constexpr int PF = (kFwdFrags * 64 + 255) / 256, PB = (NBF * 64 + 255) / 256;
     h8 vf[PF], vb[PB];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
@@ -1048,7 +1184,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 #pragma unroll
     for (int k = 0; k < PB; ++k) {
         const int i = threadIdx.x + k * 256;
-        if (i < kBwdFrags * 64) vb[k] = wb[i];
+        if (i < NBF * 64) vb[k] = wb[i];
     }
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1064,8 +1200,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         tgt[1] = t[sc * 3 + 1];
         tgt[2] = t[sc * 3 + 2];
     }
-    h8 x[5];
-    encode_fast(Q, h, x);
+    h8 x[KK0];
+    if constexpr (ENC == 1) encode_hash(Q, h, grid, x);
+    else encode_fast(Q, h, x);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int i = threadIdx.x + k * 256;
@@ -1074,7 +1211,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 #pragma unroll
     for (int k = 0; k < PB; ++k) {
         const int i = threadIdx.x + k * 256;
-        if (i < kBwdFrags * 64) lwb[i] = vb[k];
+        if (i < NBF * 64) lwb[i] = vb[k];
     }
     lds_barrier();  // weights in LDS
     stamp();
@@ -1082,11 +1219,13 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     h8 a[5][4];
     {
         lds_h8* wl = (lds_h8*)(lwf + lane);
-        h8 w0[2][5];
-        load_frags<5>(wl, 0, w0);
-        h8 xx[1][5] = {{x[0], x[1], x[2], x[3], x[4]}};
+        h8 w0[2][KK0];
+        load_frags<KK0>(wl, 0, w0);
+        h8 xx[1][KK0];
+#pragma unroll
+        for (int kk = 0; kk < KK0; ++kk) xx[0][kk] = x[kk];
         h8 yy[1][4];
-        layer_mfma<1, 5>(w0, xx, yy);
+        layer_mfma<1, KK0>(w0, xx, yy);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) a[0][kk] = yy[0][kk];
 #pragma unroll
@@ -1124,7 +1263,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     for (int off = 32; off > 0; off >>= 1) lossv += __shfl_xor(lossv, off);
     if (lane == 0) red[wave] = lossv;
 
-    float* slab = slabs + (int64_t)blockIdx.x * NRC_NUM_PARAMS;
+    float* slab = slabs + (int64_t)blockIdx.x * SLAB;
 
     // layer 5 operands (buffer 1): delta_5 = g (16 rows, k-step 0 only), a_5
 #pragma unroll
@@ -1140,25 +1279,25 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     bwd_chain<5>(lwb, g, a[4], lane, d4);
     write_rows64(img_d[0], sl, h, d4);
     write_rows64(img_a[0], sl, h, a[3]);
-    dw_layer<5>(img_d[1], img_a[1], img_xh, wave, lane, slab);
+    dw_layer<5, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
     bwd_chain<4>(lwb, d4, a[3], lane, d3);
     write_rows64(img_d[1], sl, h, d3);
     write_rows64(img_a[1], sl, h, a[2]);
-    dw_layer<4>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    dw_layer<4, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
     bwd_chain<3>(lwb, d3, a[2], lane, d2);
     write_rows64(img_d[0], sl, h, d2);
     write_rows64(img_a[0], sl, h, a[1]);
-    dw_layer<3>(img_d[1], img_a[1], img_xh, wave, lane, slab);
+    dw_layer<3, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
     bwd_chain<2>(lwb, d2, a[1], lane, d1);
     write_rows64(img_d[1], sl, h, d1);
     write_rows64(img_a[1], sl, h, a[0]);
-    dw_layer<2>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    dw_layer<2, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
     bwd_chain<1>(lwb, d1, a[0], lane, d0);
@@ -1168,11 +1307,34 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
         for (int jg = 0; jg < 2; ++jg) store_h4(img_a[0], img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
-    *(h8*)(img_xh + sl * 32 + 16 * h) = x[4];
-    dw_layer<1>(img_d[1], img_a[1], img_xh, wave, lane, slab);
+    if constexpr (ENC == 0) *(h8*)(img_xh + sl * 32 + 16 * h) = x[KK0 - 1];
+    if constexpr (ENC == 1) {
+        // dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample sl, then the trilinear scatter (tcnn
+        // kernel_grid_backward): grad[entry][f] += w_corner * dy_f. The atomics drain while dW runs.
+        f16v c = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) c = mfma(lwb[(kBwdFrags + kk) * 64 + lane], d0[kk], c);
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float dy0 = (float)(_Float16)c[2 * i], dy1 = (float)(_Float16)c[2 * i + 1];
+                if (dy0 == 0.0f && dy1 == 0.0f) continue;
+                HashCorners C;
+                if (i <= 1) hash_corners<true>(Q.p0, Q.p1, Q.p2, 8 * h + i, C);
+                else hash_corners<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, C);
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    float* gp = grid_grad + 2 * (size_t)C.entry[cc];
+                    if (dy0 != 0.0f) unsafeAtomicAdd(gp, C.w[cc] * dy0);
+                    if (dy1 != 0.0f) unsafeAtomicAdd(gp + 1, C.w[cc] * dy1);
+                }
+            }
+        }
+    }
+    dw_layer<1, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
-    dw_layer<0>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     stamp();
 }
 
@@ -1184,7 +1346,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 // bitwise reproducible for a given slab count.
 constexpr int kRedParams = 64, kRedGroups = 16, kRedThreads = kRedParams * kRedGroups;
 constexpr int kRedVec = 4;  // floats per thread: one 16-byte load per slab
-static_assert(NRC_NUM_PARAMS % (kRedParams * 4) == 0, "parameter count must tile the reduction");
+static_assert(NRC_NUM_PARAMS % (kRedParams * 4) == 0 && NRC_HASH_MLP_PARAMS % (kRedParams * 4) == 0,
+              "parameter counts must tile the reduction");
 
 __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const ModelBuffers& mb, const OptimArgs& oa,
                                               float lr_t, float ema_debias) {
@@ -1234,10 +1397,10 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
             for (int i = 0; i < nslabs; ++i) L += loss_partials[i];
-            if (mode == kReduceOnly) grad_io[NRC_NUM_PARAMS] = L;
+            if (mode == kReduceOnly) grad_io[mb.n_mlp] = L;
             else if (loss_out) loss_out[0] = L;
         } else if (mode == kApplyOnly && loss_out) {
-            loss_out[0] = grad_io[NRC_NUM_PARAMS];
+            loss_out[0] = grad_io[mb.n_mlp];
         }
     }
     if (mode == kReduceFused || mode == kReduceOnly) {
@@ -1247,7 +1410,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             f4 v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                v[u] = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)(i + u * kRedGroups) * NRC_NUM_PARAMS + p0]);
+                v[u] = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)(i + u * kRedGroups) * mb.n_mlp + p0]);
 #pragma unroll
             for (int u = 0; u < 8; u += 2) {
                 a0 += v[u];
@@ -1255,7 +1418,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             }
         }
         for (int u = 0; i < nslabs; i += kRedGroups, ++u) {
-            const f4 v = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)i * NRC_NUM_PARAMS + p0]);
+            const f4 v = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)i * mb.n_mlp + p0]);
             if (u & 1) a1 += v;
             else a0 += v;
         }
@@ -1371,6 +1534,28 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s);
 }
 
+hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
+                             const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t ntiles = (n + 31) / 32;
+    static int bpc[3] = {};
+    const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
+    switch (mode) {
+        case -1: return launch_persistent_infer(infer_hash_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi, g);
+        case 0: return launch_persistent_infer(infer_hash_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi, g);
+        case 2: return launch_persistent_infer(infer_hash_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi, g);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float* enc, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(encode_hash_kernel, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, s, queries,
+                       reinterpret_cast<const uint32_t*>(grid), enc, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -1412,13 +1597,66 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
     return hipGetLastError();
 }
 
+// Sparse Adam + EMA + f16 table packs for the HashGrid parameters (tcnn non-matrix params, SURVEY §8(f) row 3;
+// oracle/nrc_hash_oracle.c orc_hash_adam_ema): an entry whose gradient is exactly zero keeps its moments, weight
+// and step counter; bias correction uses the entry's own step. The gradient is zeroed for the next step.
+__global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= gb.n) return;
+    float w = gb.params[i], inf;
+    if (mode == kPackOnly) {
+        inf = gb.infer[i];
+    } else {
+        const float gradient = gb.grad[i] / oa.loss_scale;
+        gb.grad[i] = 0.0f;
+        if (gradient != 0.0f) {
+            const uint32_t st = gb.steps[i] + 1u;
+            gb.steps[i] = st;
+            const float lr_i = oa.lr * sqrtf(1.0f - powf(oa.beta2, (float)st)) / (1.0f - powf(oa.beta1, (float)st));
+            const float gsq = gradient * gradient;
+            const float m1 = oa.beta1 * gb.m[i] + (1.0f - oa.beta1) * gradient;
+            const float v1 = oa.beta2 * gb.v[i] + (1.0f - oa.beta2) * gsq;
+            gb.m[i] = m1;
+            gb.v[i] = v1;
+            const float eff = lr_i / (sqrtf(v1) + oa.eps);
+            w = w - eff * m1;
+            gb.params[i] = w;
+        }
+        const float e = gb.ema[i] * oa.ema_decay + w * (1.0f - oa.ema_decay);
+        gb.ema[i] = e;
+        inf = e / ema_debias;
+        gb.infer[i] = inf;
+    }
+    gb.table_train[i] = (_Float16)w;
+    gb.table_infer[i] = (_Float16)inf;
+}
+
+hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s) {
+    const float step = (float)(oa.step ? oa.step : 1);
+    const float ema_debias = 1.0f - powf(oa.ema_decay, step);
+    hipLaunchKernelGGL(grid_adam_kernel, dim3((unsigned)((gb.n + 255) / 256)), dim3(256), 0, s, mode, gb, oa,
+                       ema_debias);
+    return hipGetLastError();
+}
+
+hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                             const _Float16* wf, const _Float16* wb, const _Float16* grid, float* grid_grad,
+                             float* slabs, float* loss_partials, hipStream_t s) {
+    if (b <= 0) return hipSuccess;
+    hipLaunchKernelGGL((train_kernel<false, 1>), dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
+                       loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
+                       reinterpret_cast<const uint32_t*>(grid), grid_grad);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials, float* grad_io,
                               float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
     // Bias corrections in host f32 (glibc powf/sqrtf), identical to the oracle's.
     const float step = (float)(oa.step ? oa.step : 1);
     const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
     const float ema_debias = 1.0f - powf(oa.ema_decay, step);
-    const int grid = NRC_NUM_PARAMS / (kRedParams * kRedVec);
+    const int grid = mb.n_mlp / (kRedParams * kRedVec);
     hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
                        loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();

@@ -194,16 +194,29 @@ class Network:
         check(self._lib.nrc_train_apply(self._h, _dev_ptr(grad, "grad"), ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
+    @property
+    def num_params(self) -> int:
+        """Parameter count of the configured model (Frequency 22,528; Hash 21,504 MLP + 991,232 grid)."""
+        v = ctypes.c_uint64()
+        check(self._lib.nrc_get_num_params(self._h, ctypes.byref(v)))
+        return v.value
+
     def get_state(self, slot: StateSlot = StateSlot.PARAMS) -> np.ndarray:
-        out = np.empty(NUM_PARAMS, dtype=np.float32)
+        out = np.empty(self.num_params, dtype=np.float32)
         check(self._lib.nrc_get_state(self._h, int(slot), out.ctypes.data))
         return out
 
     def set_state(self, slot: StateSlot, values) -> None:
         v = np.ascontiguousarray(values, dtype=np.float32)
-        if v.size != NUM_PARAMS:
-            raise ValueError(f"state must have {NUM_PARAMS} floats")
+        n = self.num_params
+        if v.size != n:
+            raise ValueError(f"state must have {n} floats")
         check(self._lib.nrc_set_state(self._h, int(slot), v.ctypes.data))
+
+    def encode_hash(self, inputs, encoded, n: int, stream=None) -> None:
+        """InputEncoding::Hash: the production encoder (inference grid table), f32 [n][64] canonical order."""
+        check(self._lib.nrc_debug_encode_hash(self._h, _dev_ptr(inputs, "inputs"), _dev_ptr(encoded, "encoded"),
+                                              int(n), _stream_ptr(stream)))
 
     @property
     def step(self) -> int:

@@ -69,6 +69,20 @@ static void level_corners(int l, const float x[3], uint32_t idx[8], float w[8]) 
     }
 }
 
+/* Round-to-nearest-even of a double straight to the nearest f16 value (no intermediate f32 rounding, which
+ * could double-round): scale to the f16 ulp of |x|, nearbyint (RNE in the default mode), scale back. */
+float orc_f16_round_double(double x) {
+    if (x != x || x == 0.0) return (float)x;
+    const double ax = fabs(x);
+    int e;
+    frexp(ax, &e);                      /* ax = m * 2^e, m in [0.5, 1) */
+    int ulp_exp = (e - 1) - 10;         /* f16 has 10 fraction bits */
+    if (ulp_exp < -24) ulp_exp = -24;   /* subnormal f16 spacing */
+    const double r = ldexp(nearbyint(ldexp(x, -ulp_exp)), ulp_exp);
+    if (fabs(r) > 65504.0) return x > 0 ? INFINITY : -INFINITY;
+    return (float)r;
+}
+
 /* Grid table as the forward sees it (f16-rounded in MIXED / TCNN). */
 static float* grid_view(const float* grid, int mode) {
     float* t = (float*)malloc(sizeof(float) * NRC_HASH_GRID_PARAMS);
@@ -91,7 +105,7 @@ static void encode_one(const float* table, const float* q, int mode, float* enc)
             } else { /* half fma: the product of two halves and a half addend are exact in f64, one rounding */
                 float acc = 0.0f;
                 for (int c = 0; c < 8; ++c)
-                    acc = orc_f16_round((float)((double)orc_f16_round(w[c]) * (double)T[2 * idx[c] + f] + (double)acc));
+                    acc = orc_f16_round_double((double)orc_f16_round(w[c]) * (double)T[2 * idx[c] + f] + (double)acc);
                 enc[2 * l + f] = acc;
             }
         }

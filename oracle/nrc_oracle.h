@@ -81,6 +81,8 @@ void orc_hash_adam_ema(float* params, float* m, float* v, float* ema, float* inf
                        float eps, float l2_reg, float ema_decay);
 void orc_hash_init_params(float* params, uint64_t seed);
 void orc_hash_corners(const float* q, int level, uint32_t* entries, float* weights);
+/* round a double straight to the nearest f16 (RNE), as a half-precision FMA does */
+float orc_f16_round_double(double x);
 
 #ifdef __cplusplus
 }

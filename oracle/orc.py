@@ -57,6 +57,8 @@ def lib() -> ctypes.CDLL:
         L.orc_hash_adam_ema.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp] + [ctypes.c_float] * 7
         L.orc_hash_init_params.argtypes = [vp, u64]
         L.orc_hash_corners.argtypes = [vp, ctypes.c_int, vp, vp]
+        L.orc_f16_round_double.restype = ctypes.c_float
+        L.orc_f16_round_double.argtypes = [ctypes.c_double]
         _lib = L
     return _lib
 

@@ -291,7 +291,7 @@ def test_training_is_deterministic(nrc, torch, dev, golden):
 def test_error_behaviour(nrc, torch, dev):
     n = nrc.Network()
     with pytest.raises(nrc.NrcError):
-        n.init(encoding=nrc.InputEncoding.Hash)  # not implemented yet: reported, not silent
+        n.init(encoding=7)  # Unsupported input encoding: std::invalid_argument in the reference
     n.init(stream=torch.cuda.current_stream())
     with pytest.raises(ValueError):
         n.infer(None, None, 4)

@@ -132,3 +132,17 @@ def test_hash_sparse_adam(orc):
     st.apply(g2)
     assert np.all(st.params[:21504] != params[:21504])
     assert st.grid_steps[10] == 1  # zero gradient: no step for the grid entry
+
+
+def test_f16_round_double_matches_numpy(orc):
+    """The half-FMA emulation rounds the exact f64 result straight to f16 (numpy's float64 -> float16 is direct)."""
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=20000) * np.exp(rng.uniform(-25, 11, 20000))
+    # ties and near-ties of the f16 grid, which an f32 intermediate can double-round
+    base = rng.uniform(-2, 2, 2000).astype(np.float16).astype(np.float64)
+    x = np.concatenate([x, base + 2.0 ** -12 * np.sign(base), base + 2.0 ** -12 * np.sign(base) + 2.0 ** -40])
+    L = orc.lib()
+    got = np.array([L.orc_f16_round_double(float(v)) for v in x], np.float32)
+    with np.errstate(over="ignore"):
+        ref = x.astype(np.float16).astype(np.float32)
+    np.testing.assert_array_equal(got, ref)
