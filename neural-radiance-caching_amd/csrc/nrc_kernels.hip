@@ -1308,15 +1308,23 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 #pragma unroll
         for (int jg = 0; jg < 2; ++jg) store_h4(img_a[0], img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
     if constexpr (ENC == 0) *(h8*)(img_xh + sl * 32 + 16 * h) = x[KK0 - 1];
+    // Grid gradient (Hash): dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample sl, then the trilinear scatter
+    // of tcnn's kernel_grid_backward, grad[entry][f] += w_corner * dy_f. Fine levels (l >= kCoarseLevels) go straight
+    // to f32 global atomics, which drain while dW runs. The coarse levels cover the scene with a handful of cells
+    // (position * 0.005 spans ~1.6 * 2^l cells per axis), so every sample of the batch would hit the same few
+    // entries: they are pre-summed per block in an LDS hash table (below) and flushed with one atomic per entry.
+    constexpr int kCoarseLevels = 5;
+    float dyc[2 * kCoarseLevels] = {};
     if constexpr (ENC == 1) {
-        // dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample sl, then the trilinear scatter (tcnn
-        // kernel_grid_backward): grad[entry][f] += w_corner * dy_f. The atomics drain while dW runs.
         f16v c = zero16();
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) c = mfma(lwb[(kBwdFrags + kk) * 64 + lane], d0[kk], c);
+#pragma unroll
+        for (int k = 0; k < 2 * kCoarseLevels; ++k) dyc[k] = (float)(_Float16)c[k];
         if (valid) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
+                if (h == 0 && i < kCoarseLevels) continue;
                 const float dy0 = (float)(_Float16)c[2 * i], dy1 = (float)(_Float16)c[2 * i + 1];
                 if (dy0 == 0.0f && dy1 == 0.0f) continue;
                 HashCorners C;
@@ -1334,7 +1342,57 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     dw_layer<1, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
-    dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    if constexpr (ENC == 1) {
+        // every wave is past its last weight-image read: the weight region becomes the coarse-level table
+        constexpr int kSlots = 4096;
+        uint32_t* tkey = (uint32_t*)smem;
+        float* tval = (float*)(smem + 4 * kSlots);  // [slot][2]
+        static_assert(12 * kSlots <= kLdsWf + kLdsWb, "coarse-level table must fit the weight-image region");
+        for (int i = threadIdx.x; i < kSlots; i += 256) {
+            tkey[i] = 0xFFFFFFFFu;
+            tval[2 * i] = tval[2 * i + 1] = 0.0f;
+        }
+        dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+        lds_barrier();
+        if (valid && h == 0) {
+#pragma unroll
+            for (int i = 0; i < kCoarseLevels; ++i) {
+                const float dy0 = dyc[2 * i], dy1 = dyc[2 * i + 1];
+                if (dy0 == 0.0f && dy1 == 0.0f) continue;
+                HashCorners C;
+                if (i <= 1) hash_corners<true>(Q.p0, Q.p1, Q.p2, i, C);
+                else hash_corners<false>(Q.p0, Q.p1, Q.p2, i, C);
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    const uint32_t e = C.entry[cc];
+                    uint32_t slot = (e * 2654435761u) >> 20;  // 12-bit multiplicative hash
+                    bool done = false;
+                    for (int probe = 0; probe < 32 && !done; ++probe) {  // bounded: every lane exits
+                        const uint32_t k = atomicCAS(&tkey[slot], 0xFFFFFFFFu, e);
+                        if (k == 0xFFFFFFFFu || k == e) {
+                            atomicAdd(&tval[2 * slot], C.w[cc] * dy0);
+                            atomicAdd(&tval[2 * slot + 1], C.w[cc] * dy1);
+                            done = true;
+                        }
+                        slot = (slot + 1) & (kSlots - 1);
+                    }
+                    if (!done) {  // table crowded: direct global atomics for this corner
+                        unsafeAtomicAdd(grid_grad + 2 * (size_t)e, C.w[cc] * dy0);
+                        unsafeAtomicAdd(grid_grad + 2 * (size_t)e + 1, C.w[cc] * dy1);
+                    }
+                }
+            }
+        }
+        lds_barrier();
+        for (int i = threadIdx.x; i < kSlots; i += 256) {
+            const uint32_t e = tkey[i];
+            if (e == 0xFFFFFFFFu) continue;
+            unsafeAtomicAdd(grid_grad + 2 * (size_t)e, tval[2 * i]);
+            unsafeAtomicAdd(grid_grad + 2 * (size_t)e + 1, tval[2 * i + 1]);
+        }
+    } else {
+        dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+    }
     stamp();
 }
 
