@@ -235,6 +235,14 @@ __device__ __forceinline__ uint32_t pk2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2));  // v_cvt_pk_f16_f32 (RNE)
 }
 
+// pk2(|a|, |b|) with the absolute values as input modifiers of v_cvt_pk_f16_f32 (the compiler otherwise masks the
+// f16 result with a separate v_and).
+__device__ __forceinline__ uint32_t pk2_abs(float a, float b) {
+    uint32_t r;
+    asm("v_cvt_pk_f16_f32 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // OneBlob(4 bins) of one input in closed form. tcnn's formula sums 12 quartic-CDF terms;
 // at most two are unsaturated: with t = 4x, fl = floor(t), fr = t - fl the kernel mass falls into the
 // unit intervals j = fl-1, fl, fl+1 as A, B-A, 1-B (A = K(-fr), B = K(1-fr)); interval j lands in bin
@@ -311,7 +319,7 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
 #pragma unroll
             for (int k = 1; k < 6; ++k) g[k] = fract2(g[k - 1]);
 #pragma unroll
-            for (int k = 0; k < 6; k += 2) w[(d * 6 + k) >> 1] = pk2(fabsf(g[k] - 1.0f), fabsf(g[k + 1] - 1.0f));
+            for (int k = 0; k < 6; k += 2) w[(d * 6 + k) >> 1] = pk2_abs(g[k] - 1.0f, g[k + 1] - 1.0f);
         }
     } else {
 #pragma unroll
