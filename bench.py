@@ -42,10 +42,11 @@ def parse():
     ap.add_argument("--train-frames", type=int, default=20, help="timed frames of 4 x 16384 training")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--frame-iters", type=int, default=20, help="timed 1080p post-trace frames (0: skip)")
     return ap.parse_args()
 
 
-def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float) -> dict:
+def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train_batch) -> dict:
     """The naive C oracle (FP32, scalar loops) on the host cores, bounded sample of the workload."""
     orc = nrc_loader.load_oracle()
     threads = orc.default_threads()
@@ -62,11 +63,56 @@ def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float) -> di
         orc.forward(params, queries[:m], orc.FP32, threads)
         total += m
     dt = time.perf_counter() - t0
+    # the same forward on one thread (bounded sample) and one 16,384-sample train step
+    n1 = 8192
+    t1 = time.perf_counter()
+    orc.forward(params, queries[:n1], orc.FP32, 1)
+    dt1 = time.perf_counter() - t1
+    tq, tt = train_batch
+    t2 = time.perf_counter()
+    g, _ = orc.grad(params, tq, tt, mode=orc.FP32, threads=threads)
+    orc.AdamEmaState(params).apply(g)
+    dt2 = time.perf_counter() - t2
     return {"value": total / dt / 1e6, "unit": "M queries/s", "cores": threads, "kind": "port",
             "sample": f"{total} queries ({total / len(queries):.2f} passes over the {len(queries)}-query "
                       f"Cornell frame), oracle/nrc_oracle.c FP32 forward, "
                       f"{threads} pthreads on {platform.processor() or platform.machine()} "
-                      f"({os.cpu_count()} logical CPUs visible), {dt:.1f} s"}
+                      f"({os.cpu_count()} logical CPUs visible), {dt:.1f} s",
+            "value_1thread": n1 / dt1 / 1e6, "sample_1thread": f"{n1} queries on 1 thread, {dt1:.2f} s",
+            "train_step_ms": dt2 * 1e3,
+            "sample_train": f"one {len(tq)}-sample step: FP32 encode+fwd+loss+bwd ({threads} pthreads) + Adam/EMA"}
+
+
+def frame_bench(nrc, net, dev, iters: int) -> dict:
+    """Wall-clock ms of nrc_process_frame on a synthetic 1920x1080 Cornell frame (8x8 tiles) resident in HBM."""
+    import torch
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(1920, 1080, (8, 8), seed=1)
+    cap = F.NUM_TRAINING_RECORDS_PER_FRAME
+    nrec = min(f.num_training_records, cap)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pad = lambda a, w: np.concatenate([a[:nrec], np.zeros((cap - nrec, w), np.float32)])  # noqa: E731
+    rec = np.zeros(cap, F.TRAINING_RECORD_DTYPE)
+    rec[:nrec] = f.train_records[:nrec]
+    S, T = f.screen_size, f.num_tiles
+    fb = F.FrameBuffers(t(f.queries_inference), torch.zeros((S + T, 3), device=dev), t(f.last_render_throughput),
+                        torch.zeros((S, 4), device=dev), F.records_to_device(f.end_vertices, dev),
+                        F.records_to_device(rec, dev), [t(pad(f.train_queries, 15)), torch.zeros((cap, 15), device=dev)],
+                        [t(pad(f.train_targets, 3)), torch.zeros((cap, 3), device=dev)])
+    state = [net.get_state(s) for s in (nrc.StateSlot.PARAMS, nrc.StateSlot.INFER)]
+    for it in range(3):
+        F.process_frame(net, fb, F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(iters):
+        F.process_frame(net, fb, F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / iters * 1e3
+    for s, v in zip((nrc.StateSlot.PARAMS, nrc.StateSlot.INFER), state):  # leave the network as it was
+        net.set_state(s, v)
+    return {"frame_ms": ms, "queries": S + T, "train_records": f.num_training_records, "iters": iters,
+            "what": "nrc_process_frame: fused infer+accumulate, propagate, Feistel shuffle, 4 x 16384 train with "
+                    "loss read-back; synthetic 1920x1080 Cornell frame, 8x8 tiles"}
 
 
 def pmc_traffic() -> float | None:
@@ -168,6 +214,12 @@ def main() -> None:
     train_frame_ms = float(tw.item()) / args.train_frames * 1e3
     train_step_ms = train_frame_ms / 4
 
+    # ---- one whole post-trace frame: fused infer+accumulate over the 1080p frame's
+    # render + train-suffix queries, propagate, shuffle, 4 x train with the minibatch-loss read-back (1 GPU)
+    frame = None
+    if world == 1 and args.frame_iters > 0:
+        frame = frame_bench(nrc, net, dev, args.frame_iters)
+
     achieved = FLOP_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e12
     result = {
         "metric": "M radiance queries/sec + train-step ms, 64x5 MLP @ 2M samples/frame",
@@ -190,6 +242,7 @@ def main() -> None:
         "train_step_ms": train_step_ms,
         "train_frame_ms": train_frame_ms,
         "infer_kernel_ms": kernel_ms,
+        "frame": frame,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F16_TFLOPS, "traffic": pmc_traffic(),
                      "algorithmic_bytes_per_launch": BYTES_PER_QUERY * nq,
@@ -198,7 +251,8 @@ def main() -> None:
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         params = net.get_state(nrc.StateSlot.INFER)
-        result["cpu_baseline"] = cpu_baseline(q_np, params, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(q_np, params, args.cpu_seconds,
+                                              nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=seed * 31))
     net.destroy()
     if rank == 0:
         print(json.dumps(result), flush=True)
