@@ -31,6 +31,9 @@ extern "C" {
 /* ---- InputEncoding: neural_radiance_caching.h:24-27 ---- */
 #define NRC_ENCODING_FREQUENCY 0
 #define NRC_ENCODING_HASH      1
+/* extension (not in the reference): Frequency with the direction encoded by degree-4 spherical harmonics
+ * (BASELINE.json north_star "frequency + one-blob + spherical-harmonics"); same 80-wide MLP shape */
+#define NRC_ENCODING_FREQUENCY_SH 2
 
 /* ---- default learning rates TRAIN_LR(): neural_radiance_caching.h:47-54 ---- */
 #define NRC_TRAIN_LR_FREQUENCY 1e-3f

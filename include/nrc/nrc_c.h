@@ -141,9 +141,9 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const flo
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* the encoder the MLP kernels actually run (closed-form OneBlob, f16-rounded), same output format */
 nrc_status nrc_debug_encode_fast(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
-/* InputEncoding::Hash: the production Composite{HashGrid, OneBlob, Identity} encoder with the inference (EMA)
- * grid table, f32 [n][64] canonical order */
-nrc_status nrc_debug_encode_hash(nrc_net* net, const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
+/* The production encoder of the handle's configured encoding, f32 canonical order: Frequency / FrequencySH [n][80],
+ * Hash [n][64] (with the inference (EMA) grid table). */
+nrc_status nrc_debug_encode_net(nrc_net* net, const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* encoder variants: 0 = production (as nrc_debug_encode_fast), 1 = omod doubling-chain triangle wave */
 nrc_status nrc_debug_encode_fast_variant(int variant, const float* inputs_d, float* encoded_d, uint32_t n,
                                          hipStream_t stream);

@@ -93,7 +93,9 @@ void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd, int encodi
     int f_kk[NRC_ENC_WIDTH], f_h[NRC_ENC_WIDTH], f_j[NRC_ENC_WIDTH];
     for (int h = 0; h < 2; ++h)
         for (int sn = 0; sn < (hash ? 32 : 40); ++sn) {
-            const int f = hash ? hash_slot_feature(sn, h) : slot_feature(sn, h);
+            const int f = hash                                  ? hash_slot_feature(sn, h)
+                          : encoding == NRC_ENCODING_FREQUENCY_SH ? sh_slot_feature(sn, h)
+                                                                : slot_feature(sn, h);
             f_kk[f] = sn / 8;
             f_h[f] = h;
             f_j[f] = sn % 8;
@@ -134,6 +136,17 @@ std::string config_json(int encoding, const nrc_config& c) {
                       "neurons\":64,\"otype\":\"FullyFusedMLP\",\"output_activation\":\"ReLU\"},\"optimizer\":{"
                       "\"decay\":%g,\"nested\":{\"beta1\":%g,\"beta2\":%g,\"epsilon\":%g,\"l2_reg\":%g,\"learning_"
                       "rate\":%g,\"otype\":\"Adam\"},\"otype\":\"EMA\"}}",
+                      c.ema_decay, c.beta1, c.beta2, c.epsilon, c.l2_reg, c.learning_rate);
+    } else if (encoding == NRC_ENCODING_FREQUENCY_SH) {
+        std::snprintf(buf, sizeof(buf),
+                      "{\"encoding\":{\"nested\":[{\"n_dims_to_encode\":3,\"n_frequencies\":12,\"otype\":"
+                      "\"TriangleWave\"},{\"degree\":4,\"n_dims_to_encode\":2,\"otype\":\"SphericalHarmonics\"},"
+                      "{\"n_bins\":4,\"n_dims_to_encode\":4,\"otype\":\"OneBlob\"},{\"n_dims_to_encode\":6,\"otype\":"
+                      "\"Identity\"}],\"otype\":\"Composite\"},\"loss\":{\"otype\":\"RelativeL2Luminance\"},"
+                      "\"network\":{\"activation\":\"ReLU\",\"n_hidden_layers\":5,\"n_neurons\":64,\"otype\":"
+                      "\"FullyFusedMLP\",\"output_activation\":\"ReLU\"},\"optimizer\":{\"decay\":%g,\"nested\":{"
+                      "\"beta1\":%g,\"beta2\":%g,\"epsilon\":%g,\"l2_reg\":%g,\"learning_rate\":%g,\"otype\":"
+                      "\"Adam\"},\"otype\":\"EMA\"}}",
                       c.ema_decay, c.beta1, c.beta2, c.epsilon, c.l2_reg, c.learning_rate);
     } else {
         std::snprintf(buf, sizeof(buf),
@@ -264,7 +277,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
                                     net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream));
     else
         HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                       net->slabs, net->loss_partials, net->stream));
+                                       net->slabs, net->loss_partials, net->stream, net->encoding));
     net->step += 1;
     HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
                                  loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
@@ -279,11 +292,17 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
 hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
     if (net->hash())
         return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
+    if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
+        return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     return launch_infer(in, out, n, net->wf_infer, net->stream);
 }
 
+void require_not_hash(const nrc_net* net, const char* what) {
+    if (net->hash()) throw ApiError(NRC_ERR_UNSUPPORTED, std::string(what) + " is not implemented for InputEncoding::Hash");
+}
+
 void require_frequency(const nrc_net* net, const char* what) {
-    if (net->hash())
+    if (net->encoding != NRC_ENCODING_FREQUENCY)
         throw ApiError(NRC_ERR_UNSUPPORTED, std::string(what) + " is implemented for InputEncoding::Frequency only");
 }
 
@@ -344,7 +363,7 @@ nrc_status nrc_free(nrc_net* net) {
 nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_config* cfg, int verbose) {
     return guarded([&] {
         if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
-        if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH)
+        if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH && encoding != NRC_ENCODING_FREQUENCY_SH)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
         net->release();
         net->stream = stream;
@@ -453,6 +472,9 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
         if (net->hash())
             HIP_CHECK(launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, reinterpret_cast<const float*>(thr),
                                         rgba, num_pixels, mode, w, net->stream));
+        else if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
+            HIP_CHECK(launch_infer_sh(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba, num_pixels,
+                                      mode, w, net->stream));
         else
             HIP_CHECK(launch_infer_accumulate(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba,
                                               num_pixels, mode, w, net->stream));
@@ -505,7 +527,7 @@ nrc_status nrc_set_hyper_params(nrc_net* net, const nrc_hyper_params* hp) {
 nrc_status nrc_set_config(nrc_net* net, int encoding) {
     return guarded([&] {
         if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
-        if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH)
+        if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH && encoding != NRC_ENCODING_FREQUENCY_SH)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
         net->encoding = encoding;
         net->cfg = nrc_default_config(encoding);
@@ -537,7 +559,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
                           float* grad_d) {
     return guarded([&] {
         check_live(net);
-        require_frequency(net, "nrc_train_grad");
+        require_not_hash(net, "nrc_train_grad");
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
         if (b == 0) {
@@ -548,7 +570,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
         HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
-                                       net->wb_train, net->slabs, net->loss_partials, net->stream));
+                                       net->wb_train, net->slabs, net->loss_partials, net->stream, net->encoding));
         HIP_CHECK(launch_reduce_adam(kReduceOnly, net->slabs, blocks, net->loss_partials, grad_d, nullptr,
                                      net->buffers(), net->optim(net->step + 1), net->stream));
     });
@@ -557,7 +579,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
     return guarded([&] {
         check_live(net);
-        require_frequency(net, "nrc_train_apply");
+        require_not_hash(net, "nrc_train_apply");
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         net->step += 1;
         HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
@@ -602,13 +624,14 @@ nrc_status nrc_get_num_params(const nrc_net* net, uint64_t* n) {
     });
 }
 
-nrc_status nrc_debug_encode_hash(nrc_net* net, const float* in, float* enc, uint32_t n, hipStream_t stream) {
+nrc_status nrc_debug_encode_net(nrc_net* net, const float* in, float* enc, uint32_t n, hipStream_t stream) {
     return guarded([&] {
         check_live(net);
-        if (!net->hash()) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "network is not configured with InputEncoding::Hash");
         if (n == 0) return;
         if (!in || !enc) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
-        HIP_CHECK(launch_encode_hash(in, net->table_infer, enc, n, stream));
+        if (net->hash()) HIP_CHECK(launch_encode_hash(in, net->table_infer, enc, n, stream));
+        else if (net->encoding == NRC_ENCODING_FREQUENCY_SH) HIP_CHECK(launch_encode_sh(in, enc, n, stream));
+        else HIP_CHECK(launch_encode_fast(in, enc, n, stream));
     });
 }
 

@@ -68,6 +68,22 @@ __host__ __device__ constexpr int hash_dx_row(int feature) {
 __host__ __device__ constexpr int k0_feature(int K) {
     return slot_feature(8 * (K >> 4) + (K & 7), (K >> 3) & 1);
 }
+// FrequencySH extension (80-wide): per lane half 18 TriangleWave, 8 SH coefficients (8h..8h+7), OneBlob of dims
+// 5+2h, 6+2h (8 slots), 3 Identity, 3 pad.
+__host__ __device__ constexpr int sh_slot_feature(int n, int h) {
+    return n < 18   ? (n / 6) * 12 + (n % 6) + 6 * h
+           : n < 26 ? 36 + 8 * h + (n - 18)
+           : n < 34 ? 52 + (2 * h + (n - 26) / 4) * 4 + (n - 26) % 4
+           : n < 37 ? 68 + 3 * h + (n - 34)
+                    : 74 + 3 * h + (n - 37);
+}
+__host__ __device__ constexpr int sh_k0_feature(int K) {
+    return sh_slot_feature(8 * (K >> 4) + (K & 7), (K >> 3) & 1);
+}
+// layer-0 K index -> canonical feature, per encoding (0 Frequency, 1 Hash, 2 FrequencySH)
+__host__ __device__ constexpr int enc_k0_feature(int enc, int K) {
+    return enc == 1 ? hash_k0_feature(K) : enc == 2 ? sh_k0_feature(K) : k0_feature(K);
+}
 
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
@@ -81,12 +97,16 @@ hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, 
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
                              const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
 hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float* enc, int64_t n, hipStream_t s);
+// FrequencySH extension
+hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
+                           float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
+hipError_t launch_encode_sh(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, bool chain = false);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,
-                                float* loss_partials, hipStream_t s);
+                                float* loss_partials, hipStream_t s, int enc = 0);
 int train_blocks(int64_t b);
 // diagnostic: same kernel with s_memtime stamps (16 per block) — never used by the product path
 hipError_t launch_train_stamped(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,

@@ -36,8 +36,9 @@ __device__ __forceinline__ f16v zero16() {
 // ------------------------------------------------------------------------------------------------
 struct QLane {
     float p0, p1, p2;  // position (both halves)
-    float b0, b1, b2;  // OneBlob inputs 3+3h .. 5+3h
+    float b0, b1, b2;  // OneBlob inputs 3+3h .. 5+3h (FrequencySH: direction theta, phi, OneBlob input 5+2h)
     float i0, i1, i2;  // Identity inputs 9+3h .. 11+3h
+    float x3;          // FrequencySH only: OneBlob input 6+2h
 };
 
 __device__ __forceinline__ QLane load_q(const float* __restrict__ q, int64_t s, int h) {
@@ -55,6 +56,30 @@ __device__ __forceinline__ QLane load_q(const float* __restrict__ q, int64_t s, 
     Q.i1 = ri[1];
     Q.i2 = ri[2];
     return Q;
+}
+
+// FrequencySH extension: both halves need the direction (dims 3, 4); OneBlob dims 5+2h, 6+2h.
+__device__ __forceinline__ QLane load_q_sh(const float* __restrict__ q, int64_t s, int h) {
+    const float* r = q + s * NRC_INPUT_DIMS;
+    QLane Q;
+    Q.p0 = r[0];
+    Q.p1 = r[1];
+    Q.p2 = r[2];
+    Q.b0 = r[3];
+    Q.b1 = r[4];
+    Q.b2 = r[5 + 2 * h];
+    Q.x3 = r[6 + 2 * h];
+    const float* ri = r + 9 + 3 * h;
+    Q.i0 = ri[0];
+    Q.i1 = ri[1];
+    Q.i2 = ri[2];
+    return Q;
+}
+
+template <int ENC>
+__device__ __forceinline__ QLane load_q_enc(const float* __restrict__ q, int64_t s, int h) {
+    if constexpr (ENC == 2) return load_q_sh(q, s, h);
+    else return load_q(q, s, h);
 }
 
 // TriangleWave [L spec choice, SURVEY A.2]: |2 frac(u) - 1|.
@@ -432,6 +457,61 @@ __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// FrequencySH extension (NRC_ENCODING_FREQUENCY_SH; oracle/nrc_oracle.c orc_encode_sh): TriangleWave as the
+// Frequency composite, the direction's degree-4 real SH (tcnn SphericalHarmonics basis) with lane half h
+// producing coefficients 8h..8h+7, OneBlob of dims 5+2h, 6+2h, Identity 9+3h.., 3 pad slots.
+// ------------------------------------------------------------------------------------------------
+template <bool CHAIN = false>
+__device__ __forceinline__ void encode_sh(const QLane& Q, int h, h8 (&x)[5]) {
+    uint32_t w[20];
+    {
+        h8 t[5];
+        encode_fast<CHAIN>(Q, h, t);  // slots 0..17 (words 0..8) are the triangle wave; the rest is replaced
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            w[k] = __builtin_bit_cast(u4, t[k >> 2])[k & 3];
+        }
+    }
+    const float st = sinf(Q.b0), ct = cosf(Q.b0), sp = sinf(Q.b1), cp = cosf(Q.b1);
+    const float X = st * cp, Y = st * sp, Z = ct;
+    const float xy = X * Y, xz = X * Z, yz = Y * Z, x2 = X * X, y2 = Y * Y, z2 = Z * Z;
+    float o[8];
+    if (h == 0) {
+        o[0] = 0.28209479177387814f;
+        o[1] = -0.48860251190291987f * Y;
+        o[2] = 0.48860251190291987f * Z;
+        o[3] = -0.48860251190291987f * X;
+        o[4] = 1.0925484305920792f * xy;
+        o[5] = -1.0925484305920792f * yz;
+        o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+        o[7] = -1.0925484305920792f * xz;
+    } else {
+        o[0] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+        o[1] = 0.59004358992664352f * Y * (-3.0f * x2 + y2);
+        o[2] = 2.8906114426405538f * xy * Z;
+        o[3] = 0.45704579946446572f * Y * (1.0f - 5.0f * z2);
+        o[4] = 0.3731763325901154f * Z * (5.0f * z2 - 3.0f);
+        o[5] = 0.45704579946446572f * X * (1.0f - 5.0f * z2);
+        o[6] = 1.4453057213202769f * Z * (x2 - y2);
+        o[7] = 0.59004358992664352f * X * (-x2 + 3.0f * y2);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[9 + k] = pk2(o[2 * k], o[2 * k + 1]);
+    blob_fast(Q.b2, w[13], w[14]);
+    blob_fast(Q.x3, w[15], w[16]);
+    w[17] = pk2(Q.i0, Q.i1);
+    w[18] = pk2(Q.i2, 1.0f);
+    w[19] = 0x3C003C00u;
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
+        x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
 template <int ABL = 0>
 __device__ __forceinline__ h8 relu_h8(const f16v& a, int base) {
     h8 r;
@@ -560,7 +640,8 @@ struct InferEpilogue {
     float w;           // 1 / (iterationIndex + 1)
 };
 
-// ENC: 0 = Frequency composite (80-wide input), 1 = Hash composite (64-wide; grid = f16x2 table)
+// ENC: 0 = Frequency composite (80-wide input), 1 = Hash composite (64-wide; grid = f16x2 table),
+// 2 = FrequencySH extension (80-wide)
 template <int TILES, int THREADS, bool PREFETCH, int ABL, int EPI, int ENC = 0>
 __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float* __restrict__ out, int64_t n,
                                               const h8* __restrict__ wf, const InferEpilogue& epi,
@@ -584,13 +665,15 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
 
     QLane Q[TILES];
 #pragma unroll
-    for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
+    for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((g * TILES + t) * 32 + r, last), h);
     for (; g < ngroups; g += wstride) {
         h8 x[TILES][KK0];
 #pragma unroll
         for (int t = 0; t < TILES; ++t) {
             if constexpr (ENC == 1) {
                 encode_hash(Q[t], h, grid, x[t]);
+            } else if constexpr (ENC == 2) {
+                encode_sh<(ABL & 16) != 0>(Q[t], h, x[t]);
             } else if constexpr ((ABL & 1) != 0) {
                 typedef float f4 __attribute__((ext_vector_type(4)));
                 const f4 a = {Q[t].p0, Q[t].p1, Q[t].b0, Q[t].b1}, b = {Q[t].b2, Q[t].i0, Q[t].i1, Q[t].i2};
@@ -603,7 +686,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         const int64_t ng = g + wstride;
         if (ng < ngroups) {
 #pragma unroll
-            for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
+            for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((ng * TILES + t) * 32 + r, last), h);
         }
         // epilogue operands are fetched before the MLP so their latency hides under the MFMAs
         float tr[TILES][3];
@@ -698,6 +781,26 @@ __global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restr
                                                             int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
                                                             const uint32_t* __restrict__ grid) {
     infer_v2_body<1, 512, false, 0, EPI, 1>(q, out, n, wf, epi, grid);
+}
+
+// FrequencySH extension inference (EPI -1 plain; 0 / 2 fused accumulation)
+template <int EPI>
+__global__ __launch_bounds__(512, 4) void infer_sh_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                          int64_t n, const h8* __restrict__ wf, InferEpilogue epi) {
+    infer_v2_body<1, 512, false, kDefaultAbl, EPI, 2>(q, out, n, wf, epi);
+}
+
+// The production FrequencySH encoder unpacked to canonical order as f32 (parity tests): [n][80].
+__global__ void encode_sh_kernel(const float* __restrict__ q, float* __restrict__ enc, int64_t n) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = gid >> 1;
+    const int h = (int)(gid & 1);
+    if (s >= n) return;
+    const QLane Q = load_q_sh(q, s, h);
+    h8 x[5];
+    encode_sh(Q, h, x);
+#pragma unroll
+    for (int k = 0; k < 40; ++k) enc[s * NRC_ENC_WIDTH + sh_slot_feature(k, h)] = (float)x[k >> 3][k & 7];
 }
 
 // The production hash encoder unpacked to canonical order as f32 (parity tests): [n][64].
@@ -1094,7 +1197,7 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
         h8 A = tr_frag(img_d, mb, kk, lane);
         if (zero_a) A = h8{};
         h8 B;
-        if (ENC == 0 && L == 0 && nb == 2) B = tr_frag_xhi(img_xh, kk, lane);
+        if (ENC != 1 && L == 0 && nb == 2) B = tr_frag_xhi(img_xh, kk, lane);
         else B = tr_frag(img_a, nb, kk, lane);
         acc = mfma(A, B, acc);
     }
@@ -1107,7 +1210,7 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
             fcol = hash_k0_feature(col);
         } else {
             if (col >= NRC_ENC_WIDTH) return;
-            fcol = k0_feature(col);
+            fcol = enc_k0_feature(ENC, col);
         }
     }
 #pragma unroll
@@ -1123,9 +1226,9 @@ __device__ __forceinline__ void dw_layer(const char* img_d, const char* img_a, c
                                          float* __restrict__ slab) {
     if (L == 5) {
         if (wave < 2) dw_block<5, ENC>(img_d, img_a, img_xh, 0, wave, lane, slab);
-    } else if (L == 0 && ENC == 0) {
-        dw_block<0>(img_d, img_a, img_xh, wave / 3, wave % 3, lane, slab);
-        if (wave < 2) dw_block<0>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane, slab);
+    } else if (L == 0 && ENC != 1) {
+        dw_block<0, ENC>(img_d, img_a, img_xh, wave / 3, wave % 3, lane, slab);
+        if (wave < 2) dw_block<0, ENC>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane, slab);
     } else {
         dw_block<L, ENC>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane, slab);
     }
@@ -1201,7 +1304,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     const int64_t s = (int64_t)blockIdx.x * kTrainSamplesPerBlock + sl;
     const bool valid = s < b;
     const int64_t sc = valid ? s : b - 1;
-    const QLane Q = load_q(q, sc, h);
+    const QLane Q = load_q_enc<ENC>(q, sc, h);
     float tgt[3] = {0.f, 0.f, 0.f};
     if (h == 0) {
         tgt[0] = t[sc * 3 + 0];
@@ -1210,6 +1313,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     }
     h8 x[KK0];
     if constexpr (ENC == 1) encode_hash(Q, h, grid, x);
+    else if constexpr (ENC == 2) encode_sh(Q, h, x);
     else encode_fast(Q, h, x);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
@@ -1315,7 +1419,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
         for (int jg = 0; jg < 2; ++jg) store_h4(img_a[0], img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
-    if constexpr (ENC == 0) *(h8*)(img_xh + sl * 32 + 16 * h) = x[KK0 - 1];
+    if constexpr (ENC != 1) *(h8*)(img_xh + sl * 32 + 16 * h) = x[KK0 - 1];
     // Grid gradient (Hash): dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample sl, then the trilinear scatter
     // of tcnn's kernel_grid_backward, grad[entry][f] += w_corner * dy_f. Fine levels (l >= kCoarseLevels) go straight
     // to f32 global atomics, which drain while dW runs. The coarse levels cover the scene with a handful of cells
@@ -1615,6 +1719,26 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
     }
 }
 
+hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
+                           float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t ntiles = (n + 31) / 32;
+    static int bpc[3] = {};
+    const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
+    switch (mode) {
+        case -1: return launch_persistent_infer(infer_sh_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
+        case 0: return launch_persistent_infer(infer_sh_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_encode_sh(const float* queries, float* enc, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(encode_sh_kernel, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, s, queries, enc, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float* enc, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(encode_hash_kernel, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, s, queries,
@@ -1647,10 +1771,15 @@ int train_blocks(int64_t b) { return (int)((b + kTrainSamplesPerBlock - 1) / kTr
 
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,
-                                float* loss_partials, hipStream_t s) {
+                                float* loss_partials, hipStream_t s, int enc) {
     if (b <= 0) return hipSuccess;
-    hipLaunchKernelGGL(train_kernel<false>, dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
-                       loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr);
+    if (enc == 2)
+        hipLaunchKernelGGL((train_kernel<false, 2>), dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b,
+                           n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr, nullptr,
+                           nullptr);
+    else
+        hipLaunchKernelGGL(train_kernel<false>, dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
+                           loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -37,9 +37,10 @@ NRC_ERR_DESTROYED = 2
 
 
 class InputEncoding(IntEnum):
-    """nrc::InputEncoding (neural_radiance_caching.h:24-27)."""
+    """nrc::InputEncoding (neural_radiance_caching.h:24-27), plus the FrequencySH extension (layout.h)."""
     Frequency = 0
     Hash = 1
+    FrequencySH = 2
 
 
 class StateSlot(IntEnum):
@@ -213,10 +214,11 @@ class Network:
             raise ValueError(f"state must have {n} floats")
         check(self._lib.nrc_set_state(self._h, int(slot), v.ctypes.data))
 
-    def encode_hash(self, inputs, encoded, n: int, stream=None) -> None:
-        """InputEncoding::Hash: the production encoder (inference grid table), f32 [n][64] canonical order."""
-        check(self._lib.nrc_debug_encode_hash(self._h, _dev_ptr(inputs, "inputs"), _dev_ptr(encoded, "encoded"),
-                                              int(n), _stream_ptr(stream)))
+    def encode_features(self, inputs, encoded, n: int, stream=None) -> None:
+        """The production encoder of the configured encoding, f32 canonical order ([n][80]; Hash: [n][64] with the
+        inference grid table)."""
+        check(self._lib.nrc_debug_encode_net(self._h, _dev_ptr(inputs, "inputs"), _dev_ptr(encoded, "encoded"),
+                                             int(n), _stream_ptr(stream)))
 
     @property
     def step(self) -> int:

@@ -124,6 +124,51 @@ void orc_encode(const float* queries, int64_t n, float* enc) {
     }
 }
 
+/* Extension encoding NRC_ENCODING_FREQUENCY_SH (not in the reference; BASELINE.json north_star "frequency +
+ * one-blob + spherical-harmonics"): TriangleWave(pos) 36 | SphericalHarmonics degree 4 of the direction 16 |
+ * OneBlob(normal theta/phi, roughness x/y) 16 | Identity(albedos) 6 | pad 1.0 x 6 = 80. The direction is the unit
+ * vector of (theta, phi) under cartesianToSphericalUnitVector's convention (shader_common.h:320-333):
+ * d = (sin t cos p, sin t sin p, cos t). SH basis and constants: the real SH of tcnn's SphericalHarmonics
+ * encoding (degree 4 = 16 coefficients), evaluated on d directly. */
+static void sh16(float x, float y, float z, float* o) {
+    const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+    o[0] = 0.28209479177387814f;
+    o[1] = -0.48860251190291987f * y;
+    o[2] = 0.48860251190291987f * z;
+    o[3] = -0.48860251190291987f * x;
+    o[4] = 1.0925484305920792f * xy;
+    o[5] = -1.0925484305920792f * yz;
+    o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+    o[7] = -1.0925484305920792f * xz;
+    o[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+    o[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+    o[10] = 2.8906114426405538f * xy * z;
+    o[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+    o[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+    o[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+    o[14] = 1.4453057213202769f * z * (x2 - y2);
+    o[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+}
+
+void orc_encode_sh(const float* queries, int64_t n, float* enc) {
+    for (int64_t s = 0; s < n; ++s) {
+        const float* q = queries + s * NRC_INPUT_DIMS;
+        float* e = enc + s * NRC_ENC_WIDTH;
+        for (int d = 0; d < NRC_TRI_DIMS; ++d)
+            for (int k = 0; k < NRC_TRI_FREQS; ++k) e[d * NRC_TRI_FREQS + k] = tri_wave(q[d], k);
+        const float st = sinf(q[3]), ct = cosf(q[3]), sp = sinf(q[4]), cp = cosf(q[4]);
+        sh16(st * cp, st * sp, ct, e + 36);
+        for (int d = 0; d < 4; ++d) one_blob(q[5 + d], e + 52 + d * NRC_BLOB_BINS);
+        for (int d = 0; d < NRC_IDENT_DIMS; ++d) e[68 + d] = q[9 + d];
+        for (int f = 74; f < NRC_ENC_WIDTH; ++f) e[f] = 1.0f;
+    }
+}
+
+static void encode_kind(int kind, const float* q, float* enc) {
+    if (kind == NRC_ENCODING_FREQUENCY_SH) orc_encode_sh(q, 1, enc);
+    else orc_encode(q, 1, enc);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Network                                                                                     */
 /* ------------------------------------------------------------------------------------------ */
@@ -189,8 +234,8 @@ typedef struct {
     float y[NRC_OUT_PADDED];
 } sample_acts;
 
-static void forward_one(const float* w, const float* q, int mode, sample_acts* A) {
-    orc_encode(q, 1, A->enc);
+static void forward_one(const float* w, const float* q, int mode, int kind, sample_acts* A) {
+    encode_kind(kind, q, A->enc);
     if (mode != ORC_FP32)
         for (int f = 0; f < NRC_ENC_WIDTH; ++f) A->enc[f] = orc_f16_round(A->enc[f]);
     const float* in = A->enc;
@@ -216,7 +261,7 @@ typedef struct {
     const float* queries;
     const float* targets;
     int64_t begin, end;
-    int mode;
+    int mode, kind;
     float* out;
     /* grad job */
     double n_total;
@@ -229,7 +274,7 @@ static void* forward_job(void* arg) {
     job_t* J = (job_t*)arg;
     sample_acts A;
     for (int64_t s = J->begin; s < J->end; ++s) {
-        forward_one(J->w, J->queries + s * NRC_INPUT_DIMS, J->mode, &A);
+        forward_one(J->w, J->queries + s * NRC_INPUT_DIMS, J->mode, J->kind, &A);
         for (int c = 0; c < NRC_OUTPUT_DIMS; ++c) J->out[s * NRC_OUTPUT_DIMS + c] = A.y[c];
     }
     return NULL;
@@ -244,6 +289,11 @@ static int clamp_threads(int nthreads, int64_t n) {
 
 void orc_forward(const float* params, const float* queries, int64_t n, int mode, float* out,
                  int nthreads) {
+    orc_forward_enc(NRC_ENCODING_FREQUENCY, params, queries, n, mode, out, nthreads);
+}
+
+void orc_forward_enc(int kind, const float* params, const float* queries, int64_t n, int mode, float* out,
+                     int nthreads) {
     if (n <= 0) return;
     float* w = mode_weights(params, mode);
     nthreads = clamp_threads(nthreads, n);
@@ -256,6 +306,7 @@ void orc_forward(const float* params, const float* queries, int64_t n, int mode,
         jobs[t].begin = n * t / nthreads;
         jobs[t].end = n * (t + 1) / nthreads;
         jobs[t].mode = mode;
+        jobs[t].kind = kind;
         jobs[t].out = out;
         if (nthreads > 1) pthread_create(&th[t], NULL, forward_job, &jobs[t]);
         else forward_job(&jobs[t]);
@@ -276,7 +327,7 @@ static void* grad_job(void* arg) {
     sample_acts A;
     const float n_total = (float)J->n_total;
     for (int64_t s = J->begin; s < J->end; ++s) {
-        forward_one(w, J->queries + s * NRC_INPUT_DIMS, mode, &A);
+        forward_one(w, J->queries + s * NRC_INPUT_DIMS, mode, J->kind, &A);
         const float* t = J->targets + s * NRC_OUTPUT_DIMS;
         const float lum = 0.299f * A.y[0] + 0.587f * A.y[1] + 0.114f * A.y[2];
         const float denom = lum * lum + NRC_LUM_EPS;
@@ -319,6 +370,11 @@ static void* grad_job(void* arg) {
 
 double orc_grad(const float* params, const float* queries, const float* targets, int64_t b,
                 double n_total, float loss_scale, int mode, float* grad, int nthreads) {
+    return orc_grad_enc(NRC_ENCODING_FREQUENCY, params, queries, targets, b, n_total, loss_scale, mode, grad, nthreads);
+}
+
+double orc_grad_enc(int kind, const float* params, const float* queries, const float* targets, int64_t b,
+                    double n_total, float loss_scale, int mode, float* grad, int nthreads) {
     for (int i = 0; i < NRC_NUM_PARAMS; ++i) grad[i] = 0.0f;
     if (b <= 0) return 0.0;
     float* w = mode_weights(params, mode);
@@ -332,6 +388,7 @@ double orc_grad(const float* params, const float* queries, const float* targets,
         jobs[t].begin = b * t / nthreads;
         jobs[t].end = b * (t + 1) / nthreads;
         jobs[t].mode = mode;
+        jobs[t].kind = kind;
         jobs[t].n_total = n_total;
         jobs[t].loss_scale = loss_scale;
         jobs[t].grad = (double*)calloc(NRC_NUM_PARAMS, sizeof(double));

@@ -49,6 +49,14 @@ void orc_forward(const float* params, const float* queries, int64_t n, int mode,
 double orc_grad(const float* params, const float* queries, const float* targets, int64_t b,
                 double n_total, float loss_scale, int mode, float* grad, int nthreads);
 
+/* Extension encoding NRC_ENCODING_FREQUENCY_SH (see nrc_oracle.c): 80-wide, same MLP shape as Frequency. */
+void orc_encode_sh(const float* queries, int64_t n, float* enc);
+/* orc_forward / orc_grad for an encoding kind (NRC_ENCODING_FREQUENCY or NRC_ENCODING_FREQUENCY_SH) */
+void orc_forward_enc(int kind, const float* params, const float* queries, int64_t n, int mode, float* out,
+                     int nthreads);
+double orc_grad_enc(int kind, const float* params, const float* queries, const float* targets, int64_t b,
+                    double n_total, float loss_scale, int mode, float* grad, int nthreads);
+
 /* tcnn Adam step followed by the EMA(decay) wrapper [M]. Updates params/m/v/ema in place and
  * writes the debiased EMA weights (the inference weights) to infer_params. step is 1-based. */
 void orc_adam_ema(float* params, float* m, float* v, float* ema, float* infer_params,

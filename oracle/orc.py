@@ -44,6 +44,11 @@ def lib() -> ctypes.CDLL:
                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int64]
         L.orc_init_params.argtypes = [fp, ctypes.c_uint64]
+        L.orc_encode_sh.argtypes = [fp, ctypes.c_int64, fp]
+        L.orc_forward_enc.argtypes = [ctypes.c_int, fp, fp, ctypes.c_int64, ctypes.c_int, fp, ctypes.c_int]
+        L.orc_grad_enc.restype = ctypes.c_double
+        L.orc_grad_enc.argtypes = [ctypes.c_int, fp, fp, fp, ctypes.c_int64, ctypes.c_double, ctypes.c_float,
+                                   ctypes.c_int, fp, ctypes.c_int]
         vp, u32, u64, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64
         L.orc_accumulate.argtypes = [vp, vp, vp, i64, ctypes.c_int, u32]
         L.orc_propagate.argtypes = [vp, vp, i64, vp, vp, i64]
@@ -81,17 +86,29 @@ def encode(queries: np.ndarray) -> np.ndarray:
     return out
 
 
-def forward(params: np.ndarray, queries: np.ndarray, mode: int = MIXED, threads: int | None = None) -> np.ndarray:
+FREQUENCY, HASH, FREQUENCY_SH = 0, 1, 2
+
+
+def encode_sh(queries: np.ndarray) -> np.ndarray:
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    out = np.empty((q.shape[0], 80), dtype=np.float32)
+    if q.shape[0]:
+        lib().orc_encode_sh(_p(q), q.shape[0], _p(out))
+    return out
+
+
+def forward(params: np.ndarray, queries: np.ndarray, mode: int = MIXED, threads: int | None = None,
+            encoding: int = FREQUENCY) -> np.ndarray:
     q = np.ascontiguousarray(queries, dtype=np.float32)
     p = np.ascontiguousarray(params, dtype=np.float32)
     n = q.shape[0]
     out = np.zeros((n, 3), dtype=np.float32)
     if n:
-        lib().orc_forward(_p(p), _p(q), n, mode, _p(out), threads or default_threads())
+        lib().orc_forward_enc(encoding, _p(p), _p(q), n, mode, _p(out), threads or default_threads())
     return out
 
 
-def grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, threads=None):
+def grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, threads=None, encoding=FREQUENCY):
     q = np.ascontiguousarray(queries, dtype=np.float32)
     t = np.ascontiguousarray(targets, dtype=np.float32)
     p = np.ascontiguousarray(params, dtype=np.float32)
@@ -99,8 +116,8 @@ def grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, t
     if n_total is None:
         n_total = 3.0 * b
     g = np.zeros(NUM_PARAMS, dtype=np.float32)
-    loss = lib().orc_grad(_p(p), _p(q), _p(t), b, float(n_total), float(loss_scale), mode, _p(g),
-                          threads or default_threads())
+    loss = lib().orc_grad_enc(encoding, _p(p), _p(q), _p(t), b, float(n_total), float(loss_scale), mode, _p(g),
+                              threads or default_threads())
     return g, float(loss)
 
 

@@ -163,3 +163,32 @@ def test_synthetic_frame_invariants(nrc):
     assert set(np.unique(f.end_vertices["radiance_mask"])) <= {0.0, 1.0}
     assert f.queries_inference.shape == (f.screen_size + f.num_tiles, 15)
     assert f.train_records.dtype.itemsize == 28 and f.end_vertices.dtype.itemsize == 16
+
+
+def test_sh_encoding_oracle_matches_numpy(nrc, orc):
+    """FrequencySH extension (oracle/nrc_oracle.c orc_encode_sh) against a float64 numpy restatement."""
+    q = nrc.synthetic.cornell_queries(512, seed=8).astype(np.float64)
+    enc = orc.encode_sh(q.astype(np.float32)).astype(np.float64)
+    th, ph = q[:, 3], q[:, 4]
+    x, y, z = np.sin(th) * np.cos(ph), np.sin(th) * np.sin(ph), np.cos(th)
+    sh = np.stack([np.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+                   -0.48860251190291987 * x, 1.0925484305920792 * x * y, -1.0925484305920792 * y * z,
+                   0.94617469575755997 * z * z - 0.31539156525251999, -1.0925484305920792 * x * z,
+                   0.54627421529603959 * (x * x - y * y), 0.59004358992664352 * y * (-3 * x * x + y * y),
+                   2.8906114426405538 * x * y * z, 0.45704579946446572 * y * (1 - 5 * z * z),
+                   0.3731763325901154 * z * (5 * z * z - 3), 0.45704579946446572 * x * (1 - 5 * z * z),
+                   1.4453057213202769 * z * (x * x - y * y), 0.59004358992664352 * x * (-x * x + 3 * y * y)], 1)
+    np.testing.assert_allclose(enc[:, 36:52], sh, atol=2e-6)
+    # the orthonormal real SH: sum of squares of degree-l band is (2l+1)/(4 pi)
+    for l, (a, b) in enumerate([(0, 1), (1, 4), (4, 9), (9, 16)]):
+        np.testing.assert_allclose((sh[:, a:b] ** 2).sum(1), (2 * l + 1) / (4 * np.pi), rtol=1e-12)
+    freq = orc.encode(q.astype(np.float32)).astype(np.float64)
+    np.testing.assert_array_equal(enc[:, :36], freq[:, :36])          # triangle wave unchanged
+    np.testing.assert_array_equal(enc[:, 52:68], freq[:, 44:60])      # OneBlob of normal + roughness
+    np.testing.assert_array_equal(enc[:, 68:74], freq[:, 60:66])      # identity
+    assert np.all(enc[:, 74:] == 1.0)
+    # forward / grad entry points accept the encoding
+    p = orc.init_params(3)
+    y_sh = orc.forward(p, q[:64].astype(np.float32), orc.FP32, encoding=orc.FREQUENCY_SH)
+    y_f = orc.forward(p, q[:64].astype(np.float32), orc.FP32)
+    assert not np.array_equal(y_sh, y_f)

@@ -55,7 +55,7 @@ def test_hash_encoder_parity(nrc, orc, dev, hnet):
     q = nrc.synthetic.cornell_queries(20000, seed=3)
     q[:500, :3] = np.random.default_rng(1).uniform(-0.2, 1.2, (500, 3)).astype(np.float32)  # wrap / dense paths
     enc = torch.zeros((len(q), 64), device=dev)
-    hnet.encode_hash(_t(q, dev), enc, len(q))
+    hnet.encode_features(_t(q, dev), enc, len(q))
     torch.cuda.synchronize()
     got = enc.cpu().numpy()
     ref = orc.hash_encode(params, q, orc.MIXED)
