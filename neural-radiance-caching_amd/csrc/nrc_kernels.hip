@@ -1284,20 +1284,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     char* img_xh = smem + kLdsWf + kLdsWb + 4 * kLdsImg;
     float* red = (float*)(img_xh + kLdsXhi);
 
-    // weight images: issue every global load first, encode while they fly, then store to LDS
-    constexpr int PF = (kFwdFrags * 64 + 255) / 256, PB = (NBF * 64 + 255) / 256;
-    h8 vf[PF], vb[PB];
-#pragma unroll
-    for (int k = 0; k < PF; ++k) {
-        const int i = threadIdx.x + k * 256;
-        if (i < kFwdFrags * 64) vf[k] = wf[i];
-    }
-#pragma unroll
-    for (int k = 0; k < PB; ++k) {
-        const int i = threadIdx.x + k * 256;
-        if (i < NBF * 64) vb[k] = wb[i];
-    }
-
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, r = lane & 31;
     const int sl = wave * 32 + r;
@@ -1311,6 +1297,20 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         tgt[1] = t[sc * 3 + 1];
         tgt[2] = t[sc * 3 + 2];
     }
+    // weight images: the sample loads go first, then every weight load; the forward images are stored to LDS
+    // after the encoder, the backward images only after the forward pass (their transfer overlaps it)
+    constexpr int PF = (kFwdFrags * 64 + 255) / 256, PB = (NBF * 64 + 255) / 256;
+    h8 vf[PF], vb[PB];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < kFwdFrags * 64) vf[k] = wf[i];
+    }
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < NBF * 64) vb[k] = wb[i];
+    }
     h8 x[KK0];
     if constexpr (ENC == 1) encode_hash(Q, h, grid, x);
     else if constexpr (ENC == 2) encode_sh(Q, h, x);
@@ -1320,12 +1320,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         const int i = threadIdx.x + k * 256;
         if (i < kFwdFrags * 64) lwf[i] = vf[k];
     }
-#pragma unroll
-    for (int k = 0; k < PB; ++k) {
-        const int i = threadIdx.x + k * 256;
-        if (i < NBF * 64) lwb[i] = vb[k];
-    }
-    lds_barrier();  // weights in LDS
+    lds_barrier();  // forward weight images in LDS
     stamp();
 
     h8 a[5][4];
@@ -1351,6 +1346,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         }
     }
     const f16v o = mlp_out(lwf, a[4], lane);
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < NBF * 64) lwb[i] = vb[k];
+    }
     stamp();
 
     // RelativeL2Luminance on the f16 prediction, loss-scaled f16 gradient, ReLU-masked.
@@ -1386,32 +1386,35 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     stamp();
 
     // One barrier per layer: step l reads buffer l&1 and writes layer l-1's operands into the other
-    // buffer, whose previous readers (step l+1) all passed the barrier that ended step l+1.
+    // buffer, whose previous readers (step l+1) all passed the barrier that ended step l+1. The dW GEMM of
+    // layer l comes first in program order: its operand reads are independent of the delta chain, so the
+    // compiler can interleave the two MFMA streams without an LDS write in between.
     h8 d4[4], d3[4], d2[4], d1[4], d0[4];
+    dw_layer<5, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     bwd_chain<5>(lwb, g, a[4], lane, d4);
     write_rows64(img_d[0], sl, h, d4);
     write_rows64(img_a[0], sl, h, a[3]);
-    dw_layer<5, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
+    dw_layer<4, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     bwd_chain<4>(lwb, d4, a[3], lane, d3);
     write_rows64(img_d[1], sl, h, d3);
     write_rows64(img_a[1], sl, h, a[2]);
-    dw_layer<4, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
+    dw_layer<3, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     bwd_chain<3>(lwb, d3, a[2], lane, d2);
     write_rows64(img_d[0], sl, h, d2);
     write_rows64(img_a[0], sl, h, a[1]);
-    dw_layer<3, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
+    dw_layer<2, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     bwd_chain<2>(lwb, d2, a[1], lane, d1);
     write_rows64(img_d[1], sl, h, d1);
     write_rows64(img_a[1], sl, h, a[0]);
-    dw_layer<2, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
+    dw_layer<1, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     bwd_chain<1>(lwb, d1, a[0], lane, d0);
     // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a[0], x_hi -> img_xh)
     write_rows64(img_d[0], sl, h, d0);
@@ -1422,7 +1425,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     if constexpr (ENC != 1) *(h8*)(img_xh + sl * 32 + 16 * h) = x[KK0 - 1];
     // Grid gradient (Hash): dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample sl, then the trilinear scatter
     // of tcnn's kernel_grid_backward, grad[entry][f] += w_corner * dy_f. Fine levels (l >= kCoarseLevels) go straight
-    // to f32 global atomics, which drain while dW runs. The coarse levels cover the scene with a handful of cells
+    // to f32 global atomics, which drain while the layer-0 dW runs. The coarse levels cover the scene with a handful of cells
     // (position * 0.005 spans ~1.6 * 2^l cells per axis), so every sample of the batch would hit the same few
     // entries: they are pre-summed per block in an LDS hash table (below) and flushed with one atomic per entry.
     constexpr int kCoarseLevels = 5;
@@ -1451,7 +1454,6 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
             }
         }
     }
-    dw_layer<1, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
     lds_barrier();
     stamp();
     if constexpr (ENC == 1) {
@@ -1511,10 +1513,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 // ------------------------------------------------------------------------------------------------
 // Fixed-order weight-gradient reduction + tcnn Adam + EMA + f16 fragment-image repack.
 // ------------------------------------------------------------------------------------------------
-// Block = 64 parameters x 16 slab groups; each thread sums every 16th slab with all of its loads in
-// flight (four interleaved partial sums), the groups are combined in LDS in a fixed tree: the result is
-// bitwise reproducible for a given slab count.
-constexpr int kRedParams = 64, kRedGroups = 16, kRedThreads = kRedParams * kRedGroups;
+// Block = 16 lanes x float4 = 64 parameters x 16 slab groups (352 blocks for the Frequency config, so the
+// whole chip shares the 11.5 MB of slabs); each thread sums every 16th slab with all of its loads in flight,
+// the groups are combined in LDS in a fixed tree: the result is bitwise reproducible for a given slab count.
+constexpr int kRedParams = 16, kRedGroups = 16, kRedThreads = kRedParams * kRedGroups;
 constexpr int kRedVec = 4;  // floats per thread: one 16-byte load per slab
 static_assert(NRC_NUM_PARAMS % (kRedParams * 4) == 0 && NRC_HASH_MLP_PARAMS % (kRedParams * 4) == 0,
               "parameter counts must tile the reduction");
@@ -1551,9 +1553,8 @@ __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const
     if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
 }
 
-// Block = 256 parameters (64 lanes x float4) x 16 slab groups; each thread sums every 16th slab with
-// all of its 16-byte loads in flight (two interleaved partial sums), the groups are combined in LDS in
-// a fixed tree: bitwise reproducible for a given slab count.
+// The per-slab loss partials are summed by wave 0 of block 0: a strided per-lane sum and a fixed xor
+// butterfly (one load latency instead of a serial chain of nslabs loads).
 __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
                                                           const float* __restrict__ loss_partials,
                                                           float* __restrict__ grad_io, float* __restrict__ loss_out,
@@ -1563,13 +1564,17 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
     __shared__ f4 part[kRedGroups][kRedParams];
     const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
     const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
-            for (int i = 0; i < nslabs; ++i) L += loss_partials[i];
-            if (mode == kReduceOnly) grad_io[mb.n_mlp] = L;
-            else if (loss_out) loss_out[0] = L;
-        } else if (mode == kApplyOnly && loss_out) {
+            for (int i = threadIdx.x; i < nslabs; i += 64) L += loss_partials[i];
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
+            if (threadIdx.x == 0) {
+                if (mode == kReduceOnly) grad_io[mb.n_mlp] = L;
+                else if (loss_out) loss_out[0] = L;
+            }
+        } else if (mode == kApplyOnly && loss_out && threadIdx.x == 0) {
             loss_out[0] = grad_io[mb.n_mlp];
         }
     }
@@ -1594,7 +1599,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         }
         part[grp][pl] = a0 + a1;
         __syncthreads();
-        // one parameter per thread for the combine + Adam (threads 0..255 of the block)
+        // one parameter per thread for the combine + Adam (threads 0..63 of the block)
         if (threadIdx.x >= kRedParams * kRedVec) return;
         const int lp = threadIdx.x / kRedVec, comp = threadIdx.x % kRedVec;
         float t8[8];
