@@ -111,10 +111,16 @@ nrc_status nrc_get_config_json(const nrc_net* net, char* buf, size_t cap, size_t
 
 /* ---- data-parallel split of train() (new capability: the reference has no collectives) ----
  * nrc_train_grad writes the loss-scaled gradient of this rank's b samples, normalised by the GLOBAL
- * batch (3 * global_b), into grad_d[NRC_GRAD_FLOATS] (f32, device), with the local loss at
- * grad_d[NRC_NUM_PARAMS]. Sum grad_d over ranks (e.g. an RCCL all-reduce), then nrc_train_apply
- * performs the identical Adam + EMA step on every rank. loss_h: as in nrc_train. */
-#define NRC_GRAD_FLOATS (NRC_NUM_PARAMS + 4)
+ * batch (3 * global_b), into grad_d[nrc_get_grad_floats()] (f32, device): the gradient of every parameter
+ * in nrc_get_state order (grad_d[0 .. num_params)), then the local loss at grad_d[num_params]. Sum grad_d
+ * over ranks (e.g. an RCCL all-reduce), then nrc_train_apply performs the identical Adam + EMA step on every
+ * rank. loss_h: as in nrc_train.
+ * Frequency / FrequencySH: NRC_GRAD_FLOATS (88 KiB). Hash: NRC_HASH_GRAD_FLOATS (3.9 MiB: the MLP gradient,
+ * then the grid-table gradient [entry][2]; the sparse grid Adam steps exactly the entries whose SUMMED gradient
+ * is non-zero, as the single-GPU step over the global batch does). */
+#define NRC_GRAD_FLOATS      (NRC_NUM_PARAMS + 4)
+#define NRC_HASH_GRAD_FLOATS (NRC_HASH_NUM_PARAMS + 4)
+nrc_status nrc_get_grad_floats(const nrc_net* net, uint64_t* n);
 nrc_status nrc_train_grad(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
                           uint32_t global_b, float* grad_d);
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h);

@@ -6,5 +6,5 @@ stream and the data-parallel sharding. The directory name contains hyphens, so i
 module ``nrc_amd`` by ``load()`` in __graft_entry__.py / tests/conftest.py / bench.py.
 """
 from . import _lib, dp, frame, stream, synthetic  # noqa: F401
-from ._lib import BATCH_SIZE, GRAD_FLOATS, NUM_PARAMS, NrcError  # noqa: F401
+from ._lib import BATCH_SIZE, GRAD_FLOATS, HASH_GRAD_FLOATS, HASH_NUM_PARAMS, NUM_PARAMS, NrcError  # noqa: F401
 from .network import HyperParams, InputEncoding, Network, StateSlot, current_stream, default_config, encode  # noqa: F401

@@ -16,6 +16,8 @@ LIB_PATH = Path(os.environ["NRC_LIB_PATH"]) if os.environ.get("NRC_LIB_PATH") el
 
 NUM_PARAMS = 22528
 GRAD_FLOATS = NUM_PARAMS + 4
+HASH_NUM_PARAMS = 1012736
+HASH_GRAD_FLOATS = HASH_NUM_PARAMS + 4
 BATCH_SIZE = 16384
 INPUT_DIMS = 15
 OUTPUT_DIMS = 3
@@ -31,7 +33,7 @@ EXPORTS = [
     "nrc_version", "nrc_last_error", "nrc_default_config", "nrc_create", "nrc_free", "nrc_init", "nrc_destroy",
     "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_train_async", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
-    "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_state", "nrc_set_state", "nrc_get_step",
+    "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_encode_fast",
     "nrc_debug_encode_fast_variant",
@@ -103,6 +105,7 @@ def lib() -> ctypes.CDLL:
         "nrc_set_state": (st, [vp, ctypes.c_int, fp]),
         "nrc_get_step": (st, [vp, ctypes.POINTER(u32)]),
         "nrc_get_num_params": (st, [vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "nrc_get_grad_floats": (st, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "nrc_debug_encode_net": (st, [vp, fp, fp, u32, vp]),
         "nrc_set_step": (st, [vp, u32]),
         "nrc_encode": (st, [fp, fp, u32, vp]),

@@ -180,7 +180,6 @@ struct nrc_net {
     float* slabs = nullptr;
     int slab_blocks = 0;
     float* loss_partials = nullptr;
-    float* grad = nullptr;  // kGradFloats scratch for the fused path
     float* loss_dev = nullptr;
     float* loss_host = nullptr;  // pinned
     // InputEncoding::Hash: grid part of the model arrays starts at n_mlp
@@ -191,6 +190,7 @@ struct nrc_net {
 
     bool hash() const { return encoding == NRC_ENCODING_HASH; }
     size_t n_total() const { return (size_t)n_mlp + (size_t)n_grid; }
+    size_t grad_floats() const { return n_total() + 4; }
 
     void release() {
         auto f = [](void* p) {
@@ -199,7 +199,7 @@ struct nrc_net {
         f(params); f(m); f(v); f(ema); f(infer);
         f(wf_train); f(wb_train); f(wf_infer);
         f(fwd_pos); f(bwd_pos);
-        f(slabs); f(loss_partials); f(grad); f(loss_dev);
+        f(slabs); f(loss_partials); f(loss_dev);
         f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
         grid_grad = nullptr;
         grid_steps = nullptr;
@@ -208,7 +208,7 @@ struct nrc_net {
         params = m = v = ema = infer = nullptr;
         wf_train = wb_train = wf_infer = nullptr;
         fwd_pos = bwd_pos = nullptr;
-        slabs = loss_partials = grad = loss_dev = loss_host = nullptr;
+        slabs = loss_partials = loss_dev = loss_host = nullptr;
         slab_blocks = 0;
         initialized = false;
     }
@@ -219,6 +219,7 @@ struct nrc_net {
         b.wf_train = wf_train; b.wb_train = wb_train; b.wf_infer = wf_infer;
         b.fwd_pos = fwd_pos; b.bwd_pos = bwd_pos;
         b.n_mlp = n_mlp;
+        b.n_total = (int)n_total();
         return b;
     }
     GridBuffers grid_buffers() const {
@@ -295,10 +296,6 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
     if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
         return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     return launch_infer(in, out, n, net->wf_infer, net->stream);
-}
-
-void require_not_hash(const nrc_net* net, const char* what) {
-    if (net->hash()) throw ApiError(NRC_ERR_UNSUPPORTED, std::string(what) + " is not implemented for InputEncoding::Hash");
 }
 
 void require_frequency(const nrc_net* net, const char* what) {
@@ -394,7 +391,6 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(float) * ng));
             HIP_CHECK(hipMemset(net->grid_steps, 0, sizeof(uint32_t) * ng));
         }
-        HIP_CHECK(hipMalloc(&net->grad, sizeof(float) * kGradFloats));
         HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
         HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
         HIP_CHECK(hipMemset(net->m, 0, pb));
@@ -559,18 +555,26 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
                           float* grad_d) {
     return guarded([&] {
         check_live(net);
-        require_not_hash(net, "nrc_train_grad");
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
         if (b == 0) {
-            HIP_CHECK(hipMemsetAsync(grad_d, 0, sizeof(float) * kGradFloats, net->stream));
+            HIP_CHECK(hipMemsetAsync(grad_d, 0, sizeof(float) * net->grad_floats(), net->stream));
             return;
         }
         if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
-        HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
-                                       net->wb_train, net->slabs, net->loss_partials, net->stream, net->encoding));
+        if (net->hash()) {
+            // the grid-table gradient is scattered (atomics) straight into the caller's buffer after the MLP part
+            float* grid_g = grad_d + net->n_mlp;
+            HIP_CHECK(hipMemsetAsync(grid_g, 0, sizeof(float) * (size_t)net->n_grid, net->stream));
+            HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
+                                        net->wb_train, net->table_train, grid_g, net->slabs, net->loss_partials,
+                                        net->stream));
+        } else {
+            HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
+                                           net->wb_train, net->slabs, net->loss_partials, net->stream, net->encoding));
+        }
         HIP_CHECK(launch_reduce_adam(kReduceOnly, net->slabs, blocks, net->loss_partials, grad_d, nullptr,
                                      net->buffers(), net->optim(net->step + 1), net->stream));
     });
@@ -579,11 +583,15 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
     return guarded([&] {
         check_live(net);
-        require_not_hash(net, "nrc_train_apply");
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         net->step += 1;
         HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
                                      net->buffers(), net->optim(net->step), net->stream));
+        if (net->hash()) {
+            GridBuffers gb = net->grid_buffers();
+            gb.grad = const_cast<float*>(grad_d) + net->n_mlp;  // read-only in kApplyOnly
+            HIP_CHECK(launch_grid_adam(kApplyOnly, gb, net->optim(net->step), net->stream));
+        }
         if (loss_h) {
             HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
             HIP_CHECK(hipStreamSynchronize(net->stream));
@@ -621,6 +629,14 @@ nrc_status nrc_get_num_params(const nrc_net* net, uint64_t* n) {
         check_live(net);
         if (!n) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output pointer");
         *n = net->n_total();
+    });
+}
+
+nrc_status nrc_get_grad_floats(const nrc_net* net, uint64_t* n) {
+    return guarded([&] {
+        check_live(net);
+        if (!n) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output");
+        *n = net->grad_floats();
     });
 }
 

@@ -20,7 +20,6 @@ constexpr int kFwdHalves = kFwdFrags * kFragHalves;  // 23552 halves = 46 KiB
 constexpr int kBwdHalves = kBwdFrags * kFragHalves;  // 17408 halves = 34 KiB
 
 // Gradient exchange buffer: loss-scaled dL/dW (NRC_NUM_PARAMS f32) followed by the minibatch loss.
-constexpr int kGradFloats = NRC_NUM_PARAMS + 4;
 
 constexpr int kTrainSamplesPerBlock = 128;  // 4 waves x 32 samples
 
@@ -123,11 +122,13 @@ struct ModelBuffers {
     _Float16 *wf_train, *wb_train, *wf_infer;
     const int *fwd_pos, *bwd_pos;
     int n_mlp;  // MLP (matrix) parameter count = slab stride: 22528 Frequency, 21504 Hash
+    int n_total;  // all parameters (MLP + grid): index of the loss in a data-parallel gradient buffer
 };
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
-    float* grad;      // f32 [n], accumulated by the training kernel, zeroed by grid_adam_kernel
+    float* grad;      // f32 [n], accumulated by the training kernel; zeroed by grid_adam_kernel (fused mode) or
+                      // read-only (kApplyOnly: the all-reduced data-parallel gradient)
     uint32_t* steps;  // per-entry Adam step counters
     _Float16 *table_train, *table_infer;
     int n;

@@ -1235,15 +1235,15 @@ __device__ __forceinline__ void dw_layer(const char* img_d, const char* img_a, c
 }
 
 // delta_{L-1} = (W_L^T delta_L) * [a_L > 0]
-template <int L>
-__device__ __forceinline__ void bwd_chain(const h8* __restrict__ lwb, const h8 (&d)[4], const h8 (&a)[4], int lane,
-                                          h8 (&dn)[4]) {
+// W(i) returns backward fragment i of this lane (register-resident or LDS image).
+template <int L, class W>
+__device__ __forceinline__ void bwd_chain(W wfrag, const h8 (&d)[4], const h8 (&a)[4], h8 (&dn)[4]) {
     constexpr int KK = (L == 5) ? 1 : 4;
     f16v c0 = zero16(), c1 = zero16();
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-        c0 = mfma(lwb[bwd_frag(L, 0, kk) * 64 + lane], d[kk], c0);
-        c1 = mfma(lwb[bwd_frag(L, 1, kk) * 64 + lane], d[kk], c1);
+        c0 = mfma(wfrag(bwd_frag(L, 0, kk)), d[kk], c0);
+        c1 = mfma(wfrag(bwd_frag(L, 1, kk)), d[kk], c1);
     }
     mask_pack(c0, a[0], a[1], dn[0], dn[1]);
     mask_pack(c1, a[2], a[3], dn[2], dn[3]);
@@ -1300,21 +1300,28 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // weight images: the sample loads go first, then every weight load; the forward images are stored to LDS
     // after the encoder, the backward images only after the forward pass (their transfer overlaps it)
     constexpr int PF = (kFwdFrags * 64 + 255) / 256, PB = (NBF * 64 + 255) / 256;
-    h8 vf[PF], vb[PB];
+    h8 vf[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int i = threadIdx.x + k * 256;
         if (i < kFwdFrags * 64) vf[k] = wf[i];
     }
+    h8 vb[PB];
 #pragma unroll
     for (int k = 0; k < PB; ++k) {
         const int i = threadIdx.x + k * 256;
         if (i < NBF * 64) vb[k] = wb[i];
     }
+    auto wfrag = [&](int i) { return lwb[i * 64 + lane]; };
     h8 x[KK0];
     if constexpr (ENC == 1) encode_hash(Q, h, grid, x);
     else if constexpr (ENC == 2) encode_sh(Q, h, x);
     else encode_fast(Q, h, x);
+    // pin the encoder here (the asm consumes x) and keep the image stores and their vmcnt waits behind it, so
+    // the encoder overlaps the weight loads instead of being sunk past the barrier
+#pragma unroll
+    for (int kk = 0; kk < KK0; ++kk) asm volatile("" : "+v"(x[kk]));
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int i = threadIdx.x + k * 256;
@@ -1391,31 +1398,31 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // compiler can interleave the two MFMA streams without an LDS write in between.
     h8 d4[4], d3[4], d2[4], d1[4], d0[4];
     dw_layer<5, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    bwd_chain<5>(lwb, g, a[4], lane, d4);
+    bwd_chain<5>(wfrag, g, a[4], d4);
     write_rows64(img_d[0], sl, h, d4);
     write_rows64(img_a[0], sl, h, a[3]);
     lds_barrier();
     stamp();
     dw_layer<4, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
-    bwd_chain<4>(lwb, d4, a[3], lane, d3);
+    bwd_chain<4>(wfrag, d4, a[3], d3);
     write_rows64(img_d[1], sl, h, d3);
     write_rows64(img_a[1], sl, h, a[2]);
     lds_barrier();
     stamp();
     dw_layer<3, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    bwd_chain<3>(lwb, d3, a[2], lane, d2);
+    bwd_chain<3>(wfrag, d3, a[2], d2);
     write_rows64(img_d[0], sl, h, d2);
     write_rows64(img_a[0], sl, h, a[1]);
     lds_barrier();
     stamp();
     dw_layer<2, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
-    bwd_chain<2>(lwb, d2, a[1], lane, d1);
+    bwd_chain<2>(wfrag, d2, a[1], d1);
     write_rows64(img_d[1], sl, h, d1);
     write_rows64(img_a[1], sl, h, a[0]);
     lds_barrier();
     stamp();
     dw_layer<1, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    bwd_chain<1>(lwb, d1, a[0], lane, d0);
+    bwd_chain<1>(wfrag, d1, a[0], d0);
     // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a[0], x_hi -> img_xh)
     write_rows64(img_d[0], sl, h, d0);
 #pragma unroll
@@ -1433,7 +1440,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     if constexpr (ENC == 1) {
         f16v c = zero16();
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) c = mfma(lwb[(kBwdFrags + kk) * 64 + lane], d0[kk], c);
+        for (int kk = 0; kk < 4; ++kk) c = mfma(wfrag(kBwdFrags + kk), d0[kk], c);
 #pragma unroll
         for (int k = 0; k < 2 * kCoarseLevels; ++k) dyc[k] = (float)(_Float16)c[k];
         if (valid) {
@@ -1571,11 +1578,11 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
             if (threadIdx.x == 0) {
-                if (mode == kReduceOnly) grad_io[mb.n_mlp] = L;
+                if (mode == kReduceOnly) grad_io[mb.n_total] = L;
                 else if (loss_out) loss_out[0] = L;
             }
         } else if (mode == kApplyOnly && loss_out && threadIdx.x == 0) {
-            loss_out[0] = grad_io[mb.n_mlp];
+            loss_out[0] = grad_io[mb.n_total];
         }
     }
     if (mode == kReduceFused || mode == kReduceOnly) {
@@ -1799,7 +1806,8 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
 
 // Sparse Adam + EMA + f16 table packs for the HashGrid parameters (tcnn non-matrix params, SURVEY §8(f) row 3;
 // oracle/nrc_hash_oracle.c orc_hash_adam_ema): an entry whose gradient is exactly zero keeps its moments, weight
-// and step counter; bias correction uses the entry's own step. The gradient is zeroed for the next step.
+// and step counter; bias correction uses the entry's own step. The fused mode zeroes the gradient for the next
+// step; kApplyOnly reads a caller's (all-reduced) gradient without writing it.
 __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1809,7 +1817,7 @@ __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb
         inf = gb.infer[i];
     } else {
         const float gradient = gb.grad[i] / oa.loss_scale;
-        gb.grad[i] = 0.0f;
+        if (mode != kApplyOnly) gb.grad[i] = 0.0f;
         if (gradient != 0.0f) {
             const uint32_t st = gb.steps[i] + 1u;
             gb.steps[i] = st;

@@ -7,8 +7,10 @@ per device (/root/reference/nrc/src/Device.cpp:420, nrc/inc/Device.h:621) and ha
   queries. No collective on the data path.
 * Training: one exchange step per minibatch. Each rank computes the loss-scaled gradient of its local
   samples normalised by the GLOBAL batch (3 * global_b), the ranks sum it (one all-reduce of
-  NRC_GRAD_FLOATS f32 = 88 KiB: RCCL over xGMI with the "nccl" backend; gloo on CPU), and every rank
-  applies the identical Adam + EMA step, so replicas stay bit-identical.
+  NRC_GRAD_FLOATS f32 = 88 KiB, or NRC_HASH_GRAD_FLOATS = 3.9 MiB with the grid-table gradient for
+  InputEncoding::Hash: RCCL over xGMI with the "nccl" backend; gloo on CPU), and every rank applies the
+  identical Adam + EMA step (Hash: plus the sparse grid Adam over the entries with a non-zero summed
+  gradient), so replicas stay bit-identical.
 
 ``backend`` is any object with ``train_grad(inputs, targets, b, global_b, grad)`` and
 ``train_apply(grad, loss)`` — ``network.Network`` on the GPU, an oracle-backed stand-in in the
@@ -32,7 +34,7 @@ class DataParallelTrainer:
         import torch.distributed as dist
 
         self.backend = backend
-        self.grad = grad_buffer  # torch tensor of GRAD_FLOATS f32 on the backend's device
+        self.grad = grad_buffer  # torch tensor of backend.grad_floats f32 on the backend's device
         self.group = group
         self._dist = dist
 

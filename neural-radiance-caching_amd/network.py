@@ -188,11 +188,12 @@ class Network:
     def train_grad(self, inputs, targets, b: int, global_b: int, grad) -> None:
         check(self._lib.nrc_train_grad(self._h, _dev_ptr(inputs, "inputs") if b else None,
                                        _dev_ptr(targets, "targets") if b else None, int(b), int(global_b),
-                                       _dev_ptr(grad, "grad", GRAD_FLOATS if hasattr(grad, "numel") else None)))
+                                       _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None)))
 
     def train_apply(self, grad, loss: bool = False):
         lh = ctypes.c_float(float("nan"))
-        check(self._lib.nrc_train_apply(self._h, _dev_ptr(grad, "grad"), ctypes.byref(lh) if loss else None))
+        check(self._lib.nrc_train_apply(self._h, _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None),
+                                        ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
     @property
@@ -200,6 +201,13 @@ class Network:
         """Parameter count of the configured model (Frequency 22,528; Hash 21,504 MLP + 991,232 grid)."""
         v = ctypes.c_uint64()
         check(self._lib.nrc_get_num_params(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def grad_floats(self) -> int:
+        """Size of the data-parallel gradient buffer: num_params + 4 (the loss sits at index num_params)."""
+        v = ctypes.c_uint64()
+        check(self._lib.nrc_get_grad_floats(self._h, ctypes.byref(v)))
         return v.value
 
     def get_state(self, slot: StateSlot = StateSlot.PARAMS) -> np.ndarray:

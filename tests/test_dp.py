@@ -3,7 +3,7 @@ with the gfx950 backend replaced by an oracle-backed stand-in that has the same 
 train_apply contract as nrc_amd.Network).
 
 Checks: contiguous query shards cover the frame exactly once; a DP step over 2 ranks equals one
-single-process step on the concatenated batch; replicas stay bit-identical.
+single-process step on the concatenated batch; replicas stay bit-identical (Frequency and Hash).
 """
 import os
 import socket
@@ -32,14 +32,17 @@ def test_shard_range_covers_exactly_once(nrc):
 class OracleBackend:
     """Stand-in for nrc_amd.Network on CPU (test only): same train_grad / train_apply contract."""
 
-    def __init__(self, params):
+    def __init__(self, params, hash_grid=False):
         self.orc = nrc_loader.load_oracle()
-        self.st = self.orc.AdamEmaState(params)
+        self.hash_grid = hash_grid
+        self.st = (self.orc.HashAdamEmaState if hash_grid else self.orc.AdamEmaState)(params)
+        self.grad_floats = params.size + 4
 
     def train_grad(self, q, t, b, global_b, grad):
         import torch
 
-        g, loss = self.orc.grad(self.st.params, q[:b], t[:b], n_total=3.0 * global_b, mode=self.orc.FP32, threads=2)
+        fn = self.orc.hash_grad if self.hash_grid else self.orc.grad
+        g, loss = fn(self.st.params, q[:b], t[:b], n_total=3.0 * global_b, mode=self.orc.FP32, threads=2)
         grad.zero_()
         grad[: g.size] = torch.from_numpy(g)
         grad[g.size] = loss
@@ -55,7 +58,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, B, steps, out_dir):
+def _init_params(orc, hash_grid):
+    if hash_grid:
+        p = orc.hash_init_params(1337)
+        p[orc.HASH_MLP_PARAMS:] = np.random.default_rng(2).uniform(-0.5, 0.5, orc.HASH_GRID_PARAMS).astype(np.float32)
+        return p
+    return orc.init_params(1337) * np.float32(1.5)
+
+
+def _worker(rank, world, port, B, steps, out_dir, hash_grid=False):
     import torch
     import torch.distributed as dist
 
@@ -64,9 +75,9 @@ def _worker(rank, world, port, B, steps, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     nrc = nrc_loader.load()
     orc = nrc_loader.load_oracle()
-    params = orc.init_params(1337) * np.float32(1.5)
-    backend = OracleBackend(params)
-    grad = torch.zeros(22528 + 4, dtype=torch.float32)
+    params = _init_params(orc, hash_grid)
+    backend = OracleBackend(params, hash_grid)
+    grad = torch.zeros(backend.grad_floats, dtype=torch.float32)
     trainer = nrc.dp.DataParallelTrainer(backend, grad)
     losses = []
     for it in range(steps):
@@ -97,4 +108,31 @@ def test_dp_step_equals_single_process_step(tmp_path):
     np.testing.assert_array_equal(p0, p1)  # replicas identical
     np.testing.assert_array_equal(np.load(tmp_path / "infer_0.npy"), np.load(tmp_path / "infer_1.npy"))
     assert np.linalg.norm(p0 - st.params) <= 1e-5 * np.linalg.norm(st.params)
+    np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
+
+
+def test_dp_step_equals_single_process_step_hash(tmp_path):
+    """InputEncoding::Hash: the exchanged buffer carries the grid-table gradient too (NRC_HASH_GRAD_FLOATS); the
+    sparse grid Adam steps the entries whose summed gradient is non-zero, as the single-process step does."""
+    import torch.multiprocessing as mp
+
+    world, B, steps = 2, 256, 2
+    mp.spawn(_worker, args=(world, _free_port(), B, steps, str(tmp_path), True), nprocs=world, join=True)
+    orc = nrc_loader.load_oracle()
+    nrc = nrc_loader.load()
+    assert nrc.HASH_GRAD_FLOATS == orc.HASH_NUM_PARAMS + 4
+    st = orc.HashAdamEmaState(_init_params(orc, True))
+    ref_losses = []
+    for it in range(steps):
+        q, t = nrc.synthetic.cornell_batch(B, seed=40 + it)
+        g, loss = orc.hash_grad(st.params, q, t, mode=orc.FP32, threads=2)
+        st.apply(g)
+        ref_losses.append(loss)
+    p0, p1 = np.load(tmp_path / "params_0.npy"), np.load(tmp_path / "params_1.npy")
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(np.load(tmp_path / "infer_0.npy"), np.load(tmp_path / "infer_1.npy"))
+    M = orc.HASH_MLP_PARAMS
+    assert np.linalg.norm(p0[:M] - st.params[:M]) <= 1e-4 * np.linalg.norm(st.params[:M])
+    moved, moved_ref = p0[M:] != _init_params(orc, True)[M:], st.params[M:] != _init_params(orc, True)[M:]
+    assert moved_ref.sum() > 1000 and np.mean(moved == moved_ref) >= 0.9999
     np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)

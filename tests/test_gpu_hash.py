@@ -164,6 +164,47 @@ def test_hash_process_frame_and_unsupported_entries(nrc, dev, hnet):
     torch.cuda.synchronize()
     assert np.isfinite(loss) and hnet.step == 4
     assert torch.isfinite(fb.output_rgba).all()
-    grad = torch.zeros(nrc.GRAD_FLOATS, device=dev)
-    with pytest.raises(nrc.NrcError):  # the data-parallel split is implemented for the Frequency config only
-        hnet.train_grad(fb.train_queries[1], fb.train_targets[1], 1024, 2048, grad)
+
+
+def test_hash_data_parallel_split_matches_fused_step(nrc, orc, dev):
+    """nrc_train_grad over two halves, summed, then nrc_train_apply == one fused step on the whole batch (up to
+    the f32 summation order of the gradients): the MLP and grid-table gradients travel in one buffer of
+    NRC_HASH_GRAD_FLOATS, and the sparse grid Adam steps the entries with a non-zero summed gradient."""
+    import torch
+    nets = []
+    for _ in range(2):
+        n = nrc.Network()
+        n.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+        n.set_state(nrc.StateSlot.PARAMS, _trained_like(orc, seed=11))
+        n.set_state(nrc.StateSlot.INFER, _trained_like(orc, seed=11))
+        nets.append(n)
+    fused, split = nets
+    try:
+        assert split.grad_floats == nrc.HASH_GRAD_FLOATS == orc.HASH_NUM_PARAMS + 4
+        with pytest.raises(ValueError):
+            split.train_grad(_t(np.zeros((8, 15), np.float32), dev), _t(np.zeros((8, 3), np.float32), dev), 8, 8,
+                             torch.zeros(nrc.GRAD_FLOATS, device=dev))
+        B = nrc.BATCH_SIZE
+        for it in range(2):
+            q, t = nrc.synthetic.cornell_batch(B, seed=300 + it)
+            qd, td = _t(q, dev), _t(t, dev)
+            loss_f = fused.train(qd, td, loss=True)
+            total = torch.zeros(split.grad_floats, device=dev)
+            for lo, hi in ((0, 6000), (6000, B)):
+                g = torch.full((split.grad_floats,), 5.0, device=dev)  # stale contents must be overwritten
+                split.train_grad(qd[lo:hi].contiguous(), td[lo:hi].contiguous(), hi - lo, B, g)
+                total += g
+            loss_s = split.train_apply(total, loss=True)
+            assert abs(loss_s - loss_f) <= 1e-5 * abs(loss_f)
+        M = orc.HASH_MLP_PARAMS
+        pf, ps = fused.get_state(nrc.StateSlot.PARAMS), split.get_state(nrc.StateSlot.PARAMS)
+        p0 = _trained_like(orc, seed=11)
+        assert rel(ps[:M], pf[:M]) <= 3e-3
+        assert np.mean(np.sign(ps[:M] - p0[:M]) == np.sign(pf[:M] - p0[:M])) >= 0.99
+        moved_f, moved_s = pf[M:] != p0[M:], ps[M:] != p0[M:]
+        assert moved_f.sum() > 10_000 and np.mean(moved_f == moved_s) >= 0.999
+        assert rel(ps[M:], pf[M:]) <= 1e-4
+        assert split.step == fused.step == 2
+    finally:
+        for n in nets:
+            n.destroy()
