@@ -88,7 +88,7 @@ __host__ __device__ constexpr int enc_k0_feature(int enc, int K) {
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s);
-constexpr int kNumInferVariants = 23;
+constexpr int kNumInferVariants = 24;
 // inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);

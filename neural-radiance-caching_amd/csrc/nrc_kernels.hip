@@ -272,7 +272,9 @@ __device__ __forceinline__ uint32_t pk2_abs(float a, float b) {
 // at most two are unsaturated: with t = 4x, fl = floor(t), fr = t - fl the kernel mass falls into the
 // unit intervals j = fl-1, fl, fl+1 as A, B-A, 1-B (A = K(-fr), B = K(1-fr)); interval j lands in bin
 // j & 3 when -4 <= j <= 7 and in bin 3 otherwise (the period-1 wrap of the formula). Returns the four
-// bins as packed f16 pairs (bins 0,1 | bins 2,3).
+// bins as packed f16 pairs (bins 0,1 | bins 2,3). IN_RANGE: the caller guarantees -3 <= t < 7, where all
+// three intervals land in bins j & 3 and the wrap bookkeeping (selects, the bin-3 surplus) drops out.
+template <bool IN_RANGE = false>
 __device__ __forceinline__ void blob_fast(float x, uint32_t& lo, uint32_t& hi) {
     const float t = x * 4.0f;
     const float fl = floorf(t);
@@ -284,18 +286,46 @@ __device__ __forceinline__ void blob_fast(float x, uint32_t& lo, uint32_t& hi) {
     const float B = fmaf(w, fmaf(w2, fmaf(w2, 3.0f / 16.0f, -10.0f / 16.0f), 15.0f / 16.0f), 0.5f);
     const float M1 = B - A, M2 = 1.0f - B;
     const int j0 = (int)fl - 1;
-    const bool in0 = (unsigned)(j0 + 4) <= 11u;
-    const bool in1 = (unsigned)(j0 + 5) <= 11u;
-    const bool in2 = (unsigned)(j0 + 6) <= 11u;
-    const float m0 = in0 ? A : 0.0f, m1 = in1 ? M1 : 0.0f, m2 = in2 ? M2 : 0.0f;
-    const float extra = (in0 ? 0.0f : A) + (in1 ? 0.0f : M1) + (in2 ? 0.0f : M2);
-    uint64_t v = (uint64_t)pk2(m0, m1) | ((uint64_t)pk2(m2, 0.0f) << 32);
     const uint32_t s = (uint32_t)(j0 & 3) << 4;
-    v = (v << s) | (v >> ((64u - s) & 63u));
-    lo = (uint32_t)v;
-    h2 hv = __builtin_bit_cast(h2, (uint32_t)(v >> 32));
-    hv[1] = hv[1] + (_Float16)extra;
-    hi = __builtin_bit_cast(uint32_t, hv);
+    if constexpr (IN_RANGE) {
+        uint64_t v = (uint64_t)pk2(A, M1) | ((uint64_t)pk2(M2, 0.0f) << 32);
+        v = (v << s) | (v >> ((64u - s) & 63u));
+        lo = (uint32_t)v;
+        hi = (uint32_t)(v >> 32);
+    } else {
+        const bool in0 = (unsigned)(j0 + 4) <= 11u;
+        const bool in1 = (unsigned)(j0 + 5) <= 11u;
+        const bool in2 = (unsigned)(j0 + 6) <= 11u;
+        const float m0 = in0 ? A : 0.0f, m1 = in1 ? M1 : 0.0f, m2 = in2 ? M2 : 0.0f;
+        const float extra = (in0 ? 0.0f : A) + (in1 ? 0.0f : M1) + (in2 ? 0.0f : M2);
+        uint64_t v = (uint64_t)pk2(m0, m1) | ((uint64_t)pk2(m2, 0.0f) << 32);
+        v = (v << s) | (v >> ((64u - s) & 63u));
+        lo = (uint32_t)v;
+        h2 hv = __builtin_bit_cast(h2, (uint32_t)(v >> 32));
+        hv[1] = hv[1] + (_Float16)extra;
+        hi = __builtin_bit_cast(uint32_t, hv);
+    }
+}
+
+// OneBlob of N inputs of this lane into words (w[2i], w[2i+1]). A wave whose inputs all satisfy -3 <= 4x < 7
+// (every query of a renderer stream: OneBlob inputs are in [0, 1]) takes the branch without the wrap
+// bookkeeping (~17 VALU less per input); bit-identical to the general branch for those inputs.
+template <int N>
+__device__ __forceinline__ void blob_many(const float (&xs)[N], uint32_t (&lo)[N], uint32_t (&hi)[N]) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float t = xs[i] * 4.0f;
+        ok = ok && (t >= -3.0f) && (t < 7.0f);
+    }
+    if (__all(ok)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) blob_fast<true>(xs[i], lo[i], hi[i]);
+    } else {
+        asm volatile("; OneBlob wrap path");  // a side effect: keeps this a branch instead of both arms + selects
+#pragma unroll
+        for (int i = 0; i < N; ++i) blob_fast<false>(xs[i], lo[i], hi[i]);
+    }
 }
 
 __device__ __forceinline__ float tri_fast(float u) {
@@ -353,9 +383,16 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
             for (int k = 0; k < 6; k += 2)
                 w[(d * 6 + k) >> 1] = pk2(tri_fast(p[d] * (float)(1 << k)), tri_fast(p[d] * (float)(2 << k)));
     }
-    blob_fast(Q.b0, w[9], w[10]);
-    blob_fast(Q.b1, w[11], w[12]);
-    blob_fast(Q.b2, w[13], w[14]);
+    {
+        const float xb[3] = {Q.b0, Q.b1, Q.b2};
+        uint32_t lo[3], hi[3];
+        blob_many<3>(xb, lo, hi);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            w[9 + 2 * i] = lo[i];
+            w[9 + 2 * i + 1] = hi[i];
+        }
+    }
     w[15] = pk2(Q.i0, Q.i1);
     w[16] = pk2(Q.i2, 1.0f);
     w[17] = w[18] = w[19] = 0x3C003C00u;  // pad features = 1.0
@@ -444,9 +481,16 @@ __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_
     w[1] = hash_level_feature<true>(Q.p0, Q.p1, Q.p2, 8 * h + 1, table);
 #pragma unroll
     for (int i = 2; i < 8; ++i) w[i] = hash_level_feature<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, table);
-    blob_fast(Q.b0, w[8], w[9]);
-    blob_fast(Q.b1, w[10], w[11]);
-    blob_fast(Q.b2, w[12], w[13]);
+    {
+        const float xb[3] = {Q.b0, Q.b1, Q.b2};
+        uint32_t lo[3], hi[3];
+        blob_many<3>(xb, lo, hi);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            w[8 + 2 * i] = lo[i];
+            w[8 + 2 * i + 1] = hi[i];
+        }
+    }
     w[14] = pk2(Q.i0, Q.i1);
     w[15] = pk2(Q.i2, 1.0f);
 #pragma unroll
@@ -499,8 +543,16 @@ __device__ __forceinline__ void encode_sh(const QLane& Q, int h, h8 (&x)[5]) {
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[9 + k] = pk2(o[2 * k], o[2 * k + 1]);
-    blob_fast(Q.b2, w[13], w[14]);
-    blob_fast(Q.x3, w[15], w[16]);
+    {
+        const float xb[2] = {Q.b2, Q.x3};
+        uint32_t lo[2], hi[2];
+        blob_many<2>(xb, lo, hi);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            w[13 + 2 * i] = lo[i];
+            w[13 + 2 * i + 1] = hi[i];
+        }
+    }
     w[17] = pk2(Q.i0, Q.i1);
     w[18] = pk2(Q.i2, 1.0f);
     w[19] = 0x3C003C00u;
@@ -626,13 +678,28 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
     }
 }
 
-// Encoder option of the production kernels: 16 = omod doubling-chain triangle wave (variant 22).
-constexpr int kDefaultAbl = 16;
+// Options of the production kernels: 16 = omod doubling-chain triangle wave (variant 22), 32 = branch-free
+// prefetch and buffer load/store epilogue (variant 23).
+constexpr int kDefaultAbl = 48;
 
 // Optional epilogue: accumulate_render_radiance (nrc_helpers.cu:77-129) fused into inference for the render
 // queries [0, n_acc) (EPI = RenderMode Full 0 / CacheOnly 2); their radiance is consumed in registers and never
 // written. Queries [n_acc, n) (the train-suffix ends) are written to out as usual. Same float operations as
 // accumulate_kernel (nrc_frame.hip), so the frame buffer is bit-identical to the unfused path.
+// Raw buffer descriptors (gfx9 dword3 = 0x00020000, stride 0): loads past num_records return 0 and stores past it
+// are dropped by the hardware, which lets a tile's tail and inactive lanes go without branches.
+typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+constexpr int kBufferOff = 0x40000000;  // an offset past every descriptor below: the access is dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+// valid rows of the 32-row tile starting at s0 in an array of n rows (0..32)
+__device__ __forceinline__ int tile_rows(int64_t n, int64_t s0) {
+    const int64_t left = n - s0;
+    return (int)(left >= 32 ? 32 : left > 0 ? left : 0);
+}
+
 struct InferEpilogue {
     const float* thr;  // [n_acc] float3 lastRenderThroughput
     float4* rgba;      // [n_acc] frame buffer
@@ -659,13 +726,21 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     const bool out16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
     const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
-    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    // wave-uniform tile index (readfirstlane: scalar address arithmetic, scalar buffer descriptors)
+    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (g >= ngroups) return;
     const int64_t last = n - 1;
 
     QLane Q[TILES];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((g * TILES + t) * 32 + r, last), h);
+    if constexpr ((ABL & 32) != 0) {
+        // stores that the hardware drops (empty descriptors): the loop is then entered with the same "prefetch
+        // loads, then the epilogue's stores" vmcnt pattern as the back-edge, so the waits inside stay exact
+        if constexpr (EPI >= 0)
+            __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
+    }
     for (; g < ngroups; g += wstride) {
         h8 x[TILES][KK0];
 #pragma unroll
@@ -684,14 +759,40 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             }
         }
         const int64_t ng = g + wstride;
-        if (ng < ngroups) {
+        if constexpr ((ABL & 32) != 0) {
+            // unconditional (clamped) prefetch: no branch around the loads, so the compiler's vmcnt bookkeeping
+            // stays exact across the loop back-edge
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((ng * TILES + t) * 32 + r, last), h);
+        } else if (ng < ngroups) {
 #pragma unroll
             for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((ng * TILES + t) * 32 + r, last), h);
         }
         // epilogue operands are fetched before the MLP so their latency hides under the MFMAs
         float tr[TILES][3];
         float4 acc[TILES];
-        if constexpr (EPI >= 0) {
+        if constexpr (EPI >= 0 && (ABL & 32) != 0) {
+            // branch-free: buffer loads whose descriptors end at n_acc return 0 past it (and for the h = 1 lanes)
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                const int64_t s0 = (g * TILES + t) * 32;
+                const int rows = tile_rows(epi.n_acc, s0);
+                const u3 tv = __builtin_amdgcn_raw_buffer_load_b96(
+                    buffer_rsrc(epi.thr + s0 * 3, rows * 12), h ? kBufferOff : r * 12, 0, 0);
+                // whole-vector bit_cast: clang 22 (ROCm 7.2) miscompiles __builtin_bit_cast(float, tv[i]) on a
+                // buffer-load result into tv[0] for every i
+                typedef float f3 __attribute__((ext_vector_type(3)));
+                const f3 tf = __builtin_bit_cast(f3, tv);
+                tr[t][0] = tf.x;
+                tr[t][1] = tf.y;
+                tr[t][2] = tf.z;
+                if constexpr (EPI == 0) {
+                    const u4 av = __builtin_amdgcn_raw_buffer_load_b128(
+                        buffer_rsrc(epi.rgba + s0, rows * 16), h ? kBufferOff : r * 16, 0, 0);
+                    acc[t] = __builtin_bit_cast(float4, av);
+                }
+            }
+        } else if constexpr (EPI >= 0) {
 #pragma unroll
             for (int t = 0; t < TILES; ++t) {
                 const int64_t s = (g * TILES + t) * 32 + r;
@@ -725,6 +826,43 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
                 }
                 continue;
             }
+        }
+        if constexpr ((ABL & 32) != 0) {
+            // every lane issues its stores: raw buffer stores whose descriptors cover only this tile's valid rows
+            // drop the tail, the h = 1 lanes and the rows that belong to the other destination in hardware, so
+            // there is no branch around a store (a conditional store leaves the next iteration's vmcnt wait at
+            // 0, i.e. waiting for the store's acknowledgement)
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                const int64_t s0 = (g * TILES + t) * 32, sq = s0 + r;
+                const float L0 = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                const float L1 = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                const float L2 = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                bool to_out = h == 0;
+                if constexpr (EPI >= 0) {
+                    float4 v;
+                    if constexpr (EPI == 0) {  // Full: dst += (T * L) * w
+                        v = acc[t];
+                        v.x = __builtin_fmaf(tr[t][0] * L0, epi.w, v.x);
+                        v.y = __builtin_fmaf(tr[t][1] * L1, epi.w, v.y);
+                        v.z = __builtin_fmaf(tr[t][2] * L2, epi.w, v.z);
+                    } else {  // CacheOnly
+                        v.x = L0 * tr[t][0];
+                        v.y = L1 * tr[t][1];
+                        v.z = L2 * tr[t][2];
+                    }
+                    v.w = 1.0f;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v),
+                                                           buffer_rsrc(epi.rgba + s0, tile_rows(epi.n_acc, s0) * 16),
+                                                           h ? kBufferOff : r * 16, 0, 0);
+                    to_out = to_out && sq >= epi.n_acc;
+                }
+                const u3 ov = {__builtin_bit_cast(uint32_t, L0), __builtin_bit_cast(uint32_t, L1),
+                               __builtin_bit_cast(uint32_t, L2)};
+                __builtin_amdgcn_raw_buffer_store_b96(ov, buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12),
+                                                      to_out ? r * 12 : kBufferOff, 0, 0);
+            }
+            continue;
         }
         if (h == 0) {
 #pragma unroll
@@ -780,6 +918,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                             int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
                                                             const uint32_t* __restrict__ grid) {
+    // ABL 0: the buffer-store epilogue (32) measured 2 % slower here (536 vs 524 us; gather-bound kernel)
     infer_v2_body<1, 512, false, 0, EPI, 1>(q, out, n, wf, epi, grid);
 }
 
@@ -997,7 +1136,8 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v4(const f
     const int h = lane >> 5, r = lane & 31;
     const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
     const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
-    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    // wave-uniform tile index (readfirstlane: scalar address arithmetic, scalar buffer descriptors)
+    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (g >= ngroups) return;
     const int64_t last = n - 1;
     const uint32_t base = (uint32_t)(uintptr_t)(lds_h8*)(lw + lane);
@@ -1670,8 +1810,9 @@ static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc,
 //   5: v2, 1 tile, 512-thread blocks, 4 waves per SIMD, prefetch
 //   6: v2, 2 tiles, 512-thread blocks, 2 waves per SIMD, prefetch
 //   7-9, 14-16: ablations (timing only); 10-13: v3 register-resident weights; 17-20: v4 asm prefetch
-//   21: variant 3 + LDS-staged 16-B result stores;  22: variant 3 + omod doubling-chain encoder (default)
-static int g_default_infer_variant = 22;  // variant 3 + omod doubling-chain encoder (A/B: 91.4 vs 93.7 us)
+//   21: variant 3 + LDS-staged 16-B result stores;  22: variant 3 + omod doubling-chain encoder
+//   23: variant 22 + branch-free prefetch and buffer-store epilogue (default)
+static int g_default_infer_variant = 23;  // variant 22 + exact vmcnt waits (A/B: 90.4 vs 94.3 us)
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s) {
@@ -1698,6 +1839,8 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 21: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 8>, 512, bpc[21], ntiles, queries, out, n, wf, s);
         // v2 variant 3 with the omod doubling-chain triangle wave (f32 output denormals flushed)
         case 22: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 16>, 512, bpc[22], ntiles, queries, out, n, wf, s);
+        // variant 22 + branch-free prefetch and buffer-store epilogue (exact vmcnt waits)
+        case 23: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48>, 512, bpc[23], ntiles, queries, out, n, wf, s);
         // v4: explicit layer-ahead weight prefetch
         case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
         case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
