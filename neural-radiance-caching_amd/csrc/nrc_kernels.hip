@@ -1249,12 +1249,20 @@ hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipSt
 // ------------------------------------------------------------------------------------------------
 // Training: one block = 4 waves = 128 samples.
 // ------------------------------------------------------------------------------------------------
-// LDS images of activations / deltas for the weight-gradient GEMMs: [128 samples][64 features] f16,
-// 128-B rows, 8-byte slots XOR-swizzled by a bijection of (s mod 16) so that both the row writes
-// (ds_write_b64, one sample per lane) and the transposed reads (ds_read_b64_tr_b16) are conflict-free.
+// LDS images of activations / deltas for the weight-gradient GEMMs: [128 samples][64 features] f16, 128-B rows.
+// A lane holds 8 features of one sample per fragment, as two 4-feature quads 8 features apart (acc_row), so the
+// quads of a row are stored permuted (bits 0 and 1 of the quad index swapped within each group of 4) to make
+// those two quads one 16-byte slot, and the 8 slots of a row are XOR-swizzled by a bijection of (s mod 8) in
+// which s and s + 2 differ in bit 2. Then the row writes are one ds_write_b128 per fragment (8 contiguous
+// lanes = 8 samples hit 8 distinct slots) and the transposed reads (ds_read_b64_tr_b16: 4 samples x 8 quads
+// per 32 lanes; samples s, s+2 share a bank half and get disjoint slot groups) are conflict-free. At one wave
+// per SIMD the 16-byte stores reach the LDS store rate where 8-byte ones do not (MI355X_MICROARCH.md §LDS):
+// 16 ds_write_b64 per wave and layer took ~1,100 cycles.
 __device__ __forceinline__ int img_off(int s, int c) {
-    const int hs = (s & 1) | (((s >> 1) & 1) << 3) | (((s >> 2) & 3) << 1);
-    return s * 128 + ((((c >> 2) ^ hs)) << 3) + ((c & 3) << 1);
+    const int lq = c >> 2;
+    const int pq = (lq & ~3) | ((lq & 1) << 1) | ((lq >> 1) & 1);
+    const int hs = (s & 1) | (((s >> 2) & 1) << 1) | (((s >> 1) & 1) << 2);
+    return s * 128 + (((pq >> 1) ^ hs) << 4) + ((pq & 1) << 3) + ((c & 3) << 1);
 }
 
 __device__ __forceinline__ h4 tr_read(const char* p) {
@@ -1292,12 +1300,11 @@ __device__ __forceinline__ void store_h4(char* img, int off, h8 v, int j0) {
     *(h4*)(img + off) = t;
 }
 
-// Write a 64-row activation/delta held as 4 B fragments (rows acc_row(kk,h,j)) into the image.
+// Write a 64-row activation/delta held as 4 B fragments (rows acc_row(kk,h,j)) into the image: fragment kk is
+// one 16-byte slot (see img_off).
 __device__ __forceinline__ void write_rows64(char* img, int sl, int h, const h8 (&f)[4]) {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int jg = 0; jg < 2; ++jg) store_h4(img, img_off(sl, acc_row(kk, h, 4 * jg)), f[kk], 4 * jg);
+    for (int kk = 0; kk < 4; ++kk) *(h8*)(img + img_off(sl, acc_row(kk, h, 0))) = f[kk];
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops (lgkmcnt) but not for its
@@ -1327,9 +1334,11 @@ __host__ __device__ constexpr int w_offset() {
 }
 
 // dW output block (mb, nb) of layer L: A = delta image (features = output rows), B = activation image.
+// Split into the MFMA chain and the slab store so that a layer step can issue the delta chain between them: the
+// wave issues in order, and a store placed right after the dW MFMAs would hold it until their results are out.
 template <int L, int ENC = 0>
-__device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, const char* img_xh, int mb, int nb,
-                                         int lane, float* __restrict__ slab) {
+__device__ __forceinline__ f16v dw_block_mfma(const char* img_d, const char* img_a, const char* img_xh, int mb, int nb,
+                                              int lane) {
     f16v acc = zero16();
     const bool zero_a = (L == 5) && (lane & 16);  // rows 16..31 of the 16-row output delta do not exist
 #pragma unroll
@@ -1341,6 +1350,11 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
         else B = tr_frag(img_a, nb, kk, lane);
         acc = mfma(A, B, acc);
     }
+    return acc;
+}
+
+template <int L, int ENC = 0>
+__device__ __forceinline__ void dw_block_store(const f16v& acc, int mb, int nb, int lane, float* __restrict__ slab) {
     const int h = lane >> 5, col = 32 * nb + (lane & 31);
     constexpr int in_dim = (L == 0) ? (ENC == 1 ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH) : NRC_WIDTH;
     constexpr int off = w_offset<L, ENC>();
@@ -1361,17 +1375,69 @@ __device__ __forceinline__ void dw_block(const char* img_d, const char* img_a, c
     }
 }
 
+// The dW blocks of layer L for this wave: 64x64 layers = 2x2 blocks (one per wave); layer 5 = 1x2 (waves 0,1);
+// Frequency layer 0 = 2x3 blocks (the third column block is the 16-wide x_hi image; waves 0,1 take two).
+template <int L, int ENC = 0>
+struct DwAcc {
+    f16v a0, a1;
+    __device__ __forceinline__ void mfma_all(const char* img_d, const char* img_a, const char* img_xh, int wave,
+                                             int lane) {
+        if (L == 5) {
+            if (wave < 2) a0 = dw_block_mfma<5, ENC>(img_d, img_a, img_xh, 0, wave, lane);
+        } else if (L == 0 && ENC != 1) {
+            a0 = dw_block_mfma<0, ENC>(img_d, img_a, img_xh, wave / 3, wave % 3, lane);
+            if (wave < 2) a1 = dw_block_mfma<0, ENC>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane);
+        } else {
+            a0 = dw_block_mfma<L, ENC>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane);
+        }
+    }
+    __device__ __forceinline__ void store_all(int wave, int lane, float* __restrict__ slab) const {
+        if (L == 5) {
+            if (wave < 2) dw_block_store<5, ENC>(a0, 0, wave, lane, slab);
+        } else if (L == 0 && ENC != 1) {
+            dw_block_store<0, ENC>(a0, wave / 3, wave % 3, lane, slab);
+            if (wave < 2) dw_block_store<0, ENC>(a1, (wave + 4) / 3, (wave + 4) % 3, lane, slab);
+        } else {
+            dw_block_store<L, ENC>(a0, wave >> 1, wave & 1, lane, slab);
+        }
+    }
+};
+
 template <int L, int ENC = 0>
 __device__ __forceinline__ void dw_layer(const char* img_d, const char* img_a, const char* img_xh, int wave, int lane,
                                          float* __restrict__ slab) {
-    if (L == 5) {
-        if (wave < 2) dw_block<5, ENC>(img_d, img_a, img_xh, 0, wave, lane, slab);
-    } else if (L == 0 && ENC != 1) {
-        dw_block<0, ENC>(img_d, img_a, img_xh, wave / 3, wave % 3, lane, slab);
-        if (wave < 2) dw_block<0, ENC>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane, slab);
-    } else {
-        dw_block<L, ENC>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane, slab);
+    DwAcc<L, ENC> d;
+    d.mfma_all(img_d, img_a, img_xh, wave, lane);
+    d.store_all(wave, lane, slab);
+}
+
+// Backward ReLU on packed halves: d = f16(acc) where the forward activation a > 0, else +0. One dword (two
+// features) costs v_cvt_pk_f16_f32 + v_pk_max_i16 + v_pk_min_i16 + v_pk_mul_lo_u16: the activation bits as i16
+// are positive exactly for a > 0 (+0, -0 and negatives are not; a ReLU output is never negative), clamped to
+// 0/1 they select the delta bits by an integer multiply. Same values as mask_pack (7 VALU per dword there)
+// except for a NaN activation, which this keeps and a > 0 drops.
+__device__ __forceinline__ uint32_t relu_gate_pk(uint32_t d, uint32_t m) {
+    // written out: the compiler folds clamp-to-0/1-and-multiply back into per-half compares and selects
+    uint32_t r;
+    asm("v_pk_max_i16 %0, %1, 0\n\t"
+        "v_pk_min_i16 %0, %0, %3\n\t"
+        "v_pk_mul_lo_u16 %0, %0, %2"
+        : "=&v"(r)
+        : "v"(m), "v"(d), "s"(0x00010001u));
+    return r;
+}
+
+__device__ __forceinline__ void mask_pack_pk(const f16v& a, const h8& m_lo, const h8& m_hi, h8& lo, h8& hi) {
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const u4v ml = __builtin_bit_cast(u4v, m_lo), mh = __builtin_bit_cast(u4v, m_hi);
+    u4v ol, oh;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ol[k] = relu_gate_pk(pk2(a[2 * k], a[2 * k + 1]), ml[k]);
+        oh[k] = relu_gate_pk(pk2(a[8 + 2 * k], a[8 + 2 * k + 1]), mh[k]);
     }
+    lo = __builtin_bit_cast(h8, ol);
+    hi = __builtin_bit_cast(h8, oh);
 }
 
 // delta_{L-1} = (W_L^T delta_L) * [a_L > 0]
@@ -1385,8 +1451,8 @@ __device__ __forceinline__ void bwd_chain(W wfrag, const h8 (&d)[4], const h8 (&
         c0 = mfma(wfrag(bwd_frag(L, 0, kk)), d[kk], c0);
         c1 = mfma(wfrag(bwd_frag(L, 1, kk)), d[kk], c1);
     }
-    mask_pack(c0, a[0], a[1], dn[0], dn[1]);
-    mask_pack(c1, a[2], a[3], dn[2], dn[3]);
+    mask_pack_pk(c0, a[0], a[1], dn[0], dn[1]);
+    mask_pack_pk(c1, a[2], a[3], dn[2], dn[3]);
 }
 
 // STAMP (diagnostic build only): wave 0 of every block records s_memtime at phase boundaries into
@@ -1525,8 +1591,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     float* slab = slabs + (int64_t)blockIdx.x * SLAB;
 
     // layer 5 operands (buffer 1): delta_5 = g (16 rows, k-step 0 only), a_5
-#pragma unroll
-    for (int jg = 0; jg < 2; ++jg) store_h4(img_d[1], img_off(sl, acc_row(0, h, 4 * jg)), g[0], 4 * jg);
+    *(h8*)(img_d[1] + img_off(sl, acc_row(0, h, 0))) = g[0];
     write_rows64(img_a[1], sl, h, a[4]);
     lds_barrier();
     if (threadIdx.x == 0) loss_partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
@@ -1537,31 +1602,52 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     // layer l comes first in program order: its operand reads are independent of the delta chain, so the
     // compiler can interleave the two MFMA streams without an LDS write in between.
     h8 d4[4], d3[4], d2[4], d1[4], d0[4];
-    dw_layer<5, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    bwd_chain<5>(wfrag, g, a[4], d4);
-    write_rows64(img_d[0], sl, h, d4);
-    write_rows64(img_a[0], sl, h, a[3]);
+    {
+        DwAcc<5, ENC> dw;
+        dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
+        bwd_chain<5>(wfrag, g, a[4], d4);
+        write_rows64(img_d[0], sl, h, d4);
+        write_rows64(img_a[0], sl, h, a[3]);
+        dw.store_all(wave, lane, slab);
+    }
     lds_barrier();
     stamp();
-    dw_layer<4, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
-    bwd_chain<4>(wfrag, d4, a[3], d3);
-    write_rows64(img_d[1], sl, h, d3);
-    write_rows64(img_a[1], sl, h, a[2]);
+    {
+        DwAcc<4, ENC> dw;
+        dw.mfma_all(img_d[0], img_a[0], img_xh, wave, lane);
+        bwd_chain<4>(wfrag, d4, a[3], d3);
+        write_rows64(img_d[1], sl, h, d3);
+        write_rows64(img_a[1], sl, h, a[2]);
+        dw.store_all(wave, lane, slab);
+    }
     lds_barrier();
     stamp();
-    dw_layer<3, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
-    bwd_chain<3>(wfrag, d3, a[2], d2);
-    write_rows64(img_d[0], sl, h, d2);
-    write_rows64(img_a[0], sl, h, a[1]);
+    {
+        DwAcc<3, ENC> dw;
+        dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
+        stamp();  // L3 sub-phases (diagnostic build only): dW issued, delta chain, image writes, slab stores, barrier
+        bwd_chain<3>(wfrag, d3, a[2], d2);
+        stamp();
+        write_rows64(img_d[0], sl, h, d2);
+        write_rows64(img_a[0], sl, h, a[1]);
+        stamp();
+        dw.store_all(wave, lane, slab);
+        stamp();
+    }
     lds_barrier();
     stamp();
-    dw_layer<2, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
-    bwd_chain<2>(wfrag, d2, a[1], d1);
-    write_rows64(img_d[1], sl, h, d1);
-    write_rows64(img_a[1], sl, h, a[0]);
+    {
+        DwAcc<2, ENC> dw;
+        dw.mfma_all(img_d[0], img_a[0], img_xh, wave, lane);
+        bwd_chain<2>(wfrag, d2, a[1], d1);
+        write_rows64(img_d[1], sl, h, d1);
+        write_rows64(img_a[1], sl, h, a[0]);
+        dw.store_all(wave, lane, slab);
+    }
     lds_barrier();
     stamp();
-    dw_layer<1, ENC>(img_d[1], img_a[1], img_xh, wave, lane, slab);
+    DwAcc<1, ENC> dw1;
+    dw1.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
     bwd_chain<1>(wfrag, d1, a[0], d0);
     // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a[0], x_hi -> img_xh)
     write_rows64(img_d[0], sl, h, d0);
@@ -1601,6 +1687,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
             }
         }
     }
+    dw1.store_all(wave, lane, slab);
     lds_barrier();
     stamp();
     if constexpr (ENC == 1) {
