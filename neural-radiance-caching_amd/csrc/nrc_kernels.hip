@@ -410,6 +410,26 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 
+// Raw buffer descriptors (gfx9 dword3 = 0x00020000, stride 0): loads past num_records return 0 and stores past it
+// are dropped by the hardware, which lets a tile's tail and inactive lanes go without branches.
+typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+constexpr int kBufferOff = 0x40000000;  // an offset past every descriptor below: the access is dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+// valid rows of the 32-row tile starting at s0 in an array of n rows (0..32)
+__device__ __forceinline__ int tile_rows(int64_t n, int64_t s0) {
+    const int64_t left = n - s0;
+    return (int)(left >= 32 ? 32 : left > 0 ? left : 0);
+}
+
+// element i (0..3) of a 16-byte load, by named components (see the bit_cast note in infer_v2_body)
+__device__ __forceinline__ uint32_t pick4(const u4& q, uint32_t i) {
+    const uint32_t lo = (i & 1u) ? q.y : q.x, hi = (i & 1u) ? q.w : q.z;
+    return (i & 2u) ? hi : lo;
+}
+
 struct HashCorners {
     uint32_t entry[8];  // global table entries
     float w[8];         // trilinear weights, tcnn order ((1 * wx) * wy) * wz
@@ -458,9 +478,22 @@ __device__ __forceinline__ uint32_t hash_level_feature(float px, float py, float
                                                         const uint32_t* __restrict__ table) {
     HashCorners C;
     hash_corners<DENSE_OK>(px, py, pz, l, C);
+    // Corners 2p and 2p+1 differ only in x: their entries share an aligned group of 4 unless the x carry leaves
+    // it (hashed: cell x = 3 mod 4; dense: entry = 3 mod 4), i.e. for 1 lane in 4. One 16-byte load of the
+    // group serves both; the partner gets its own 4-byte load only when it lies outside (the buffer load of the
+    // other lanes is dropped by the descriptor bound and touches no cache line): 1.25 cache-line accesses per
+    // corner pair instead of 2 — the random gathers run at the L1 line rate.
+    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(table, NRC_HASH_ENTRIES * 4);
     uint32_t v[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = table[C.entry[c]];
+    for (int p = 0; p < 4; ++p) {
+        const uint32_t e0 = C.entry[2 * p], e1 = C.entry[2 * p + 1];
+        const u4 quad = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((e0 & ~3u) * 4u), 0, 0);
+        const bool same = (e1 >> 2) == (e0 >> 2);
+        const uint32_t far = __builtin_amdgcn_raw_buffer_load_b32(rs, same ? kBufferOff : (int)(e1 * 4u), 0, 0);
+        v[2 * p] = pick4(quad, e0 & 3u);
+        v[2 * p + 1] = same ? pick4(quad, e1 & 3u) : far;
+    }
     h2v acc = {(_Float16)0.0f, (_Float16)0.0f};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -477,10 +510,15 @@ __device__ __forceinline__ uint32_t hash_level_feature(float px, float py, float
 // one pad; as 4 B fragments.
 __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_t* __restrict__ table, h8 (&x)[4]) {
     uint32_t w[16];
+    // levels in two groups of 4 with a scheduling fence between them: the compiler otherwise hoists every
+    // level's gathers (8 x 4 x 20 B per lane) ahead of the interpolation and runs out of registers
     w[0] = hash_level_feature<true>(Q.p0, Q.p1, Q.p2, 8 * h + 0, table);
     w[1] = hash_level_feature<true>(Q.p0, Q.p1, Q.p2, 8 * h + 1, table);
 #pragma unroll
-    for (int i = 2; i < 8; ++i) w[i] = hash_level_feature<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, table);
+    for (int i = 2; i < 8; ++i) {
+        if (i == 4) asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+        w[i] = hash_level_feature<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, table);
+    }
     {
         const float xb[3] = {Q.b0, Q.b1, Q.b2};
         uint32_t lo[3], hi[3];
@@ -686,20 +724,6 @@ constexpr int kDefaultAbl = 48;
 // queries [0, n_acc) (EPI = RenderMode Full 0 / CacheOnly 2); their radiance is consumed in registers and never
 // written. Queries [n_acc, n) (the train-suffix ends) are written to out as usual. Same float operations as
 // accumulate_kernel (nrc_frame.hip), so the frame buffer is bit-identical to the unfused path.
-// Raw buffer descriptors (gfx9 dword3 = 0x00020000, stride 0): loads past num_records return 0 and stores past it
-// are dropped by the hardware, which lets a tile's tail and inactive lanes go without branches.
-typedef uint32_t u3 __attribute__((ext_vector_type(3)));
-typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-constexpr int kBufferOff = 0x40000000;  // an offset past every descriptor below: the access is dropped
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
-}
-// valid rows of the 32-row tile starting at s0 in an array of n rows (0..32)
-__device__ __forceinline__ int tile_rows(int64_t n, int64_t s0) {
-    const int64_t left = n - s0;
-    return (int)(left >= 32 ? 32 : left > 0 ? left : 0);
-}
-
 struct InferEpilogue {
     const float* thr;  // [n_acc] float3 lastRenderThroughput
     float4* rgba;      // [n_acc] frame buffer
