@@ -184,7 +184,7 @@ struct nrc_net {
     float* loss_host = nullptr;  // pinned
     // InputEncoding::Hash: grid part of the model arrays starts at n_mlp
     int n_mlp = NRC_NUM_PARAMS, n_grid = 0;
-    float* grid_grad = nullptr;
+    _Float16* grid_grad = nullptr;  // f16 [n_grid]: half2 per entry, packed-half atomics (tcnn)
     uint32_t* grid_steps = nullptr;
     _Float16 *table_train = nullptr, *table_infer = nullptr;
 
@@ -225,7 +225,7 @@ struct nrc_net {
     GridBuffers grid_buffers() const {
         GridBuffers g;
         g.params = params + n_mlp; g.m = m + n_mlp; g.v = v + n_mlp; g.ema = ema + n_mlp; g.infer = infer + n_mlp;
-        g.grad = grid_grad; g.steps = grid_steps;
+        g.grad16 = grid_grad; g.grad32 = nullptr; g.steps = grid_steps;
         g.table_train = table_train; g.table_infer = table_infer;
         g.n = n_grid;
         return g;
@@ -384,11 +384,11 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMalloc(&net->bwd_pos, sizeof(int) * net->n_mlp));
         if (net->hash()) {
             const size_t ng = (size_t)net->n_grid;
-            HIP_CHECK(hipMalloc(&net->grid_grad, sizeof(float) * ng));
+            HIP_CHECK(hipMalloc(&net->grid_grad, sizeof(_Float16) * ng));
             HIP_CHECK(hipMalloc(&net->grid_steps, sizeof(uint32_t) * ng));
             HIP_CHECK(hipMalloc(&net->table_train, sizeof(_Float16) * ng));
             HIP_CHECK(hipMalloc(&net->table_infer, sizeof(_Float16) * ng));
-            HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(float) * ng));
+            HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(_Float16) * ng));
             HIP_CHECK(hipMemset(net->grid_steps, 0, sizeof(uint32_t) * ng));
         }
         HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
@@ -565,12 +565,12 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
         if (net->hash()) {
-            // the grid-table gradient is scattered (atomics) straight into the caller's buffer after the MLP part
-            float* grid_g = grad_d + net->n_mlp;
-            HIP_CHECK(hipMemsetAsync(grid_g, 0, sizeof(float) * (size_t)net->n_grid, net->stream));
+            // the grid-table gradient accumulates in the handle's f16 buffer (packed-half atomics) and is exported as
+            // f32 into the caller's buffer after the MLP part; the export zeroes the f16 buffer again
             HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
-                                        net->wb_train, net->table_train, grid_g, net->slabs, net->loss_partials,
+                                        net->wb_train, net->table_train, net->grid_grad, net->slabs, net->loss_partials,
                                         net->stream));
+            HIP_CHECK(launch_grid_grad_export(net->grid_grad, grad_d + net->n_mlp, net->n_grid, net->stream));
         } else {
             HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
                                            net->wb_train, net->slabs, net->loss_partials, net->stream, net->encoding));
@@ -589,7 +589,7 @@ nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
                                      net->buffers(), net->optim(net->step), net->stream));
         if (net->hash()) {
             GridBuffers gb = net->grid_buffers();
-            gb.grad = const_cast<float*>(grad_d) + net->n_mlp;  // read-only in kApplyOnly
+            gb.grad32 = grad_d + net->n_mlp;  // read-only in kApplyOnly
             HIP_CHECK(launch_grid_adam(kApplyOnly, gb, net->optim(net->step), net->stream));
         }
         if (loss_h) {

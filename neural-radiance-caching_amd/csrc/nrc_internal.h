@@ -127,15 +127,16 @@ struct ModelBuffers {
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
-    float* grad;      // f32 [n], accumulated by the training kernel; zeroed by grid_adam_kernel (fused mode) or
-                      // read-only (kApplyOnly: the all-reduced data-parallel gradient)
+    _Float16* grad16;     // f16 [n] (half2 per entry), accumulated by the training kernel, zeroed by grid_adam_kernel
+    const float* grad32;  // kApplyOnly: the all-reduced data-parallel gradient (f32 [n], read-only)
     uint32_t* steps;  // per-entry Adam step counters
     _Float16 *table_train, *table_infer;
     int n;
 };
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
+hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
-                             const _Float16* wf, const _Float16* wb, const _Float16* grid, float* grid_grad,
+                             const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,

@@ -1479,10 +1479,17 @@ __device__ __forceinline__ void bwd_chain(W wfrag, const h8 (&d)[4], const h8 (&
     mask_pack_pk(c1, a[2], a[3], dn[2], dn[3]);
 }
 
+// grid_grad[e] += (half2){a, b}: each product rounded to f16, accumulated in f16 at the memory side
+__device__ __forceinline__ void grid_atomic(h2v* __restrict__ grid_grad, uint32_t e, float a, float b) {
+    const h2v v = {(_Float16)a, (_Float16)b};
+    __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v*)(grid_grad + e), v);
+}
+
 // STAMP (diagnostic build only): wave 0 of every block records s_memtime at phase boundaries into
 // stamps[block][16]; the product instantiation (STAMP = false) executes no stamp.
 // ENC 1 (InputEncoding::Hash): 64-wide layer 0, grid table `grid` (f16x2, training weights); the grid-feature
-// gradient W0^T delta_0 is scattered into grid_grad (f32 [entry][2]) with atomics.
+// gradient W0^T delta_0 is scattered into grid_grad (f16x2 per entry) with packed-half atomics, as tcnn's
+// kernel_grid_backward does (half2 atomicAdd): one 4-byte atomic per corner for both features.
 template <bool STAMP, int ENC = 0>
 __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                        int64_t b, float n_total, float loss_scale,
@@ -1490,7 +1497,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
                                                        float* __restrict__ slabs, float* __restrict__ loss_partials,
                                                        uint64_t* __restrict__ stamps,
                                                        const uint32_t* __restrict__ grid = nullptr,
-                                                       float* __restrict__ grid_grad = nullptr) {
+                                                       h2v* __restrict__ grid_grad = nullptr) {
     constexpr int KK0 = ENC == 1 ? 4 : 5;
     constexpr int NBF = ENC == 1 ? kBwdFragsHash : kBwdFrags;
     constexpr int SLAB = ENC == 1 ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS;
@@ -1703,11 +1710,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
                 if (i <= 1) hash_corners<true>(Q.p0, Q.p1, Q.p2, 8 * h + i, C);
                 else hash_corners<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, C);
 #pragma unroll
-                for (int cc = 0; cc < 8; ++cc) {
-                    float* gp = grid_grad + 2 * (size_t)C.entry[cc];
-                    if (dy0 != 0.0f) unsafeAtomicAdd(gp, C.w[cc] * dy0);
-                    if (dy1 != 0.0f) unsafeAtomicAdd(gp + 1, C.w[cc] * dy1);
-                }
+                for (int cc = 0; cc < 8; ++cc) grid_atomic(grid_grad, C.entry[cc], C.w[cc] * dy0, C.w[cc] * dy1);
             }
         }
     }
@@ -1748,10 +1751,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
                         }
                         slot = (slot + 1) & (kSlots - 1);
                     }
-                    if (!done) {  // table crowded: direct global atomics for this corner
-                        unsafeAtomicAdd(grid_grad + 2 * (size_t)e, C.w[cc] * dy0);
-                        unsafeAtomicAdd(grid_grad + 2 * (size_t)e + 1, C.w[cc] * dy1);
-                    }
+                    if (!done) grid_atomic(grid_grad, e, C.w[cc] * dy0, C.w[cc] * dy1);  // table crowded
                 }
             }
         }
@@ -1759,8 +1759,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         for (int i = threadIdx.x; i < kSlots; i += 256) {
             const uint32_t e = tkey[i];
             if (e == 0xFFFFFFFFu) continue;
-            unsafeAtomicAdd(grid_grad + 2 * (size_t)e, tval[2 * i]);
-            unsafeAtomicAdd(grid_grad + 2 * (size_t)e + 1, tval[2 * i + 1]);
+            grid_atomic(grid_grad, e, tval[2 * i], tval[2 * i + 1]);
         }
     } else {
         dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
@@ -2060,8 +2059,9 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
 
 // Sparse Adam + EMA + f16 table packs for the HashGrid parameters (tcnn non-matrix params, SURVEY §8(f) row 3;
 // oracle/nrc_hash_oracle.c orc_hash_adam_ema): an entry whose gradient is exactly zero keeps its moments, weight
-// and step counter; bias correction uses the entry's own step. The fused mode zeroes the gradient for the next
-// step; kApplyOnly reads a caller's (all-reduced) gradient without writing it.
+// and step counter; bias correction uses the entry's own step. The fused mode reads the f16 gradient the training
+// kernel accumulated and zeroes it for the next step; kApplyOnly reads a caller's (all-reduced) f32 gradient
+// without writing it.
 __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -2070,8 +2070,13 @@ __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb
     if (mode == kPackOnly) {
         inf = gb.infer[i];
     } else {
-        const float gradient = gb.grad[i] / oa.loss_scale;
-        if (mode != kApplyOnly) gb.grad[i] = 0.0f;
+        float gradient;
+        if (mode == kApplyOnly) {
+            gradient = gb.grad32[i] / oa.loss_scale;
+        } else {
+            gradient = (float)gb.grad16[i] / oa.loss_scale;
+            gb.grad16[i] = (_Float16)0.0f;
+        }
         if (gradient != 0.0f) {
             const uint32_t st = gb.steps[i] + 1u;
             gb.steps[i] = st;
@@ -2102,13 +2107,27 @@ hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa
     return hipGetLastError();
 }
 
+// Data-parallel export of the f16 grid gradient: f32 copy into the exchange buffer, source zeroed for the next step.
+__global__ __launch_bounds__(256) void grid_grad_export_kernel(_Float16* __restrict__ g16, float* __restrict__ g32,
+                                                               int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    g32[i] = (float)g16[i];
+    g16[i] = (_Float16)0.0f;
+}
+
+hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t s) {
+    hipLaunchKernelGGL(grid_grad_export_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g16, g32, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
-                             const _Float16* wf, const _Float16* wb, const _Float16* grid, float* grid_grad,
+                             const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s) {
     if (b <= 0) return hipSuccess;
     hipLaunchKernelGGL((train_kernel<false, 1>), dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
-                       reinterpret_cast<const uint32_t*>(grid), grid_grad);
+                       reinterpret_cast<const uint32_t*>(grid), reinterpret_cast<h2v*>(grid_grad));
     return hipGetLastError();
 }
 

@@ -17,8 +17,10 @@
  *  [M] grid parameters initialised uniform in [-1e-4, 1e-4]; stored as f16 for the forward (PARAMS_T);
  *      interpolation as tcnn's kernel_grid: result = fma((half)weight, value, result) in half precision,
  *      corners in order 0..7 (MIXED and TCNN modes; the GPU's v_pk_fma_f16). FP32 mode: exact f64 sum.
- *  [M] grid gradient: sum over samples and corners of weight * dL/dfeature; tcnn accumulates it with f16
- *      atomics [L]; here f64 (oracle) / f32 atomics (GPU).
+ *  [M] grid gradient: sum over samples and corners of weight * dL/dfeature; tcnn accumulates it with half2
+ *      atomics [L], as the GPU build does. Here (MIXED / TCNN) every contribution weight * dy is rounded to f16,
+ *      the contributions are summed in f64 and the sum is rounded to f16; the atomics' per-add f16 rounding in
+ *      arbitrary order is not reproducible, so the tests compare the grid update with sign / support tolerances.
  *  [M] tcnn Adam treats the grid as non-matrix parameters: no l2 regularisation, an entry whose gradient is
  *      exactly zero is skipped (moments, weight and its step counter untouched), and bias correction uses
  *      the entry's own step counter. The EMA wrapper filters every parameter every step [L].
@@ -282,7 +284,9 @@ static void* grad_job(void* arg) {
                     for (int f = 0; f < 2; ++f) {
                         const float dy = rnd(nd[2 * lv + f], mode);
                         if (dy == 0.0f) continue;
-                        for (int c = 0; c < 8; ++c) G[2 * idx[c] + f] += (double)w[c] * (double)dy;
+                        for (int c = 0; c < 8; ++c)
+                            G[2 * idx[c] + f] += mode == ORC_FP32 ? (double)w[c] * (double)dy
+                                                                  : (double)orc_f16_round(w[c] * dy);
                     }
                 }
                 break;
@@ -324,7 +328,8 @@ double orc_hash_grad(const float* params, const float* queries, const float* tar
     for (int i = 0; i < NRC_HASH_NUM_PARAMS; ++i) {
         double acc = 0.0;
         for (int t = 0; t < nthreads; ++t) acc += jobs[t].grad[i];
-        grad[i] = (float)acc;
+        /* the grid gradient is an f16 buffer (half2 atomics) except in FP32 mode */
+        grad[i] = (i >= NRC_HASH_GRID_OFFSET && mode != ORC_FP32) ? orc_f16_round_double(acc) : (float)acc;
     }
     for (int t = 0; t < nthreads; ++t) {
         loss += jobs[t].loss;

@@ -5,8 +5,8 @@ Tolerances (stated here): encoder features within 1 f16 ulp; inf
 most 0.1 % of queries beyond 16 f16 ulps; one training step: loss rel <= 1e-3, MLP weights rel-L2 <= 3e-3 with
 >= 99 % of update signs equal,
 grid entries: the same set of entries updated (>= 99.5 %) with the same update sign (>= 99 %) — the first Adam
-step moves every touched entry by +-lr, so the sign is the whole update; the grid gradient is summed with f32
-atomics in an arbitrary order (tcnn: f16 atomics), so training is not bitwise reproducible in this mode."""
+step moves every touched entry by +-lr, so the sign is the whole update; the grid gradient is summed with half2
+atomics in an arbitrary order (as tcnn's), so training is not bitwise reproducible in this mode."""
 import numpy as np
 import pytest
 
@@ -203,7 +203,9 @@ def test_hash_data_parallel_split_matches_fused_step(nrc, orc, dev):
         assert np.mean(np.sign(ps[:M] - p0[:M]) == np.sign(pf[:M] - p0[:M])) >= 0.99
         moved_f, moved_s = pf[M:] != p0[M:], ps[M:] != p0[M:]
         assert moved_f.sum() > 10_000 and np.mean(moved_f == moved_s) >= 0.999
-        assert rel(ps[M:], pf[M:]) <= 1e-4
+        # the grid gradient accumulates in f16 (half2 atomics, as tcnn): the two halves round differently from the
+        # whole batch, and an entry whose near-zero gradient flips sign moves by 2 lr — a handful of the ~1e5
+        assert rel(ps[M:], pf[M:]) <= 5e-4
         assert split.step == fused.step == 1
     finally:
         for n in nets:
