@@ -69,6 +69,36 @@ void init_params_hash(std::vector<float>& p, uint64_t seed) {
     for (int i = 0; i < NRC_HASH_GRID_PARAMS; ++i) p[NRC_HASH_GRID_OFFSET + i] = (g.next_float() * 2.0f - 1.0f) * 1e-4f;
 }
 
+// Parameter of every position of the fragment-major weight-gradient slab (nrc_internal.h slab_block_base):
+// position (block, j, lane, e) holds accumulator register 4j + e of that lane, i.e. dW[row][col] with
+// row = 32 mb + (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5), col = 32 nb + (lane & 31) (layer 0: K slot -> feature).
+std::vector<int> build_slab_map(int encoding) {
+    const bool hash = encoding == NRC_ENCODING_HASH;
+    const int enc = hash ? 1 : encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0;
+    const int in0 = hash ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH;
+    int off[NRC_NUM_LAYERS];
+    for (int l = 0; l < NRC_NUM_LAYERS; ++l)
+        off[l] = hash ? (l == 0 ? NRC_HASH_W0_OFFSET : l <= 4 ? NRC_HASH_W1_OFFSET + (l - 1) * 4096 : NRC_HASH_W5_OFFSET)
+                      : kLayerOff[l];
+    std::vector<int> m(slab_floats(enc), -1);
+    for (int L = 0; L < NRC_NUM_LAYERS; ++L) {
+        const int nmb = L == 5 ? 1 : 2, nnb = L == 0 ? slab_l0_nb(enc) : 2, nreg = L == 5 ? 8 : 16;
+        const int in_dim = L == 0 ? in0 : 64;
+        for (int mb = 0; mb < nmb; ++mb)
+            for (int nb = 0; nb < nnb; ++nb)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int reg = 0; reg < nreg; ++reg) {
+                        const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+                        const int col = 32 * nb + (lane & 31);
+                        if (L == 0 && col >= in0) continue;  // x_hi block lanes past the 80 inputs
+                        const int fcol = L == 0 ? enc_k0_feature(enc, col) : col;
+                        const int pos = slab_block_base(enc, L, mb, nb) + ((reg >> 2) * 64 + lane) * 4 + (reg & 3);
+                        m[pos] = off[L] + row * in_dim + fcol;
+                    }
+    }
+    return m;
+}
+
 // Position of every canonical parameter inside the forward / backward MFMA fragment images.
 void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd, int encoding) {
     const bool hash = encoding == NRC_ENCODING_HASH;
@@ -177,6 +207,8 @@ struct nrc_net {
     float *params = nullptr, *m = nullptr, *v = nullptr, *ema = nullptr, *infer = nullptr;
     _Float16 *wf_train = nullptr, *wb_train = nullptr, *wf_infer = nullptr;
     int *fwd_pos = nullptr, *bwd_pos = nullptr;
+    int* slab_param = nullptr;  // [n_slab] parameter of each weight-gradient slab position
+    int n_slab = 0;
     float* slabs = nullptr;
     int slab_blocks = 0;
     float* loss_partials = nullptr;
@@ -198,7 +230,7 @@ struct nrc_net {
         };
         f(params); f(m); f(v); f(ema); f(infer);
         f(wf_train); f(wb_train); f(wf_infer);
-        f(fwd_pos); f(bwd_pos);
+        f(fwd_pos); f(bwd_pos); f(slab_param);
         f(slabs); f(loss_partials); f(loss_dev);
         f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
         grid_grad = nullptr;
@@ -208,6 +240,7 @@ struct nrc_net {
         params = m = v = ema = infer = nullptr;
         wf_train = wb_train = wf_infer = nullptr;
         fwd_pos = bwd_pos = nullptr;
+        slab_param = nullptr;
         slabs = loss_partials = loss_dev = loss_host = nullptr;
         slab_blocks = 0;
         initialized = false;
@@ -220,6 +253,8 @@ struct nrc_net {
         b.fwd_pos = fwd_pos; b.bwd_pos = bwd_pos;
         b.n_mlp = n_mlp;
         b.n_total = (int)n_total();
+        b.slab_param = slab_param;
+        b.n_slab = n_slab;
         return b;
     }
     GridBuffers grid_buffers() const {
@@ -243,7 +278,7 @@ struct nrc_net {
         slabs = nullptr;
         loss_partials = nullptr;
         slab_blocks = 0;
-        HIP_CHECK(hipMalloc(&slabs, sizeof(float) * (size_t)blocks * n_mlp));
+        HIP_CHECK(hipMalloc(&slabs, sizeof(float) * (size_t)blocks * n_slab));
         HIP_CHECK(hipMalloc(&loss_partials, sizeof(float) * (size_t)blocks));
         slab_blocks = blocks;
     }
@@ -404,6 +439,12 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         build_scatter_maps(fwd, bwd, net->encoding);
         HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
+        {
+            const std::vector<int> sm = build_slab_map(net->encoding);
+            net->n_slab = (int)sm.size();
+            HIP_CHECK(hipMalloc(&net->slab_param, sizeof(int) * sm.size()));
+            HIP_CHECK(hipMemcpy(net->slab_param, sm.data(), sizeof(int) * sm.size(), hipMemcpyHostToDevice));
+        }
         std::vector<float> p(net->n_total());
         if (net->hash()) init_params_hash(p, net->cfg.seed);
         else init_params(p, net->cfg.seed);

@@ -117,12 +117,28 @@ struct OptimArgs {
     float lr, beta1, beta2, eps, l2_reg, ema_decay, loss_scale;
     uint32_t step;
 };
+// Per-block weight-gradient slab, fragment-major: the 32x32 dW blocks one after another (layer 0 blocks (mb, nb)
+// with nb over 3 column blocks (80-wide input incl. the x_hi block) or 2 (Hash), layers 1..4 blocks (mb, nb), layer 5
+// the two 16x32 halves), each block as [j = 0..3][lane 0..63][4 floats]: register 4j + e of lane `lane` of the
+// MFMA accumulator. The training kernel then writes every block with lane-contiguous 16-byte stores; the reduce
+// maps positions to parameters through ModelBuffers::slab_param (-1 for the x_hi block's padding lanes).
+__host__ __device__ constexpr int slab_l0_nb(int enc) { return enc == 1 ? 2 : 3; }
+__host__ __device__ constexpr int slab_block_base(int enc, int L, int mb, int nb) {
+    return L == 0 ? (mb * slab_l0_nb(enc) + nb) * 1024
+           : L <= 4 ? 2 * slab_l0_nb(enc) * 1024 + (L - 1) * 4096 + (mb * 2 + nb) * 1024
+                    : 2 * slab_l0_nb(enc) * 1024 + 4 * 4096 + nb * 512;
+}
+__host__ __device__ constexpr int slab_floats(int enc) { return slab_block_base(enc, 5, 0, 2); }
+static_assert(slab_floats(0) == 23552 && slab_floats(1) == NRC_HASH_MLP_PARAMS, "slab sizes");
+
 struct ModelBuffers {
     float *params, *m, *v, *ema, *infer;  // f32 master / Adam / EMA / debiased EMA (inference)
     _Float16 *wf_train, *wb_train, *wf_infer;
     const int *fwd_pos, *bwd_pos;
     int n_mlp;  // MLP (matrix) parameter count = slab stride: 22528 Frequency, 21504 Hash
     int n_total;  // all parameters (MLP + grid): index of the loss in a data-parallel gradient buffer
+    const int* slab_param;  // [n_slab] parameter of each slab position, -1 = padding
+    int n_slab;             // slab stride (floats per training block)
 };
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
 struct GridBuffers {

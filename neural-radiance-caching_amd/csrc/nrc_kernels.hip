@@ -1379,23 +1379,15 @@ __device__ __forceinline__ f16v dw_block_mfma(const char* img_d, const char* img
 
 template <int L, int ENC = 0>
 __device__ __forceinline__ void dw_block_store(const f16v& acc, int mb, int nb, int lane, float* __restrict__ slab) {
-    const int h = lane >> 5, col = 32 * nb + (lane & 31);
-    constexpr int in_dim = (L == 0) ? (ENC == 1 ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH) : NRC_WIDTH;
-    constexpr int off = w_offset<L, ENC>();
-    int fcol = col;
-    if (L == 0) {
-        if (ENC == 1) {
-            fcol = hash_k0_feature(col);
-        } else {
-            if (col >= NRC_ENC_WIDTH) return;
-            fcol = enc_k0_feature(ENC, col);
-        }
-    }
+    // fragment-major slab block (slab_block_base): 4 (layer 5: 2) lane-contiguous 16-byte stores per lane
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4* dst = (f4*)(slab + slab_block_base(ENC, L, mb, nb));
+    constexpr int J = L == 5 ? 2 : 4;  // layer 5: registers 0..7 hold the 16 real rows
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (L == 5 && row >= NRC_OUT_PADDED) continue;
-        __builtin_nontemporal_store(acc[reg], &slab[off + row * in_dim + fcol]);  // streamed, read once
+    for (int j = 0; j < J; ++j) {
+        const f4 v = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
+        // streamed: nontemporal (plain stores measured 18.8 -> 20.7 us per step)
+        __builtin_nontemporal_store(v, &dst[j * 64 + lane]);
     }
 }
 
@@ -1500,7 +1492,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
                                                        h2v* __restrict__ grid_grad = nullptr) {
     constexpr int KK0 = ENC == 1 ? 4 : 5;
     constexpr int NBF = ENC == 1 ? kBwdFragsHash : kBwdFrags;
-    constexpr int SLAB = ENC == 1 ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS;
+    constexpr int SLAB = slab_floats(ENC);
     int nst = 0;
     auto stamp = [&]() {
         if (STAMP) {
@@ -1656,14 +1648,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     {
         DwAcc<3, ENC> dw;
         dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
-        stamp();  // L3 sub-phases (diagnostic build only): dW issued, delta chain, image writes, slab stores, barrier
         bwd_chain<3>(wfrag, d3, a[2], d2);
-        stamp();
         write_rows64(img_d[0], sl, h, d2);
         write_rows64(img_a[0], sl, h, a[1]);
-        stamp();
         dw.store_all(wave, lane, slab);
-        stamp();
     }
     lds_barrier();
     stamp();
@@ -1775,8 +1763,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 // the groups are combined in LDS in a fixed tree: the result is bitwise reproducible for a given slab count.
 constexpr int kRedParams = 16, kRedGroups = 16, kRedThreads = kRedParams * kRedGroups;
 constexpr int kRedVec = 4;  // floats per thread: one 16-byte load per slab
-static_assert(NRC_NUM_PARAMS % (kRedParams * 4) == 0 && NRC_HASH_MLP_PARAMS % (kRedParams * 4) == 0,
-              "parameter counts must tile the reduction");
+static_assert(NRC_NUM_PARAMS % (kRedParams * 4) == 0 && NRC_HASH_MLP_PARAMS % (kRedParams * 4) == 0 &&
+                  slab_floats(0) % (kRedParams * 4) == 0 && slab_floats(1) % (kRedParams * 4) == 0,
+              "parameter counts and slab sizes must tile the reduction");
 
 __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const ModelBuffers& mb, const OptimArgs& oa,
                                               float lr_t, float ema_debias) {
@@ -1820,7 +1809,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ f4 part[kRedGroups][kRedParams];
     const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
-    const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;
+    const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;  // slab position (reduce modes) / parameter (apply, pack)
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
@@ -1842,7 +1831,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             f4 v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                v[u] = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)(i + u * kRedGroups) * mb.n_mlp + p0]);
+                v[u] = *(const f4*)&slabs[(int64_t)(i + u * kRedGroups) * mb.n_slab + p0];  // plain loads: 0.4 us
+                                                                                          // faster than nontemporal
 #pragma unroll
             for (int u = 0; u < 8; u += 2) {
                 a0 += v[u];
@@ -1850,7 +1840,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             }
         }
         for (int u = 0; i < nslabs; i += kRedGroups, ++u) {
-            const f4 v = __builtin_nontemporal_load((const f4*)&slabs[(int64_t)i * mb.n_mlp + p0]);
+            const f4 v = *(const f4*)&slabs[(int64_t)i * mb.n_slab + p0];
             if (u & 1) a1 += v;
             else a0 += v;
         }
@@ -1863,7 +1853,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 #pragma unroll
         for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][lp][comp] + part[2 * u + 1][lp][comp];
         const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
-        const int p = blockIdx.x * kRedParams * kRedVec + threadIdx.x;
+        const int p = mb.slab_param[blockIdx.x * kRedParams * kRedVec + threadIdx.x];
+        if (p < 0) return;  // padding position (x_hi block lanes past the 80 inputs)
         if (mode == kReduceOnly) {
             grad_io[p] = g1;
             return;
@@ -2137,7 +2128,8 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
     const float step = (float)(oa.step ? oa.step : 1);
     const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
     const float ema_debias = 1.0f - powf(oa.ema_decay, step);
-    const int grid = mb.n_mlp / (kRedParams * kRedVec);
+    // reduce modes walk the slab positions, apply / pack modes the parameters
+    const int grid = (mode == kReduceFused || mode == kReduceOnly ? mb.n_slab : mb.n_mlp) / (kRedParams * kRedVec);
     hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
                        loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();

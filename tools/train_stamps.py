@@ -9,9 +9,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import nrc_loader  # noqa: E402
 
-PHASES = ["start", "weights+encode", "forward", "loss+img5", "L5", "L4", "L3.dw", "L3.chain", "L3.write", "L3.store",
-          "L3.barrier",
-          "L2", "L1", "L0"]
+PHASES = ["start", "weights+encode", "forward", "loss+img5", "L5", "L4", "L3", "L2", "L1", "L0"]
 
 
 def main():
