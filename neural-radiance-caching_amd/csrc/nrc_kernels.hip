@@ -1829,10 +1829,9 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         int i = grp;
         for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
             f4 v[8];
+            // plain loads (0.4 us per step faster than nontemporal ones here)
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                v[u] = *(const f4*)&slabs[(int64_t)(i + u * kRedGroups) * mb.n_slab + p0];  // plain loads: 0.4 us
-                                                                                          // faster than nontemporal
+            for (int u = 0; u < 8; ++u) v[u] = *(const f4*)&slabs[(int64_t)(i + u * kRedGroups) * mb.n_slab + p0];
 #pragma unroll
             for (int u = 0; u < 8; u += 2) {
                 a0 += v[u];
