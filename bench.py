@@ -49,8 +49,9 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train_batch) -> dict:
-    """The naive C oracle (FP32, scalar loops) on the host cores, bounded sample of the workload."""
+def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train_batch, gpu_out=None) -> dict:
+    """The naive C oracle (FP32, scalar loops) on the host cores, bounded sample of the workload. Its first pass over
+    the frame doubles as the checker of the timed GPU inference (gpu_out: the bench's last output buffer)."""
     orc = nrc_loader.load_oracle()
     threads = orc.default_threads()
     n = 4096
@@ -60,12 +61,22 @@ def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train
     # whole passes over the frame while they fit the budget, then a partial pass to reach ~target_s
     want = int(max(n, n * target_s / max(dt, 1e-6)))
     total = 0
+    first = None
     t0 = time.perf_counter()
     while total < want:
         m = min(len(queries), want - total)
-        orc.forward(params, queries[:m], orc.FP32, threads)
+        y = orc.forward(params, queries[:m], orc.FP32, threads)
+        if first is None:
+            first = y
         total += m
     dt = time.perf_counter() - t0
+    parity = None
+    if gpu_out is not None and first is not None:
+        ref = first.astype(np.float64)
+        got = gpu_out[:len(ref)].astype(np.float64)
+        parity = {"rel_l2_vs_oracle_fp32": float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30)),
+                  "queries": int(len(ref)), "tolerance": 1e-3,
+                  "what": "the timed inference's output buffer vs the FP32 oracle forward of the same queries"}
     # the same forward on one thread (bounded sample) and one 16,384-sample train step
     n1 = 8192
     t1 = time.perf_counter()
@@ -83,7 +94,8 @@ def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train
                       f"({os.cpu_count()} logical CPUs visible), {dt:.1f} s",
             "value_1thread": n1 / dt1 / 1e6, "sample_1thread": f"{n1} queries on 1 thread, {dt1:.2f} s",
             "train_step_ms": dt2 * 1e3,
-            "sample_train": f"one {len(tq)}-sample step: FP32 encode+fwd+loss+bwd ({threads} pthreads) + Adam/EMA"}
+            "sample_train": f"one {len(tq)}-sample step: FP32 encode+fwd+loss+bwd ({threads} pthreads) + Adam/EMA",
+            "parity": parity}
 
 
 def frame_bench(nrc, net, dev, iters: int) -> dict:
@@ -207,6 +219,8 @@ def main() -> None:
     wall_max = float(t.item())
     ms_per_step = wall_max / args.steps * 1e3
     value = world * nq * args.steps / wall_max / 1e6
+    # the weights the timed inference used (training below moves them), for the CPU leg's parity check
+    infer_params = net.get_state(nrc.StateSlot.INFER) if rank == 0 and world == 1 and not args.no_cpu else None
 
     # ---- training: frames of 4 x 16384
     for f in range(2):
@@ -258,9 +272,11 @@ def main() -> None:
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        params = net.get_state(nrc.StateSlot.INFER)
+        params = infer_params
+        out_np = out.cpu().numpy()  # the last timed inference step's output, computed with infer_params
         result["cpu_baseline"] = cpu_baseline(q_np, params, args.cpu_seconds,
-                                              nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=seed * 31))
+                                              nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=seed * 31),
+                                              gpu_out=out_np)
     net.destroy()
     if rank == 0:
         print(json.dumps(result), flush=True)
