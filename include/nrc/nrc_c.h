@@ -135,7 +135,7 @@ nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
 nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 
 /* ---- test / tuning entries ---- */
-/* Inference through a specific kernel variant (0..2, see nrc_kernels.hip) for in-process A/B timing;
+/* Inference through a specific kernel variant (0..23, see nrc_kernels.hip) for in-process A/B timing;
  * results are identical in meaning to nrc_infer_stream. */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
                                    hipStream_t stream);
@@ -143,6 +143,12 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* input
  * written to stamps_d); performs no optimizer step. */
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
                                   uint64_t* stamps_d);
+/* Diagnostic: the default inference kernel with s_memtime phase stamps; per wave of its persistent grid, 8 uint64
+ * cycle sums (encode + prefetch, layers 0..4, output layer, epilogue) go to stamps_d, which must hold
+ * 8 * NRC_INFER_STAMP_WAVES_MAX entries; *waves_h receives the number of waves written. */
+#define NRC_INFER_STAMP_WAVES_MAX 8192
+nrc_status nrc_debug_infer_stamps(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n,
+                                  uint64_t* stamps_d, uint64_t* waves_h);
 /* the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* the encoder the MLP kernels actually run (closed-form OneBlob, f16-rounded), same output format */

@@ -719,6 +719,19 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
     });
 }
 
+nrc_status nrc_debug_infer_stamps(nrc_net* net, const float* in, float* out, uint32_t n, uint64_t* stamps_d,
+                                  uint64_t* waves_h) {
+    return guarded([&] {
+        check_live(net);
+        require_frequency(net, "nrc_debug_infer_stamps");
+        if (!in || !out || !stamps_d || !waves_h || n == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
+        int64_t waves = 0;
+        HIP_CHECK(launch_infer_stamped(in, out, n, net->wf_infer, stamps_d, &waves, net->stream));
+        if (waves > NRC_INFER_STAMP_WAVES_MAX) throw ApiError(NRC_ERR_INTERNAL, "stamp buffer too small");
+        *waves_h = (uint64_t)waves;
+    });
+}
+
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint64_t* stamps_d) {
     return guarded([&] {
         check_live(net);

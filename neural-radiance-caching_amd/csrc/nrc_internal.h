@@ -151,6 +151,8 @@ struct GridBuffers {
 };
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
 hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t s);
+hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
+                                int64_t* waves, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s);

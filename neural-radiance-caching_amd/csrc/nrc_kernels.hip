@@ -602,6 +602,15 @@ __device__ __forceinline__ void encode_sh(const QLane& Q, int h, h8 (&x)[5]) {
     }
 }
 
+// s_memtime between scheduling fences (diagnostic builds only)
+__device__ __forceinline__ uint64_t stamp_now() {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+constexpr int kInferPhases = 8;  // encode+prefetch, layers 0..4, output layer, epilogue
+
 template <int ABL = 0>
 __device__ __forceinline__ h8 relu_h8(const f16v& a, int base) {
     h8 r;
@@ -662,7 +671,15 @@ __device__ __forceinline__ void layer_mfma(const h8 (&a)[2][KK], const h8 (&in)[
 // PREFETCH: issue layer l+1's weight-fragment reads before layer l's MFMAs (double-buffered
 // fragment registers) instead of at the head of layer l+1.
 template <int TILES, bool PREFETCH, int ABL = 0, int KK0 = 5>
-__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][KK0], f16v (&o)[TILES]) {
+__device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][KK0], f16v (&o)[TILES],
+                                          uint64_t* ph = nullptr, uint64_t* tprev = nullptr) {
+    auto mark = [&](int k) {  // ABL & 256: add the time since the previous mark to phase k
+        if constexpr ((ABL & 256) != 0) {
+            const uint64_t t = stamp_now();
+            ph[k] += t - *tprev;
+            *tprev = t;
+        }
+    };
     static_assert(KK0 == 5 || !PREFETCH, "the prefetch schedule is written for the 80-wide input layer");
     h8 y[TILES][4], z[TILES][4];
     if constexpr (PREFETCH) {
@@ -691,18 +708,20 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
     } else {
         {
             h8 a0[2][KK0];
-            load_frags<KK0, ABL>(lw_lane, 0, a0);
-            layer_mfma<TILES, KK0, ABL>(a0, x, y);
+            load_frags<KK0, ABL & 7>(lw_lane, 0, a0);
+            layer_mfma<TILES, KK0, ABL & 7>(a0, x, y);
         }
+        mark(1);
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
             h8 a[2][4];
-            load_frags<4, ABL>(lw_lane, l, a);
-            layer_mfma<TILES, 4, ABL>(a, y, z);
+            load_frags<4, ABL & 7>(lw_lane, l, a);
+            layer_mfma<TILES, 4, ABL & 7>(a, y, z);
 #pragma unroll
             for (int t = 0; t < TILES; ++t)
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) y[t][kk] = z[t][kk];
+            mark(1 + l);
         }
         lds_h8* wl = launder(lw_lane);
 #pragma unroll
@@ -713,6 +732,12 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
 #pragma unroll
             for (int t = 0; t < TILES; ++t) o[t] = mfma(a, y[t][kk], o[t]);
         }
+        if constexpr ((ABL & 256) != 0) {
+            // make the output MFMAs complete inside their own phase
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) asm volatile("" : "+v"(o[t]));
+        }
+        mark(6);
     }
 }
 
@@ -729,7 +754,9 @@ struct InferEpilogue {
     float4* rgba;      // [n_acc] frame buffer
     int64_t n_acc;
     float w;           // 1 / (iterationIndex + 1)
+    uint64_t* stamps = nullptr;  // diagnostic build only (ABL & 256): per-wave phase cycle sums
 };
+
 
 // ENC: 0 = Frequency composite (80-wide input), 1 = Hash composite (64-wide; grid = f16x2 table),
 // 2 = FrequencySH extension (80-wide)
@@ -765,7 +792,17 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
     }
+    uint64_t ph[kInferPhases] = {};
+    uint64_t tprev = 0;
+    if constexpr ((ABL & 256) != 0) tprev = stamp_now();
+    bool first_iter = true;
     for (; g < ngroups; g += wstride) {
+        if constexpr ((ABL & 256) != 0) {  // the previous iteration's epilogue (stores, loop overhead)
+            const uint64_t tn = stamp_now();
+            if (!first_iter) ph[7] += tn - tprev;
+            tprev = tn;
+            first_iter = false;
+        }
         h8 x[TILES][KK0];
 #pragma unroll
         for (int t = 0; t < TILES; ++t) {
@@ -830,7 +867,16 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             }
         }
         f16v o[TILES];
-        mlp_tiles<TILES, PREFETCH, ABL & 7, KK0>((lds_h8*)(lw + lane), x, o);
+        if constexpr ((ABL & 256) != 0) {
+#pragma unroll
+            for (int t = 0; t < TILES; ++t)
+#pragma unroll
+                for (int kk = 0; kk < KK0; ++kk) asm volatile("" : "+v"(x[t][kk]));
+            const uint64_t tn = stamp_now();
+            ph[0] += tn - tprev;
+            tprev = tn;
+        }
+        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
         if constexpr ((ABL & 8) && EPI < 0) {
             const int64_t s0 = g * TILES * 32;
             if (out16 && s0 + TILES * 32 <= n) {
@@ -920,6 +966,14 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             }
         }
     }
+    if constexpr ((ABL & 256) != 0) {
+        const uint64_t tn = stamp_now();
+        ph[7] += tn - tprev;
+        const int64_t wid = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < kInferPhases; ++k) epi.stamps[wid * kInferPhases + k] = ph[k];
+    }
 }
 
 template <int TILES, int WAVES_PER_EU, int THREADS, bool PREFETCH, int ABL = 0>
@@ -927,6 +981,15 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
                                                                          float* __restrict__ out, int64_t n,
                                                                          const h8* __restrict__ wf) {
     infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, InferEpilogue{});
+}
+
+// Diagnostic build of the default inference kernel (variant 23) with per-wave phase stamps (ABL & 256).
+__global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                             int64_t n, const h8* __restrict__ wf,
+                                                             uint64_t* __restrict__ stamps) {
+    InferEpilogue e{};
+    e.stamps = stamps;
+    infer_v2_body<1, 512, false, kDefaultAbl | 256, -1>(q, out, n, wf, e);
 }
 
 // the default inference configuration (variant 22) with the accumulation epilogue
@@ -1953,6 +2016,19 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 13: return launch_persistent_infer(infer_kernel_v3<3, 46, 1>, 256, bpc[13], (ntiles + 2) / 3, queries, out, n, wf, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+// Diagnostic: the default kernel with phase stamps; stamps gets kInferPhases sums per wave of the persistent grid.
+hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
+                                int64_t* waves, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t ntiles = (n + 31) / 32;
+    const int bpc = blocks_per_cu(infer_stamp_kernel, 512);
+    const int64_t blocks = std::min<int64_t>((int64_t)num_cus() * bpc, (ntiles + 7) / 8);
+    *waves = blocks * 8;
+    hipLaunchKernelGGL(infer_stamp_kernel, dim3((unsigned)blocks), dim3(512), 0, s, queries, out, n,
+                       (const h8*)wf, stamps);
+    return hipGetLastError();
 }
 
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
