@@ -109,6 +109,15 @@ typedef struct nrc_float3 { float x, y, z; } nrc_float3;
 #define NRC_HASH_PRIME1 2654435761u /* tcnn coherent prime hash: x * 1 ^ y * 2654435761 ^ z * 805459861 */
 #define NRC_HASH_PRIME2 805459861u
 
+/* ---- width-128 network (BASELINE.json configs[4]; beyond the reference's n_neurons = 64) ----
+ * The same FullyFusedMLP with 128 neurons: W0[128][80], W1..W4[128][128], W5[16][128], canonical blob order as
+ * above. Frequency and FrequencySH encodings (80-wide input). Inference in f16 or FP8 (nrc_config.infer_precision). */
+#define NRC_WIDE_WIDTH         128
+#define NRC_WIDE_W0_OFFSET     0
+#define NRC_WIDE_W1_OFFSET     (NRC_WIDE_W0_OFFSET + NRC_WIDE_WIDTH * NRC_ENC_WIDTH)       /* 10240 */
+#define NRC_WIDE_W5_OFFSET     (NRC_WIDE_W1_OFFSET + 4 * NRC_WIDE_WIDTH * NRC_WIDE_WIDTH)  /* 75776 */
+#define NRC_WIDE_NUM_PARAMS    (NRC_WIDE_W5_OFFSET + NRC_OUT_PADDED * NRC_WIDE_WIDTH)      /* 77824 */
+
 /* tcnn defaults used by the Frequency config (survey Appendix A.7-A.8). */
 #define NRC_LOSS_SCALE     128.0f
 #define NRC_ADAM_BETA1     0.9f

@@ -46,7 +46,17 @@ typedef struct nrc_config {
     float ema_decay;     /* EMA optimizer wrapper decay (0.99) */
     float loss_scale;    /* f16 loss scale (128) */
     uint64_t seed;       /* weight initialisation seed */
+    /* Extensions (BASELINE.json configs[4]; not in the reference, whose FullyFusedMLP has 64 neurons): */
+    uint32_t width;           /* MLP neurons: 64 (reference) or 128 (NRC_WIDE_*; Frequency / FrequencySH only) */
+    uint32_t infer_precision; /* nrc_precision of infer(): F16 (reference numerics) or FP8 (width 128 only) */
 } nrc_config;
+
+/* Arithmetic of infer() (nrc_config.infer_precision). FP8: e4m3 weights (one power-of-two scale per output row)
+ * and e4m3 activations on the MX-scaled fp8 MFMA for layers 1..5, layer 0 in f16. */
+typedef enum nrc_precision {
+    NRC_PRECISION_F16 = 0,
+    NRC_PRECISION_FP8 = 1
+} nrc_precision;
 
 /* HyperParams (NRCNetwork.h:10-13) */
 typedef struct nrc_hyper_params {
@@ -149,6 +159,12 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const flo
 #define NRC_INFER_STAMP_WAVES_MAX 8192
 nrc_status nrc_debug_infer_stamps(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n,
                                   uint64_t* stamps_d, uint64_t* waves_h);
+/* Width-128 networks: inference with either precision's weight image (both are packed from the inference
+ * weights), regardless of the configured infer_precision (A/B timing and parity tests). */
+nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* inputs_d, float* outputs_d, uint32_t n,
+                                     hipStream_t stream);
+/* e4m3 conversion exactly as the FP8 kernels do it: clamp to [relu ? 0 : -448, 448], round to nearest even. */
+nrc_status nrc_debug_fp8_convert(const float* x_d, uint8_t* y_d, uint32_t n, int relu, hipStream_t stream);
 /* the Composite encoding alone, f32 [n][80] canonical tcnn feature order ---- */
 nrc_status nrc_encode(const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
 /* the encoder the MLP kernels actually run (closed-form OneBlob, f16-rounded), same output format */

@@ -18,6 +18,8 @@ NUM_PARAMS = 22528
 GRAD_FLOATS = NUM_PARAMS + 4
 HASH_NUM_PARAMS = 1012736
 HASH_GRAD_FLOATS = HASH_NUM_PARAMS + 4
+WIDE_NUM_PARAMS = 77824  # width-128 network (BASELINE configs[4])
+PRECISION_F16, PRECISION_FP8 = 0, 1
 BATCH_SIZE = 16384
 INPUT_DIMS = 15
 OUTPUT_DIMS = 3
@@ -36,7 +38,7 @@ EXPORTS = [
     "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
-    "nrc_debug_encode_fast_variant",
+    "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame",
@@ -49,7 +51,8 @@ EXPORTS = [
 class NrcConfig(ctypes.Structure):
     _fields_ = [("learning_rate", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("epsilon", ctypes.c_float), ("l2_reg", ctypes.c_float), ("ema_decay", ctypes.c_float),
-                ("loss_scale", ctypes.c_float), ("seed", ctypes.c_uint64)]
+                ("loss_scale", ctypes.c_float), ("seed", ctypes.c_uint64), ("width", ctypes.c_uint32),
+                ("infer_precision", ctypes.c_uint32)]
 
 
 class NrcHyperParams(ctypes.Structure):
@@ -114,6 +117,8 @@ def lib() -> ctypes.CDLL:
         "nrc_debug_infer_stamps": (st, [vp, fp, fp, u32, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "nrc_debug_encode_fast": (st, [fp, fp, u32, vp]),
         "nrc_debug_encode_fast_variant": (st, [ctypes.c_int, fp, fp, u32, vp]),
+        "nrc_debug_infer_precision": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
+        "nrc_debug_fp8_convert": (st, [fp, fp, u32, ctypes.c_int, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

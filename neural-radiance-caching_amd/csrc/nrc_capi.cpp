@@ -69,6 +69,19 @@ void init_params_hash(std::vector<float>& p, uint64_t seed) {
     for (int i = 0; i < NRC_HASH_GRID_PARAMS; ++i) p[NRC_HASH_GRID_OFFSET + i] = (g.next_float() * 2.0f - 1.0f) * 1e-4f;
 }
 
+// Width-128 network (BASELINE configs[4]): the same xavier-uniform stream over the wide shapes.
+void init_params_wide(std::vector<float>& p, uint64_t seed) {
+    const int in[NRC_NUM_LAYERS] = {NRC_ENC_WIDTH, 128, 128, 128, 128, 128};
+    const int out[NRC_NUM_LAYERS] = {128, 128, 128, 128, 128, NRC_OUT_PADDED};
+    Pcg32 rng(seed, 0xda3e39cb94b95bdbULL);
+    int off = 0;
+    for (int l = 0; l < NRC_NUM_LAYERS; ++l) {
+        const float scale = std::sqrt(6.0f / (float)(in[l] + out[l]));
+        for (int i = 0; i < in[l] * out[l]; ++i) p[off + i] = (rng.next_float() * 2.0f - 1.0f) * scale;
+        off += in[l] * out[l];
+    }
+}
+
 // Parameter of every position of the fragment-major weight-gradient slab (nrc_internal.h slab_block_base):
 // position (block, j, lane, e) holds accumulator register 4j + e of that lane, i.e. dW[row][col] with
 // row = 32 mb + (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5), col = 32 nb + (lane & 31) (layer 0: K slot -> feature).
@@ -190,7 +203,13 @@ std::string config_json(int encoding, const nrc_config& c) {
                       "\"Adam\"},\"otype\":\"EMA\"}}",
                       c.ema_decay, c.epsilon, c.l2_reg, c.learning_rate);
     }
-    return buf;
+    std::string r = buf;
+    if (c.width != 64) {
+        const std::string k = "\"n_neurons\":64";
+        const size_t at = r.find(k);
+        if (at != std::string::npos) r.replace(at, k.size(), "\"n_neurons\":" + std::to_string(c.width));
+    }
+    return r;
 }
 
 }  // namespace
@@ -220,7 +239,13 @@ struct nrc_net {
     uint32_t* grid_steps = nullptr;
     _Float16 *table_train = nullptr, *table_infer = nullptr;
 
+    // width-128 network (BASELINE configs[4]): inference images only
+    uint8_t *wide_img16 = nullptr, *wide_img8 = nullptr;
+    uint32_t* wide_scales = nullptr;
+    int32_t* wide_exps = nullptr;
+
     bool hash() const { return encoding == NRC_ENCODING_HASH; }
+    bool wide() const { return cfg.width == NRC_WIDE_WIDTH; }
     size_t n_total() const { return (size_t)n_mlp + (size_t)n_grid; }
     size_t grad_floats() const { return n_total() + 4; }
 
@@ -233,6 +258,10 @@ struct nrc_net {
         f(fwd_pos); f(bwd_pos); f(slab_param);
         f(slabs); f(loss_partials); f(loss_dev);
         f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
+        f(wide_img16); f(wide_img8); f(wide_scales); f(wide_exps);
+        wide_img16 = wide_img8 = nullptr;
+        wide_scales = nullptr;
+        wide_exps = nullptr;
         grid_grad = nullptr;
         grid_steps = nullptr;
         table_train = table_infer = nullptr;
@@ -298,12 +327,26 @@ void upload_all(nrc_net* net, const std::vector<float>& params, const std::vecto
 }
 
 void repack(nrc_net* net, hipStream_t s) {
+    if (net->wide()) {
+        HIP_CHECK(launch_wide_pack(net->infer, net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0,
+                                   reinterpret_cast<_Float16*>(net->wide_img16), net->wide_img8, net->wide_scales,
+                                   net->wide_exps, s));
+        return;
+    }
     HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
     if (net->hash()) HIP_CHECK(launch_grid_adam(kPackOnly, net->grid_buffers(), net->optim(1), s));
 }
 
+void require_trainable(const nrc_net* net) {
+    if (net->wide())
+        throw ApiError(NRC_ERR_UNSUPPORTED,
+                       "the width-128 network (BASELINE configs[4]) is inference-only in this build: load its weights "
+                       "with nrc_set_state");
+}
+
 void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h, float* loss_d = nullptr) {
     check_live(net);
+    require_trainable(net);
     if (b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "batch size must be >= 1");
     if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
     const int blocks = train_blocks(b);
@@ -325,7 +368,17 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     }
 }
 
+int wide_enc(const nrc_net* net) { return net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0; }
+
+hipError_t infer_wide(nrc_net* net, int prec, const float* in, float* out, uint32_t n, const float* thr, float* rgba,
+                      uint32_t n_acc, int mode, float w, hipStream_t s) {
+    return launch_infer_wide(prec, wide_enc(net), in, out, n, prec ? net->wide_img8 : net->wide_img16, net->wide_scales,
+                             thr, rgba, n_acc, mode, w, s);
+}
+
 hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
+    if (net->wide())
+        return infer_wide(net, (int)net->cfg.infer_precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     if (net->hash())
         return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
@@ -371,6 +424,8 @@ nrc_config nrc_default_config(int encoding) {
     c.ema_decay = NRC_EMA_DECAY;
     c.loss_scale = NRC_LOSS_SCALE;
     c.seed = 1337;
+    c.width = NRC_WIDTH;
+    c.infer_precision = NRC_PRECISION_F16;
     return c;
 }
 
@@ -397,13 +452,53 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
         if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH && encoding != NRC_ENCODING_FREQUENCY_SH)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
+        const nrc_config c = cfg ? *cfg : nrc_default_config(encoding);
+        if (c.width != NRC_WIDTH && c.width != NRC_WIDE_WIDTH)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "width must be 64 or 128");
+        if (c.infer_precision != NRC_PRECISION_F16 && c.infer_precision != NRC_PRECISION_FP8)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown infer_precision");
+        if (c.infer_precision == NRC_PRECISION_FP8 && c.width != NRC_WIDE_WIDTH)
+            throw ApiError(NRC_ERR_UNSUPPORTED, "FP8 inference is implemented for the width-128 network only");
+        if (c.width == NRC_WIDE_WIDTH && encoding == NRC_ENCODING_HASH)
+            throw ApiError(NRC_ERR_UNSUPPORTED, "the width-128 network supports the Frequency / FrequencySH encodings");
         net->release();
         net->stream = stream;
         net->encoding = encoding;
-        net->cfg = cfg ? *cfg : nrc_default_config(encoding);
+        net->cfg = c;
         net->destroyed = false;
         net->step = 0;
         HIP_CHECK(hipGetDevice(&net->device));
+        if (net->wide()) {
+            net->n_mlp = NRC_WIDE_NUM_PARAMS;
+            net->n_grid = 0;
+            const size_t pb = sizeof(float) * net->n_total();
+            HIP_CHECK(hipMalloc(&net->params, pb));
+            HIP_CHECK(hipMalloc(&net->m, pb));
+            HIP_CHECK(hipMalloc(&net->v, pb));
+            HIP_CHECK(hipMalloc(&net->ema, pb));
+            HIP_CHECK(hipMalloc(&net->infer, pb));
+            HIP_CHECK(hipMemset(net->m, 0, pb));
+            HIP_CHECK(hipMemset(net->v, 0, pb));
+            HIP_CHECK(hipMemset(net->ema, 0, pb));
+            HIP_CHECK(hipMalloc(&net->wide_img16, kWideF16Bytes));
+            HIP_CHECK(hipMalloc(&net->wide_img8, kWide8Bytes));
+            HIP_CHECK(hipMalloc(&net->wide_scales, sizeof(uint32_t) * 5 * 32));
+            HIP_CHECK(hipMalloc(&net->wide_exps, sizeof(int32_t) * 5 * 128));
+            HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
+            HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
+            HIP_CHECK(hipMemset(net->loss_dev, 0, sizeof(float) * 4));
+            std::vector<float> p(net->n_total());
+            init_params_wide(p, net->cfg.seed);
+            upload_all(net, p, p);
+            net->initialized = true;
+            repack(net, nullptr);
+            HIP_CHECK(hipDeviceSynchronize());
+            if (verbose)
+                std::printf("\n----------------------- NETWORK CONFIG -----------------------\n%s\n"
+                            "--------------------------------------------------------------\n\n",
+                            config_json(net->encoding, net->cfg).c_str());
+            return;
+        }
         net->n_mlp = net->hash() ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS;
         net->n_grid = net->hash() ? NRC_HASH_GRID_PARAMS : 0;
         const size_t pb = sizeof(float) * net->n_total();
@@ -506,7 +601,10 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
         if (num_pixels > 0 && (!thr || !rgba || (reinterpret_cast<uintptr_t>(rgba) & 15)))
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "throughput / 16-byte aligned float4 frame buffer required");
         const float w = 1.0f / (float)(iteration_index + 1u);  // nrc_helpers.cu:98
-        if (net->hash())
+        if (net->wide())
+            HIP_CHECK(infer_wide(net, (int)net->cfg.infer_precision, in, out, n, reinterpret_cast<const float*>(thr),
+                                 rgba, num_pixels, mode, w, net->stream));
+        else if (net->hash())
             HIP_CHECK(launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, reinterpret_cast<const float*>(thr),
                                         rgba, num_pixels, mode, w, net->stream));
         else if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
@@ -596,6 +694,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
                           float* grad_d) {
     return guarded([&] {
         check_live(net);
+        require_trainable(net);
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
         if (b == 0) {
@@ -624,6 +723,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
     return guarded([&] {
         check_live(net);
+        require_trainable(net);
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         net->step += 1;
         HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
@@ -712,6 +812,7 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
     return guarded([&] {
         check_live(net);
         require_frequency(net, "nrc_debug_infer_variant");
+        if (net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "inference variants are 64-wide kernels");
         if (variant < 0 || variant >= kNumInferVariants) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown variant");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
@@ -724,6 +825,7 @@ nrc_status nrc_debug_infer_stamps(nrc_net* net, const float* in, float* out, uin
     return guarded([&] {
         check_live(net);
         require_frequency(net, "nrc_debug_infer_stamps");
+        if (net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "inference stamps are a 64-wide diagnostic");
         if (!in || !out || !stamps_d || !waves_h || n == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
         int64_t waves = 0;
         HIP_CHECK(launch_infer_stamped(in, out, n, net->wf_infer, stamps_d, &waves, net->stream));
@@ -736,11 +838,33 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tg
     return guarded([&] {
         check_live(net);
         require_frequency(net, "nrc_debug_train_stamps");
+        require_trainable(net);
         if (!in || !tgt || !stamps_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
         HIP_CHECK(launch_train_stamped(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                        net->slabs, net->loss_partials, stamps_d, net->stream));
+    });
+}
+
+nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* in, float* out, uint32_t n,
+                                     hipStream_t stream) {
+    return guarded([&] {
+        check_live(net);
+        if (!net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "precision selection is for the width-128 network");
+        if (precision != NRC_PRECISION_F16 && precision != NRC_PRECISION_FP8)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown precision");
+        if (n == 0) return;
+        if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+        HIP_CHECK(infer_wide(net, precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, stream));
+    });
+}
+
+nrc_status nrc_debug_fp8_convert(const float* x, uint8_t* y, uint32_t n, int relu, hipStream_t stream) {
+    return guarded([&] {
+        if (n == 0) return;
+        if (!x || !y) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
+        HIP_CHECK(launch_fp8_convert(x, y, n, relu, stream));
     });
 }
 

@@ -84,6 +84,35 @@ __host__ __device__ constexpr int enc_k0_feature(int enc, int K) {
     return enc == 1 ? hash_k0_feature(K) : enc == 2 ? sh_k0_feature(K) : k0_feature(K);
 }
 
+// ---- width-128 network (BASELINE configs[4]). f16 image: 156 fragments of 1 KiB in the layout of
+// the 64-wide forward image (L0 4 M-blocks x 5 k-steps, L1..L4 4 x 8, L5 1 x 8). FP8 image: the 20 f16 layer-0
+// fragments, then 34 fp8 fragments of layers 1..5 (L1..L4 4 M-blocks x 2 k-steps of 64, L5 1 x 2), each 2 KiB =
+// two 1-KiB planes (bytes 0-15 / 16-31 of every lane's 32-byte MX-MFMA operand, lane-linear 16 B so that each plane
+// is one conflict-free ds_read_b128), plus per-row E8M0 scales [5 layers][32 lanes] (byte mb = row 32 mb + lane).
+constexpr int kWideF16Frags = 4 * 5 + 4 * 4 * 8 + 8;  // 156
+constexpr int kWide8Frags = 4 * 4 * 2 + 2;            // 34
+constexpr int kWideF16Bytes = kWideF16Frags * 1024;                   // 159744
+constexpr int kWide8Bytes = 20 * 1024 + kWide8Frags * 2048;           // 90112
+__host__ __device__ constexpr int wide_frag(int layer, int mb, int kk) {
+    return layer == 0 ? mb * 5 + kk : layer <= 4 ? 20 + (layer - 1) * 32 + mb * 8 + kk : 148 + kk;
+}
+__host__ __device__ constexpr int wide8_frag(int layer, int mb, int s) {
+    return layer <= 4 ? (layer - 1) * 8 + mb * 2 + s : 32 + s;
+}
+// Byte j (0..31) of lane half h of an fp8 B operand for k-step s, built from the accumulators of M-blocks 2s and
+// 2s + 1 (register j & 15 of block 2s + (j >> 4)): the previous layer's output row it carries.
+__host__ __device__ constexpr int f8_row(int s, int h, int j) {
+    return 64 * s + 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
+}
+hipError_t launch_wide_pack(const float* w, int enc, _Float16* img16, uint8_t* img8, uint32_t* scales, int32_t* exps,
+                            hipStream_t s);
+// prec 0 = f16, 1 = fp8; enc 0 = Frequency, 2 = FrequencySH; mode -1 plain, 0 / 2 fused accumulation
+hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out, int64_t n, const void* img,
+                             const uint32_t* scales, const float* thr, float* rgba, int64_t n_acc, int mode, float w,
+                             hipStream_t s);
+// diagnostic: e4m3 conversion exactly as the FP8 kernels do it (clamp to [lo, 448], v_cvt_pk_fp8_f32)
+hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s);
+
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,

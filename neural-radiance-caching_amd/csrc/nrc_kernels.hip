@@ -1044,6 +1044,301 @@ __global__ void encode_hash_kernel(const float* __restrict__ q, const uint32_t* 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Width-128 MLP inference (BASELINE.json configs[4] / SURVEY §8 C5; oracle/nrc_wide_oracle.c).
+// Same structure as the 64-wide kernel: one wave = 32 queries on the MFMA column axis, the encoder's f16 output as
+// layer 0's B operand, every layer's accumulators converted in registers into the next layer's B operand.
+//   PREC 0 (f16): 4 M-blocks x 8 k-steps of v_mfma_f32_32x32x16_f16 per hidden layer; 156 KiB of fragments in LDS.
+//   PREC 1 (FP8): layer 0 f16; layers 1..5 on v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 x e4m3, 2x the f16 rate), the
+//   weights e4m3 with one E8M0 scale per output row (the MX scale-A operand: byte mb of the lane's scale word via
+//   op_sel), activations clamped to [0, 448] and converted with v_cvt_pk_fp8_f32 (RNE; med3 does ReLU + saturation
+//   in one op); 88 KiB of fragments in LDS.
+// ------------------------------------------------------------------------------------------------
+typedef int i8v __attribute__((ext_vector_type(8)));  // 32 e4m3 bytes: one operand of the 32x32x64 MX MFMA
+
+template <int OPSEL>
+__device__ __forceinline__ f16v mfma_fp8(const i8v& a, const i8v& b, const f16v& c, uint32_t scale_a) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, OPSEL, (int)scale_a, 0, 127);
+}
+__device__ __forceinline__ f16v mfma_fp8_mb(int mb, const i8v& a, const i8v& b, const f16v& c, uint32_t scale_a) {
+    switch (mb) {  // mb is a constant after unrolling: the switch folds
+        case 0: return mfma_fp8<0>(a, b, c, scale_a);
+        case 1: return mfma_fp8<1>(a, b, c, scale_a);
+        case 2: return mfma_fp8<2>(a, b, c, scale_a);
+        default: return mfma_fp8<3>(a, b, c, scale_a);
+    }
+}
+
+// e4m3 bytes of ReLU(accumulator registers 4q .. 4q+3), saturated at 448
+__device__ __forceinline__ uint32_t relu_fp8x4(const f16v& c, int q) {
+    const float a0 = __builtin_amdgcn_fmed3f(c[4 * q + 0], 0.0f, 448.0f);
+    const float a1 = __builtin_amdgcn_fmed3f(c[4 * q + 1], 0.0f, 448.0f);
+    const float a2 = __builtin_amdgcn_fmed3f(c[4 * q + 2], 0.0f, 448.0f);
+    const float a3 = __builtin_amdgcn_fmed3f(c[4 * q + 3], 0.0f, 448.0f);
+    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    return __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, lo, true);
+}
+
+// next layer's fp8 B operands from the 4 accumulator blocks: k-step s byte j = row f8_row(s, h, j)
+__device__ __forceinline__ void pack_fp8(const f16v (&c)[4], i8v (&y)[2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int d = 0; d < 8; ++d) y[s][d] = (int)relu_fp8x4(c[2 * s + (d >> 2)], d & 3);
+}
+
+// wait for LDS reads at this point only (the image copy) — a full __syncthreads() would also wait for the
+// prefetched query loads
+template <int THREADS, int COUNT>
+__device__ __forceinline__ void copy_to_lds_chunked(h8* __restrict__ dst, const h8* __restrict__ src) {
+    constexpr int PER = (COUNT + THREADS - 1) / THREADS;
+    constexpr int CH = 5;
+#pragma unroll
+    for (int k0 = 0; k0 < PER; k0 += CH) {
+        h8 v[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int i = threadIdx.x + (k0 + k) * THREADS;
+            if (k0 + k < PER && i < COUNT) v[k] = src[i];
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int i = threadIdx.x + (k0 + k) * THREADS;
+            if (k0 + k < PER && i < COUNT) dst[i] = v[k];
+        }
+    }
+}
+
+template <int PREC>
+__device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], const uint32_t (&sc)[5]) {
+    f16v c[4];
+    {
+        lds_h8* wl = launder(lw_lane);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(0, mb, kk) * 64], x[kk], c[mb]);
+    }
+    if constexpr (PREC == 0) {
+        h8 y[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) y[kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
+#pragma unroll
+        for (int l = 1; l < 5; ++l) {
+            lds_h8* wl = launder(lw_lane);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(l, mb, kk) * 64], y[kk], c[mb]);
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) y[kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
+        }
+        lds_h8* wl = launder(lw_lane);
+        f16v o = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) o = mfma(wl[wide_frag(5, 0, kk) * 64], y[kk], o);
+        return o;
+    } else {
+        i8v y[2];
+        pack_fp8(c, y);
+        // fp8 fragment f: planes at h8 offsets (20 + 2 f) * 64 and (21 + 2 f) * 64 from the lane's base
+        auto frag8 = [&](lds_h8* wl, int f) {
+            const h8 lo = wl[(20 + 2 * f) * 64], hi = wl[(21 + 2 * f) * 64];
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            const u4 a = __builtin_bit_cast(u4, lo), b = __builtin_bit_cast(u4, hi);
+            const i8v r = {(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+            return r;
+        };
+#pragma unroll
+        for (int l = 1; l < 5; ++l) {
+            lds_h8* wl = launder(lw_lane);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+                    c[mb] = mfma_fp8_mb(mb, frag8(wl, wide8_frag(l, mb, s)), y[s], c[mb], sc[l - 1]);
+            pack_fp8(c, y);
+        }
+        lds_h8* wl = launder(lw_lane);
+        f16v o = zero16();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) o = mfma_fp8<0>(frag8(wl, wide8_frag(5, 0, s)), y[s], o, sc[4]);
+        return o;
+    }
+}
+
+// ENC 0 = Frequency, 2 = FrequencySH (both 80-wide); EPI -1 plain, 0 / 2 fused accumulate_render_radiance.
+// Persistent waves, 2 per SIMD (one 512-thread block per CU: the f16 image takes 156 KiB of LDS).
+template <int ENC, int PREC, int EPI>
+__global__ __launch_bounds__(512, 2) void infer_wide_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                            int64_t n, const h8* __restrict__ img, InferEpilogue epi,
+                                                            const uint32_t* __restrict__ wscale) {
+    constexpr int THREADS = 512;
+    constexpr int NH8 = (PREC == 0 ? kWideF16Bytes : kWide8Bytes) / 16;
+    __shared__ __attribute__((aligned(16))) h8 lw[NH8];
+    fp32_flush_output_denorms();  // the omod doubling-chain encoder
+    copy_to_lds_chunked<THREADS, NH8>(lw, img);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    uint32_t sc[5] = {};
+    if constexpr (PREC == 1) {
+#pragma unroll
+        for (int l = 0; l < 5; ++l) sc[l] = wscale[l * 32 + r];
+    }
+    const int64_t ngroups = (n + 31) >> 5;
+    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
+    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (g >= ngroups) return;
+    const int64_t last = n - 1;
+    QLane Q = load_q_enc<ENC>(q, min(g * 32 + r, last), h);
+    if constexpr (EPI >= 0) __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
+    for (; g < ngroups; g += wstride) {
+        h8 x[5];
+        if constexpr (ENC == 2) encode_sh<true>(Q, h, x);
+        else encode_fast<true>(Q, h, x);
+        Q = load_q_enc<ENC>(q, min((g + wstride) * 32 + r, last), h);  // clamped, branch-free prefetch
+        const int64_t s0 = g * 32, sq = s0 + r;
+        float tr[3] = {};
+        float4 acc = {};
+        if constexpr (EPI >= 0) {
+            const int rows = tile_rows(epi.n_acc, s0);
+            const u3 tv = __builtin_amdgcn_raw_buffer_load_b96(buffer_rsrc(epi.thr + s0 * 3, rows * 12),
+                                                               h ? kBufferOff : r * 12, 0, 0);
+            typedef float f3 __attribute__((ext_vector_type(3)));
+            const f3 tf = __builtin_bit_cast(f3, tv);  // whole-vector bit_cast (see infer_v2_body)
+            tr[0] = tf.x;
+            tr[1] = tf.y;
+            tr[2] = tf.z;
+            if constexpr (EPI == 0) {
+                const u4 av = __builtin_amdgcn_raw_buffer_load_b128(buffer_rsrc(epi.rgba + s0, rows * 16),
+                                                                    h ? kBufferOff : r * 16, 0, 0);
+                acc = __builtin_bit_cast(float4, av);
+            }
+        }
+        const f16v o = wide_mlp<PREC>((lds_h8*)(lw + lane), x, sc);
+        const float L0 = (float)(_Float16)fmaxf(o[0], 0.0f);
+        const float L1 = (float)(_Float16)fmaxf(o[1], 0.0f);
+        const float L2 = (float)(_Float16)fmaxf(o[2], 0.0f);
+        bool to_out = h == 0;
+        if constexpr (EPI >= 0) {
+            float4 v;
+            if constexpr (EPI == 0) {  // Full: dst += (T * L) * w
+                v = acc;
+                v.x = __builtin_fmaf(tr[0] * L0, epi.w, v.x);
+                v.y = __builtin_fmaf(tr[1] * L1, epi.w, v.y);
+                v.z = __builtin_fmaf(tr[2] * L2, epi.w, v.z);
+            } else {  // CacheOnly
+                v.x = L0 * tr[0];
+                v.y = L1 * tr[1];
+                v.z = L2 * tr[2];
+            }
+            v.w = 1.0f;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v),
+                                                   buffer_rsrc(epi.rgba + s0, tile_rows(epi.n_acc, s0) * 16),
+                                                   h ? kBufferOff : r * 16, 0, 0);
+            to_out = to_out && sq >= epi.n_acc;
+        }
+        const u3 ov = {__builtin_bit_cast(uint32_t, L0), __builtin_bit_cast(uint32_t, L1),
+                       __builtin_bit_cast(uint32_t, L2)};
+        __builtin_amdgcn_raw_buffer_store_b96(ov, buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12),
+                                              to_out ? r * 12 : kBufferOff, 0, 0);
+    }
+}
+
+// Per-row E8M0 exponents of W1..W5 (oracle orc_fp8_row_exponent): one thread per (layer, row).
+__global__ void wide_row_exp_kernel(const float* __restrict__ w, int32_t* __restrict__ exps,
+                                    uint32_t* __restrict__ scales) {
+    const int t = threadIdx.x;  // one block of 640 threads
+    const int layer = 1 + t / 128, row = t % 128;
+    int e = 0;
+    if (layer < 5 || row < NRC_OUT_PADDED) {
+        const float* wr = w + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;  // W5 rows follow W4's
+        float amax = 0.0f;
+        for (int k = 0; k < 128; ++k) amax = fmaxf(amax, fabsf(wr[k]));
+        if (amax > 0.0f) {
+            int E = 0;
+            const float M = frexpf(amax, &E);
+            e = M <= 0.875f ? E - 9 : E - 8;
+            e = max(-127, min(127, e));
+        }
+    }
+    __shared__ int se[5 * 128];
+    exps[t] = e;
+    se[t] = e;
+    __syncthreads();
+    // scale words: lane r of layer l holds bytes e(l, 32 mb + r) + 127, mb = 0..3
+    if (t < 5 * 32) {
+        const int l = t / 32, rr = t % 32;
+        uint32_t word = 0;
+        for (int mb = 0; mb < 4; ++mb) word |= (uint32_t)(se[l * 128 + 32 * mb + rr] + 127) << (8 * mb);
+        scales[t] = word;
+    }
+}
+
+// f16 image (img16, 156 fragments) and FP8 image (img8: 20 f16 layer-0 fragments + 34 fp8 fragments) from the f32
+// inference weights; one thread per 16-byte unit of either image.
+__global__ void wide_pack_kernel(const float* __restrict__ w, int enc, const int32_t* __restrict__ exps,
+                                 _Float16* __restrict__ img16, uint8_t* __restrict__ img8) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int U16 = kWideF16Bytes / 16, U8 = kWide8Frags * 128;
+    if (u < U16) {
+        const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
+        int layer, mb, kk;
+        if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
+        else if (f < 148) { layer = 1 + (f - 20) / 32; mb = ((f - 20) % 32) / 8; kk = (f - 20) % 8; }
+        else { layer = 5; mb = 0; kk = f - 148; }
+        const int row = 32 * mb + r;
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x = 0.0f;
+            if (layer == 0) x = w[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
+            else if (layer < 5 || row < NRC_OUT_PADDED)
+                x = w[NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128 + acc_row(kk, h, j)];
+            v[j] = (_Float16)x;
+        }
+        reinterpret_cast<h8*>(img16)[u] = v;
+        if (f < 20) reinterpret_cast<h8*>(img8)[u] = v;
+    } else if (u < U16 + U8) {
+        const int v8 = u - U16, f = v8 / 128, plane = (v8 / 64) % 2, lane = v8 % 64, r = lane & 31, h = lane >> 5;
+        const int layer = f < 32 ? 1 + f / 8 : 5, mb = f < 32 ? (f % 8) / 2 : 0, s = f < 32 ? f % 2 : f - 32;
+        const int row = 32 * mb + r;
+        const bool live = layer < 5 || row < NRC_OUT_PADDED;
+        const int e = live ? exps[(layer - 1) * 128 + row] : 0;
+        const float* wr = w + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;
+        uint32_t wd[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            float a[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = 16 * plane + 4 * d + i;
+                a[i] = live ? __builtin_amdgcn_fmed3f(ldexpf(wr[f8_row(s, h, j)], -e), -448.0f, 448.0f) : 0.0f;
+            }
+            const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+            wd[d] = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], lo, true);
+        }
+        reinterpret_cast<u4*>(img8 + 20 * 1024)[v8] = u4{wd[0], wd[1], wd[2], wd[3]};
+    }
+}
+
+// e4m3 conversion as the FP8 kernels do it (diagnostic entry for the exhaustive conversion test)
+__global__ void fp8_convert_kernel(const float* __restrict__ x, uint8_t* __restrict__ y, int64_t n, int relu) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = __builtin_amdgcn_fmed3f(x[i], relu ? 0.0f : -448.0f, 448.0f);
+    y[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.0f, 0, false) & 0xffu);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Inference v3: weight fragments resident in registers (loaded once per wave from LDS), so the MFMA
 // stream never waits on LDS. RESIDENT = 46: every layer in registers (1 wave per SIMD, TILES
 // independent tiles interleaved for ILP); RESIDENT = 32: hidden layers 1..4 in registers, input and
@@ -2062,6 +2357,48 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
         case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_wide_pack(const float* w, int enc, _Float16* img16, uint8_t* img8, uint32_t* scales, int32_t* exps,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(wide_row_exp_kernel, dim3(1), dim3(5 * 128), 0, s, w, exps, scales);
+    constexpr int units = kWideF16Bytes / 16 + kWide8Frags * 128;
+    hipLaunchKernelGGL(wide_pack_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w, enc, exps, img16, img8);
+    return hipGetLastError();
+}
+
+hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out, int64_t n, const void* img,
+                             const uint32_t* scales, const float* thr, float* rgba, int64_t n_acc, int mode, float w,
+                             hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if ((prec != 0 && prec != 1) || (enc != 0 && enc != 2) || (mode != -1 && mode != 0 && mode != 2))
+        return hipErrorInvalidValue;
+    const int64_t ntiles = (n + 31) / 32;
+    static int bpc[2][2][3] = {};
+    const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
+    const _Float16* im = reinterpret_cast<const _Float16*>(img);
+    int& b = bpc[prec][enc >> 1][mode + 1 == 0 ? 0 : mode == 0 ? 1 : 2];
+#define NRC_WIDE_LAUNCH(E, P, M) \
+    return launch_persistent_infer(infer_wide_kernel<E, P, M>, 512, b, ntiles, queries, out, n, im, s, epi, scales)
+#define NRC_WIDE_MODES(E, P)                  \
+    switch (mode) {                           \
+        case -1: NRC_WIDE_LAUNCH(E, P, -1);   \
+        case 0: NRC_WIDE_LAUNCH(E, P, 0);     \
+        default: NRC_WIDE_LAUNCH(E, P, 2);    \
+    }
+    if (enc == 0) {
+        if (prec == 0) { NRC_WIDE_MODES(0, 0) } else { NRC_WIDE_MODES(0, 1) }
+    } else {
+        if (prec == 0) { NRC_WIDE_MODES(2, 0) } else { NRC_WIDE_MODES(2, 1) }
+    }
+#undef NRC_WIDE_MODES
+#undef NRC_WIDE_LAUNCH
+}
+
+hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fp8_convert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, y, n, relu);
+    return hipGetLastError();
 }
 
 hipError_t launch_encode_sh(const float* queries, float* enc, int64_t n, hipStream_t s) {

@@ -149,6 +149,14 @@ class Network:
             return None
         check(st)
 
+    def infer_precision(self, precision: int, inputs, outputs, numInputs: int, stream=None) -> None:
+        """Width-128 network: inference through the f16 (0) or FP8 (1) weight image, whatever infer_precision the
+        handle was configured with (A/B timing, parity tests)."""
+        n = int(numInputs)
+        pi = _dev_ptr(inputs, "inputs", n * 15 if hasattr(inputs, "numel") else None)
+        po = _dev_ptr(outputs, "outputs", n * 3 if hasattr(outputs, "numel") else None)
+        check(self._lib.nrc_debug_infer_precision(self._h, int(precision), pi, po, n, _stream_ptr(stream)))
+
     # ---- configuration -----------------------------------------------------------------------
     def setStream(self, stream) -> None:
         check(self._lib.nrc_set_stream(self._h, _stream_ptr(stream)))
@@ -244,9 +252,23 @@ def encode(inputs, encoded, n: int, stream=None) -> None:
     check(lib().nrc_encode(_dev_ptr(inputs, "inputs"), _dev_ptr(encoded, "encoded"), int(n), _stream_ptr(stream)))
 
 
-def default_config(encoding: InputEncoding = InputEncoding.Frequency) -> NrcConfig:
-    return lib().nrc_default_config(int(encoding))
+def default_config(encoding: InputEncoding = InputEncoding.Frequency, width: int = 64,
+                   infer_precision: int = 0) -> NrcConfig:
+    """The reference's hyper-parameters for an encoding; width 128 / infer_precision PRECISION_FP8 select the
+    BASELINE configs[4] network (inference-only in this build)."""
+    c = lib().nrc_default_config(int(encoding))
+    c.width = int(width)
+    c.infer_precision = int(infer_precision)
+    return c
 
 
-__all__ = ["Network", "InputEncoding", "HyperParams", "StateSlot", "NrcError", "encode", "default_config",
+def fp8_convert(x, y, n: int, relu: bool = True, stream=None) -> None:
+    """e4m3 conversion exactly as the FP8 kernels do it (test entry): y[i] = e4m3(clamp(x[i], relu ? 0 : -448, 448))."""
+    py = y if isinstance(y, int) else y.data_ptr()  # uint8 output
+    if not isinstance(y, int) and (not y.is_cuda or y.numel() < n):
+        raise ValueError("y: uint8 GPU tensor of >= n elements required")
+    check(lib().nrc_debug_fp8_convert(_dev_ptr(x, "x", n), py, int(n), int(bool(relu)), _stream_ptr(stream)))
+
+
+__all__ = ["Network", "InputEncoding", "HyperParams", "StateSlot", "NrcError", "encode", "default_config", "fp8_convert",
            "BATCH_SIZE", "NUM_PARAMS", "GRAD_FLOATS", "current_stream"]

@@ -29,7 +29,7 @@ extern "C" {
  *  ORC_TCNN  : tcnn FullyFusedMLP emulation [M]: as MIXED, but every matmul accumulates in f16
  *              (one f16 rounding per 16-wide k chunk, WMMA 16x16x16), and the parameter gradient
  *              is stored as f16 (tcnn keeps PARAMS_T gradients). */
-enum { ORC_FP32 = 0, ORC_MIXED = 1, ORC_TCNN = 2 };
+enum { ORC_FP32 = 0, ORC_MIXED = 1, ORC_TCNN = 2, ORC_FP8 = 3 /* width-128 inference only */ };
 
 float orc_f16_round(float x);
 
@@ -67,6 +67,17 @@ void orc_adam_ema(float* params, float* m, float* v, float* ema, float* infer_pa
  * a pcg32 stream; init parity with tcnn is not attainable [M], parity tests inject weights. */
 void orc_init_params(float* params, uint64_t seed);
 
+
+/* ---- width-128 network (nrc_wide_oracle.c; BASELINE configs[4]) ----
+ * params: NRC_WIDE_NUM_PARAMS f32 canonical blob. kind: NRC_ENCODING_FREQUENCY or NRC_ENCODING_FREQUENCY_SH.
+ * mode: ORC_FP32, ORC_MIXED or ORC_FP8 (spec in nrc_wide_oracle.c). */
+void orc_wide_forward(int kind, const float* params, const float* queries, int64_t n, int mode, float* out,
+                      int nthreads);
+/* RNE onto OCP e4m3fn, |x| <= 448 */
+float orc_e4m3(float x);
+int orc_fp8_row_exponent(float amax);
+/* FP8 inference weights (values incl. their row scale) and the row exponents exps[5][128] of W1..W5 */
+void orc_wide_quantize(const float* params, float* q, int32_t* exps);
 
 /* ---- per-frame kernels around the network (nrc_frame_oracle.c) ---- */
 void orc_accumulate(const float* radiance, const float* throughput, float* rgba, int64_t n, int mode,

@@ -15,8 +15,9 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "liborc.so"
 
-FP32, MIXED, TCNN = 0, 1, 2
+FP32, MIXED, TCNN, FP8 = 0, 1, 2, 3
 NUM_PARAMS = 22528
+WIDE_NUM_PARAMS = 77824
 
 _lib = None
 
@@ -64,6 +65,12 @@ def lib() -> ctypes.CDLL:
         L.orc_hash_corners.argtypes = [vp, ctypes.c_int, vp, vp]
         L.orc_f16_round_double.restype = ctypes.c_float
         L.orc_f16_round_double.argtypes = [ctypes.c_double]
+        L.orc_wide_forward.argtypes = [ctypes.c_int, vp, vp, i64, ctypes.c_int, vp, ctypes.c_int]
+        L.orc_e4m3.restype = ctypes.c_float
+        L.orc_e4m3.argtypes = [ctypes.c_float]
+        L.orc_fp8_row_exponent.restype = ctypes.c_int
+        L.orc_fp8_row_exponent.argtypes = [ctypes.c_float]
+        L.orc_wide_quantize.argtypes = [vp, vp, vp]
         _lib = L
     return _lib
 
@@ -272,3 +279,31 @@ class HashAdamEmaState:
         lr, b1, b2, eps, l2, dec = self.hp
         lib().orc_hash_adam_ema(_v(self.params), _v(self.m), _v(self.v), _v(self.ema), _v(self.infer),
                                 _v(self.grid_steps), self.step, _v(g), self.loss_scale, lr, b1, b2, eps, l2, dec)
+
+
+# ---- width-128 network (nrc_wide_oracle.c) ----
+def wide_forward(params, queries, mode: int = MIXED, threads: int | None = None, encoding: int = FREQUENCY) -> np.ndarray:
+    params = _f32(params)
+    queries = _f32(queries)
+    assert params.size == WIDE_NUM_PARAMS
+    n = queries.shape[0]
+    out = np.zeros((n, 3), np.float32)
+    lib().orc_wide_forward(int(encoding), _v(params), _v(queries), n, mode, _v(out), threads or default_threads())
+    return out
+
+
+def e4m3(x: float) -> float:
+    return lib().orc_e4m3(float(x))
+
+
+def fp8_row_exponent(amax: float) -> int:
+    return lib().orc_fp8_row_exponent(float(amax))
+
+
+def wide_quantize(params):
+    """(quantized weight values incl. row scales [77824], row exponents [5][128]) of the FP8 inference path"""
+    params = _f32(params)
+    q = np.zeros(WIDE_NUM_PARAMS, np.float32)
+    e = np.zeros((5, 128), np.int32)
+    lib().orc_wide_quantize(_v(params), _v(q), _v(e))
+    return q, e

@@ -15,7 +15,7 @@ def header_functions() -> list[str]:
     names = set()
     for h in HEADERS:
         text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
-        names |= set(re.findall(r"\b(nrc_[a-z_]+)\s*\(", text))
+        names |= set(re.findall(r"\b(nrc_[a-z0-9_]+)\s*\(", text))
     return sorted(names)
 
 
