@@ -81,7 +81,66 @@ static uint32_t rnd() {
     return rng_state >> 8;
 }
 
-int main() {
+// Dump mode (fp8_probe dump <file>): T trials of random A, B (bytes), C (f32) and the hardware D, for offline
+// modelling of the block sum: per trial 64x32 A bytes, 64x32 B bytes, 64x16 C floats, 64x16 D floats.
+__global__ void mfma_dump(const v8i* a, const v8i* b, const float* cin, float* d, int trials) {
+    const int l = threadIdx.x;
+    for (int t = 0; t < trials; ++t) {
+        v16f c;
+        for (int i = 0; i < 16; ++i) c[i] = cin[(t * 64 + l) * 16 + i];
+        c = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[t * 64 + l], b[t * 64 + l], c, 0, 0, 0, 127, 0, 127);
+        for (int i = 0; i < 16; ++i) d[(t * 64 + l) * 16 + i] = c[i];
+    }
+}
+
+static int dump(const char* path) {
+    const int T = 256;
+    std::vector<uint8_t> A(T * 64 * 32), B(T * 64 * 32);
+    std::vector<float> C(T * 64 * 16), D(T * 64 * 16);
+    for (int t = 0; t < T; ++t) {
+        const int span = 1 + t % 14;  // exponent spread of the operands
+        for (int i = 0; i < 64 * 32; ++i) {
+            for (int which = 0; which < 2; ++which) {
+                uint8_t c;
+                do {
+                    const int e = 7 - span / 2 + (int)(rnd() % (span + 1));
+                    c = (uint8_t)(((rnd() & 1) << 7) | ((e & 15) << 3) | (rnd() & 7));
+                } while ((c & 0x7f) == 0x7f || ((c >> 3) & 15) == 0);
+                if (t % 4 == 3 && (rnd() % 4) == 0) c &= 0x80;  // some zeros
+                (which ? B : A)[t * 64 * 32 + i] = c;
+            }
+        }
+        for (int i = 0; i < 64 * 16; ++i) {
+            const float u = (float)(rnd() & 0xffff) / 65536.0f - 0.5f;
+            C[t * 64 * 16 + i] = (t % 2) ? std::ldexp(u, (int)(rnd() % 16) - 8) : 0.0f;
+        }
+    }
+    v8i *dA, *dB;
+    float *dC, *dD;
+    CK(hipMalloc(&dA, A.size()));
+    CK(hipMalloc(&dB, B.size()));
+    CK(hipMalloc(&dC, C.size() * 4));
+    CK(hipMalloc(&dD, D.size() * 4));
+    CK(hipMemcpy(dA, A.data(), A.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, B.data(), B.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dC, C.data(), C.size() * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(mfma_dump, dim3(1), dim3(64), 0, 0, dA, dB, dC, dD, T);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(D.data(), dD, D.size() * 4, hipMemcpyDeviceToHost));
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return 3;
+    std::fwrite(&T, 4, 1, f);
+    std::fwrite(A.data(), 1, A.size(), f);
+    std::fwrite(B.data(), 1, B.size(), f);
+    std::fwrite(C.data(), 4, C.size(), f);
+    std::fwrite(D.data(), 4, D.size(), f);
+    std::fclose(f);
+    std::printf("dumped %d trials to %s\n", T, path);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc == 3 && std::strcmp(argv[1], "dump") == 0) return dump(argv[2]);
     int fails = 0;
     // ---- 1 + 2: MFMA pairing and scale byte select
     std::vector<uint8_t> A(64 * 32), B(64 * 32);
