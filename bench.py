@@ -28,6 +28,8 @@ FLOP_PER_QUERY = 2 * (66 * 64 + 4 * 64 * 64 + 64 * 3)  # 41,600 algorithmic (SUR
 BYTES_PER_QUERY = 60 + 12
 TRAIN_FLOP_PER_SAMPLE = 116_352
 PEAK_F16_TFLOPS = 2500.0  # MI355X dense f16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0  # MI355X dense fp8 (MX-scaled) MFMA
+FLOP_PER_QUERY_WIDE = 2 * (66 * 128 + 4 * 128 * 128 + 128 * 3)  # 148,736
 PEAK_HBM_GBS = 8000.0
 QUERIES_PER_GPU = 1 << 21
 ROUND = "r01"
@@ -42,6 +44,7 @@ def parse():
     ap.add_argument("--train-frames", type=int, default=20, help="timed frames of 4 x 16384 training")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-wide", action="store_true", help="skip the configs[4] width-128 f16/FP8 inference lines")
     ap.add_argument("--frame-iters", type=int, default=20, help="timed 1080p post-trace frames (0: skip)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one "
@@ -128,6 +131,45 @@ def frame_bench(nrc, net, dev, iters: int) -> dict:
     return {"frame_ms": ms, "queries": S + T, "train_records": f.num_training_records, "iters": iters,
             "what": "nrc_process_frame: fused infer+accumulate, propagate, Feistel shuffle, 4 x 16384 train with "
                     "loss read-back; synthetic 1920x1080 Cornell frame, 8x8 tiles"}
+
+
+def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
+    """BASELINE configs[4] (C5): the width-128 network on the ~8M-query 4K frame, sharded over the ranks
+    (2^23 / world queries per GPU, no collective), f16 and FP8 inference; HIP events on the launch stream and the
+    max-over-ranks wall time."""
+    import torch
+    import torch.distributed as dist
+
+    nq = (1 << 23) // world
+    q = torch.from_numpy(nrc.synthetic.cornell_queries(nq, seed=nrc.synthetic.SEED + 1000 + rank)).to(dev)
+    out = torch.empty((nq, 3), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream()
+    net = nrc.Network()
+    net.init(stream=stream, encoding=nrc.InputEncoding.Frequency,
+             config=nrc.default_config(nrc.InputEncoding.Frequency, width=128))
+    res = {"workload": "configs[4]: 128-wide 5-hidden-layer MLP + Frequency encoding, 4K frame of 2^23 queries "
+                       "sharded over the GPUs (xavier-init weights)", "queries_per_gpu": nq,
+           "flop_per_query": FLOP_PER_QUERY_WIDE}
+    for prec, name, peak in ((nrc.PRECISION_F16, "f16", PEAK_F16_TFLOPS), (nrc.PRECISION_FP8, "fp8", PEAK_FP8_TFLOPS)):
+        for _ in range(3):
+            net.infer_precision(prec, q, out, nq, stream=stream)
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            net.infer_precision(prec, q, out, nq, stream=stream)
+        ev1.record(stream)
+        barrier()
+        wall = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        kms = ev0.elapsed_time(ev1) / steps
+        tf = FLOP_PER_QUERY_WIDE * nq / (kms * 1e-3) / 1e12
+        res[name] = {"M_queries_per_s": world * nq * steps / float(wall.item()) / 1e6, "kernel_ms": kms,
+                     "achieved_tflops": tf, "peak_tflops": peak, "frac": tf / peak}
+    net.destroy()
+    return res
 
 
 def pmc_traffic() -> float | None:
@@ -242,6 +284,8 @@ def main() -> None:
     if world == 1 and args.frame_iters > 0:
         frame = frame_bench(nrc, net, dev, args.frame_iters)
 
+    wide = None if args.no_wide else wide_bench(nrc, dev, world, rank, max(10, args.steps // 4), barrier)
+
     achieved = FLOP_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e12
     result = {
         "metric": "M radiance queries/sec + train-step ms, 64x5 MLP @ 2M samples/frame",
@@ -265,6 +309,7 @@ def main() -> None:
         "train_frame_ms": train_frame_ms,
         "infer_kernel_ms": kernel_ms,
         "frame": frame,
+        "wide_c5": wide,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F16_TFLOPS, "traffic": pmc_traffic(),
                      "algorithmic_bytes_per_launch": BYTES_PER_QUERY * nq,

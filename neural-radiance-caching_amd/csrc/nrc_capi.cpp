@@ -239,10 +239,15 @@ struct nrc_net {
     uint32_t* grid_steps = nullptr;
     _Float16 *table_train = nullptr, *table_infer = nullptr;
 
-    // width-128 network (BASELINE configs[4]): inference images only
+    // width-128 network (BASELINE configs[4]): inference images (f16, FP8 + row scales), training images (f16
+    // forward / backward from the master weights) and the training workspace
     uint8_t *wide_img16 = nullptr, *wide_img8 = nullptr;
     uint32_t* wide_scales = nullptr;
     int32_t* wide_exps = nullptr;
+    _Float16 *wide_fwd_train = nullptr, *wide_bwd_train = nullptr;
+    _Float16 *wide_ws_in = nullptr, *wide_ws_d = nullptr;
+    float *wide_slabs = nullptr, *wide_loss_partials = nullptr;
+    int64_t wide_ws_bpad = 0;
 
     bool hash() const { return encoding == NRC_ENCODING_HASH; }
     bool wide() const { return cfg.width == NRC_WIDE_WIDTH; }
@@ -259,9 +264,13 @@ struct nrc_net {
         f(slabs); f(loss_partials); f(loss_dev);
         f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
         f(wide_img16); f(wide_img8); f(wide_scales); f(wide_exps);
+        f(wide_fwd_train); f(wide_bwd_train); f(wide_ws_in); f(wide_ws_d); f(wide_slabs); f(wide_loss_partials);
         wide_img16 = wide_img8 = nullptr;
         wide_scales = nullptr;
         wide_exps = nullptr;
+        wide_fwd_train = wide_bwd_train = wide_ws_in = wide_ws_d = nullptr;
+        wide_slabs = wide_loss_partials = nullptr;
+        wide_ws_bpad = 0;
         grid_grad = nullptr;
         grid_steps = nullptr;
         table_train = table_infer = nullptr;
@@ -300,6 +309,22 @@ struct nrc_net {
         o.l2_reg = cfg.l2_reg; o.ema_decay = cfg.ema_decay; o.loss_scale = cfg.loss_scale; o.step = s;
         return o;
     }
+    void ensure_wide_ws(int64_t b) {
+        const int64_t bpad = wide_bpad(b);
+        if (bpad <= wide_ws_bpad) return;
+        auto f = [](void* p) {
+            if (p) HIP_CHECK(hipFree(p));
+        };
+        f(wide_ws_in); f(wide_ws_d); f(wide_slabs); f(wide_loss_partials);
+        wide_ws_in = wide_ws_d = nullptr;
+        wide_slabs = wide_loss_partials = nullptr;
+        wide_ws_bpad = 0;
+        HIP_CHECK(hipMalloc(&wide_ws_in, sizeof(_Float16) * kWideInRows * bpad));
+        HIP_CHECK(hipMalloc(&wide_ws_d, sizeof(_Float16) * kWideDRows * bpad));
+        HIP_CHECK(hipMalloc(&wide_slabs, sizeof(float) * NRC_WIDE_NUM_PARAMS * (size_t)wide_chunks(bpad)));
+        HIP_CHECK(hipMalloc(&wide_loss_partials, sizeof(float) * (size_t)(bpad / 32)));
+        wide_ws_bpad = bpad;
+    }
     void ensure_slabs(int blocks) {
         if (blocks <= slab_blocks) return;
         if (slabs) HIP_CHECK(hipFree(slabs));
@@ -328,27 +353,42 @@ void upload_all(nrc_net* net, const std::vector<float>& params, const std::vecto
 
 void repack(nrc_net* net, hipStream_t s) {
     if (net->wide()) {
-        HIP_CHECK(launch_wide_pack(net->infer, net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0,
-                                   reinterpret_cast<_Float16*>(net->wide_img16), net->wide_img8, net->wide_scales,
-                                   net->wide_exps, s));
+        const int enc = net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0;
+        HIP_CHECK(launch_wide_pack(net->infer, enc, reinterpret_cast<_Float16*>(net->wide_img16), net->wide_img8,
+                                   net->wide_scales, net->wide_exps, s));
+        HIP_CHECK(launch_wide_pack_train(net->params, enc, net->wide_fwd_train, net->wide_bwd_train, s));
         return;
     }
     HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
     if (net->hash()) HIP_CHECK(launch_grid_adam(kPackOnly, net->grid_buffers(), net->optim(1), s));
 }
 
-void require_trainable(const nrc_net* net) {
-    if (net->wide())
-        throw ApiError(NRC_ERR_UNSUPPORTED,
-                       "the width-128 network (BASELINE configs[4]) is inference-only in this build: load its weights "
-                       "with nrc_set_state");
+// width-128 fwd/bwd + dW partials of b samples normalised by n_total (nrc_kernels.hip wide_fwd_bwd_kernel)
+void wide_grad_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total) {
+    net->ensure_wide_ws(b);
+    HIP_CHECK(launch_wide_train_fwd_bwd(net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0, in, tgt, b, n_total,
+                                        net->cfg.loss_scale, net->wide_fwd_train, net->wide_bwd_train, net->wide_ws_in,
+                                        net->wide_ws_d, net->wide_slabs, net->wide_loss_partials, net->stream));
 }
 
 void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h, float* loss_d = nullptr) {
     check_live(net);
-    require_trainable(net);
     if (b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "batch size must be >= 1");
     if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
+    if (net->wide()) {
+        wide_grad_partials(net, in, tgt, b, 3.0f * (float)b);
+        net->step += 1;
+        HIP_CHECK(launch_wide_adam(kReduceFused, net->wide_slabs, wide_chunks(b), net->wide_loss_partials,
+                                   (int)(wide_bpad(b) / 32), nullptr, loss_d ? loss_d : net->loss_dev, net->buffers(),
+                                   net->optim(net->step), net->stream));
+        repack(net, net->stream);
+        if (loss_h) {
+            HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
+            HIP_CHECK(hipStreamSynchronize(net->stream));
+            *loss_h = *net->loss_host;
+        }
+        return;
+    }
     const int blocks = train_blocks(b);
     net->ensure_slabs(blocks);
     if (net->hash())
@@ -484,6 +524,8 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->wide_img8, kWide8Bytes));
             HIP_CHECK(hipMalloc(&net->wide_scales, sizeof(uint32_t) * 5 * 32));
             HIP_CHECK(hipMalloc(&net->wide_exps, sizeof(int32_t) * 5 * 128));
+            HIP_CHECK(hipMalloc(&net->wide_fwd_train, kWideF16Bytes));
+            HIP_CHECK(hipMalloc(&net->wide_bwd_train, kWideBwdBytes));
             HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
             HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
             HIP_CHECK(hipMemset(net->loss_dev, 0, sizeof(float) * 4));
@@ -493,6 +535,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             net->initialized = true;
             repack(net, nullptr);
             HIP_CHECK(hipDeviceSynchronize());
+            net->ensure_wide_ws(NRC_BATCH_SIZE);
             if (verbose)
                 std::printf("\n----------------------- NETWORK CONFIG -----------------------\n%s\n"
                             "--------------------------------------------------------------\n\n",
@@ -694,7 +737,6 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
                           float* grad_d) {
     return guarded([&] {
         check_live(net);
-        require_trainable(net);
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
         if (b == 0) {
@@ -702,6 +744,13 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
             return;
         }
         if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
+        if (net->wide()) {
+            wide_grad_partials(net, in, tgt, b, 3.0f * (float)global_b);
+            HIP_CHECK(launch_wide_adam(kReduceOnly, net->wide_slabs, wide_chunks(b), net->wide_loss_partials,
+                                       (int)(wide_bpad(b) / 32), grad_d, nullptr, net->buffers(),
+                                       net->optim(net->step + 1), net->stream));
+            return;
+        }
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
         if (net->hash()) {
@@ -723,9 +772,20 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
     return guarded([&] {
         check_live(net);
-        require_trainable(net);
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         net->step += 1;
+        if (net->wide()) {
+            HIP_CHECK(launch_wide_adam(kApplyOnly, nullptr, 0, nullptr, 0, const_cast<float*>(grad_d), net->loss_dev,
+                                       net->buffers(), net->optim(net->step), net->stream));
+            repack(net, net->stream);
+            if (loss_h) {
+                HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost,
+                                         net->stream));
+                HIP_CHECK(hipStreamSynchronize(net->stream));
+                *loss_h = *net->loss_host;
+            }
+            return;
+        }
         HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
                                      net->buffers(), net->optim(net->step), net->stream));
         if (net->hash()) {
@@ -838,7 +898,7 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tg
     return guarded([&] {
         check_live(net);
         require_frequency(net, "nrc_debug_train_stamps");
-        require_trainable(net);
+        if (net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "training stamps are a 64-wide diagnostic");
         if (!in || !tgt || !stamps_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);

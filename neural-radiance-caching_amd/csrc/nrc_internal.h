@@ -110,6 +110,20 @@ hipError_t launch_wide_pack(const float* w, int enc, _Float16* img16, uint8_t* i
 hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out, int64_t n, const void* img,
                              const uint32_t* scales, const float* thr, float* rgba, int64_t n_acc, int mode, float w,
                              hipStream_t s);
+// width-128 training (nrc_kernels.hip): backward image W_l^T (L5^T 4 M-blocks x 1 k-step, L4^T..L1^T 4 x 8)
+constexpr int kWideBwdFrags = 4 + 4 * 4 * 8;  // 132
+constexpr int kWideBwdBytes = kWideBwdFrags * 1024;
+// workspace rows ([feature][bpad] f16): inputs x (80) + a_0..a_4 (5 x 128) = 720; deltas 5 x 128 + 16 = 656
+constexpr int kWideInRows = 80 + 5 * 128, kWideDRows = 5 * 128 + 16;
+int64_t wide_bpad(int64_t b);
+int wide_chunks(int64_t b);
+hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float* targets, int64_t b, float n_total,
+                                     float loss_scale, const _Float16* fwd16, const _Float16* bwd16, _Float16* ws_in,
+                                     _Float16* ws_d, float* slabs, float* loss_partials, hipStream_t s);
+hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const float* loss_partials, int nlp,
+                            float* grad_io, float* loss_out, const struct ModelBuffers& mb, const struct OptimArgs& oa,
+                            hipStream_t s);
+hipError_t launch_wide_pack_train(const float* w, int enc, _Float16* fwd16, _Float16* bwd16, hipStream_t s);
 // diagnostic: e4m3 conversion exactly as the FP8 kernels do it (clamp to [lo, 448], v_cvt_pk_fp8_f32)
 hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s);
 

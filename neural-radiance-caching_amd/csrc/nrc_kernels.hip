@@ -2225,6 +2225,257 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 }
 
 // ------------------------------------------------------------------------------------------------
+// Width-128 training step (BASELINE configs[4]; oracle/nrc_wide_oracle.c orc_wide_grad + orc_adam_ema):
+//   wide_fwd_bwd_kernel  one wave per 32 samples: encode, forward (f16 MFMA chain, A fragments straight from the
+//                        L2-resident training images), RelativeL2Luminance, delta chain through W_l^T; stores every
+//                        layer's input and delta as f16 [feature][sample] rows of a workspace;
+//   wide_dw_kernel       dW_l = sum_s delta_l in_l^T as 32x32 tiles x 1024-sample chunks (A and B fragments are
+//                        16-byte loads of those rows), partial sums per chunk in canonical parameter order;
+//   wide_adam_kernel     fixed-order chunk sum + tcnn Adam + EMA per parameter (same float operations as
+//                        adam_pack_one), then the f16 / FP8 images are repacked (launch_wide_pack, wide_pack_train).
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ constexpr int wide_bwd_frag(int layer, int mb, int kk) {
+    return layer == 5 ? mb : 4 + (layer - 1) * 32 + mb * 8 + kk;
+}
+__host__ __device__ constexpr int64_t wide_in_row(int layer) { return layer == 0 ? 0 : 80 + (layer - 1) * 128; }
+__host__ __device__ constexpr int64_t wide_d_row(int layer) { return (int64_t)layer * 128; }
+__host__ __device__ constexpr int wide_off(int layer) {
+    return layer == 0 ? NRC_WIDE_W0_OFFSET : layer <= 4 ? NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 : NRC_WIDE_W5_OFFSET;
+}
+
+// f16 B fragments (rows acc_row(kk, h, j)) -> ws[(row0 + row) * bpad + s]
+__device__ __forceinline__ void store_frag_rows(_Float16* __restrict__ ws, int64_t bpad, int64_t s, int h,
+                                                const h8 (&y)[8]) {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ws[(int64_t)acc_row(kk, h, j) * bpad + s] = y[kk][j];
+}
+
+template <int ENC>
+__global__ __launch_bounds__(64, 1) void wide_fwd_bwd_kernel(const float* __restrict__ q, const float* __restrict__ t,
+                                                             int64_t b, int64_t bpad, float n_total, float loss_scale,
+                                                             const h8* __restrict__ wf, const h8* __restrict__ wb,
+                                                             _Float16* __restrict__ ws_in, _Float16* __restrict__ ws_d,
+                                                             float* __restrict__ loss_partials) {
+    fp32_flush_output_denorms();  // the omod doubling-chain encoder (as the inference kernels)
+    const int lane = threadIdx.x, h = lane >> 5, r = lane & 31;
+    const int64_t s = (int64_t)blockIdx.x * 32 + r;  // s < bpad
+    const bool valid = s < b;
+    const int64_t sc = valid ? s : b - 1;
+    const QLane Q = load_q_enc<ENC>(q, sc, h);
+    float tgt[3] = {0.f, 0.f, 0.f};
+    if (h == 0) {
+        tgt[0] = t[sc * 3 + 0];
+        tgt[1] = t[sc * 3 + 1];
+        tgt[2] = t[sc * 3 + 2];
+    }
+    h8 x[5];
+    if constexpr (ENC == 2) encode_sh<true>(Q, h, x);
+    else encode_fast<true>(Q, h, x);
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ws_in[(int64_t)enc_k0_feature(ENC, 16 * kk + 8 * h + j) * bpad + s] = x[kk][j];
+
+    const h8* wl = wf + lane;
+    h8 a[5][8];
+    f16v c[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(0, mb, kk) * 64], x[kk], c[mb]);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) a[0][kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
+    store_frag_rows(ws_in + wide_in_row(1) * bpad, bpad, s, h, a[0]);
+#pragma unroll
+    for (int l = 1; l < 5; ++l) {
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(l, mb, kk) * 64], a[l - 1][kk], c[mb]);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) a[l][kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
+        store_frag_rows(ws_in + wide_in_row(l + 1) * bpad, bpad, s, h, a[l]);
+    }
+    f16v o = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) o = mfma(wl[wide_frag(5, 0, kk) * 64], a[4][kk], o);
+
+    // RelativeL2Luminance on the f16 prediction, loss-scaled f16 gradient, ReLU-masked (as train_kernel)
+    float lossv = 0.0f;
+    h8 g = {};
+    if (h == 0) {
+        float y[3];
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) y[cc] = (float)(_Float16)fmaxf(o[cc], 0.0f);
+        const float lum = 0.299f * y[0] + 0.587f * y[1] + 0.114f * y[2];
+        const float denom = lum * lum + NRC_LUM_EPS;
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) {
+            const float diff = y[cc] - tgt[cc];
+            const float lv = diff * diff / denom / n_total;
+            const float gv = loss_scale * 2.0f * diff / denom / n_total;
+            lossv += valid ? lv : 0.0f;
+            g[cc] = (valid && y[cc] > 0.0f) ? (_Float16)gv : (_Float16)0.0f;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lossv += __shfl_xor(lossv, off);
+    if (lane == 0) loss_partials[blockIdx.x] = lossv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ws_d[(wide_d_row(5) + acc_row(0, h, j)) * bpad + s] = g[j];
+
+    // delta chain: d_{l-1} = relu'(a_{l-1}) (W_l^T d_l); accumulator block mb regs 0-7 / 8-15 are the rows of the
+    // B fragments 2 mb / 2 mb + 1, so the gate takes the activation fragments as they are
+    const h8* bl = wb + lane;
+    h8 d[8];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(bl[wide_bwd_frag(5, mb, 0) * 64], g, zero16());
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) mask_pack_pk(c[mb], a[4][2 * mb], a[4][2 * mb + 1], d[2 * mb], d[2 * mb + 1]);
+    store_frag_rows(ws_d + wide_d_row(4) * bpad, bpad, s, h, d);
+#pragma unroll
+    for (int l = 4; l >= 1; --l) {
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(bl[wide_bwd_frag(l, mb, kk) * 64], d[kk], c[mb]);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+            mask_pack_pk(c[mb], a[l - 1][2 * mb], a[l - 1][2 * mb + 1], d[2 * mb], d[2 * mb + 1]);
+        store_frag_rows(ws_d + wide_d_row(l - 1) * bpad, bpad, s, h, d);
+    }
+}
+
+// One wave per (32x32 tile of dW_l, chunk of kWideChunk samples). Tiles: layer 0 4 x 3 (80 inputs), layers 1-4
+// 4 x 4, layer 5 1 x 4 (16 outputs) = 80.
+constexpr int kWideTiles = 12 + 64 + 4;
+constexpr int kWideChunk = 1024;
+__global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict__ ws_in, const _Float16* __restrict__ ws_d,
+                                                      int64_t bpad, int nchunks, float* __restrict__ slabs) {
+    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (task >= kWideTiles * nchunks) return;
+    const int tile = task % kWideTiles, chunk = task / kWideTiles;
+    int layer, mb, nb;
+    if (tile < 12) { layer = 0; mb = tile / 3; nb = tile % 3; }
+    else if (tile < 76) { layer = 1 + (tile - 12) / 16; mb = ((tile - 12) % 16) / 4; nb = (tile - 12) % 4; }
+    else { layer = 5; mb = 0; nb = tile - 76; }
+    const int in_dim = layer == 0 ? NRC_ENC_WIDTH : 128, out_dim = layer == 5 ? NRC_OUT_PADDED : 128;
+    const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    const int o = 32 * mb + r, i = 32 * nb + r;  // this lane's A row / B column
+    const bool oa = o < out_dim, ib = i < in_dim;
+    const h8* pa = reinterpret_cast<const h8*>(ws_d + (wide_d_row(layer) + (oa ? o : 0)) * bpad + 8 * h);
+    const h8* pb = reinterpret_cast<const h8*>(ws_in + (wide_in_row(layer) + (ib ? i : 0)) * bpad + 8 * h);
+    const int64_t k0 = (int64_t)chunk * kWideChunk, k1 = min<int64_t>(bpad, k0 + kWideChunk);
+    f16v acc[2] = {zero16(), zero16()};
+    const h8 z = {};
+    int u = 0;
+    for (int64_t k = k0; k < k1; k += 16, u ^= 1) {
+        const h8 av = oa ? pa[k >> 3] : z;
+        const h8 bv = ib ? pb[k >> 3] : z;
+        acc[u] = mfma(av, bv, acc[u]);
+    }
+    const f16v sum = acc[0] + acc[1];
+    float* slab = slabs + (int64_t)chunk * NRC_WIDE_NUM_PARAMS + wide_off(layer);
+    if (!ib) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < out_dim) slab[row * in_dim + i] = sum[reg];
+    }
+}
+
+// fixed-order chunk sum + Adam + EMA (modes as reduce_adam_kernel); loss partials summed by wave 0 of block 0
+__global__ __launch_bounds__(256) void wide_adam_kernel(int mode, const float* __restrict__ slabs, int nchunks,
+                                                        const float* __restrict__ loss_partials, int nlp,
+                                                        float* __restrict__ grad_io, float* __restrict__ loss_out,
+                                                        ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+#pragma clang fp contract(off)
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        if (mode == kReduceFused || mode == kReduceOnly) {
+            float L = 0.0f;
+            for (int i = threadIdx.x; i < nlp; i += 64) L += loss_partials[i];
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
+            if (threadIdx.x == 0) {
+                if (mode == kReduceOnly) grad_io[mb.n_total] = L;
+                else if (loss_out) loss_out[0] = L;
+            }
+        } else if (mode == kApplyOnly && loss_out && threadIdx.x == 0) {
+            loss_out[0] = grad_io[mb.n_total];
+        }
+    }
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= NRC_WIDE_NUM_PARAMS) return;
+    float gsum = 0.0f;
+    if (mode == kApplyOnly) {
+        gsum = grad_io[p];
+    } else {
+        for (int c = 0; c < nchunks; ++c) gsum += slabs[(int64_t)c * NRC_WIDE_NUM_PARAMS + p];
+        if (mode == kReduceOnly) {
+            grad_io[p] = gsum;
+            return;
+        }
+    }
+    float gradient = gsum / oa.loss_scale;
+    float w = mb.params[p];
+    gradient += oa.l2_reg * w;
+    const float gsq = gradient * gradient;
+    const float m1 = oa.beta1 * mb.m[p] + (1.0f - oa.beta1) * gradient;
+    const float v1 = oa.beta2 * mb.v[p] + (1.0f - oa.beta2) * gsq;
+    mb.m[p] = m1;
+    mb.v[p] = v1;
+    const float eff = lr_t / (sqrtf(v1) + oa.eps);
+    w = w - eff * m1;
+    mb.params[p] = w;
+    const float e = mb.ema[p] * oa.ema_decay + w * (1.0f - oa.ema_decay);
+    mb.ema[p] = e;
+    mb.infer[p] = e / ema_debias;
+}
+
+// training images from the f32 master weights: forward (img16, as wide_pack_kernel) and backward W_l^T fragments
+__global__ void wide_pack_train_kernel(const float* __restrict__ w, int enc, _Float16* __restrict__ fwd16,
+                                       _Float16* __restrict__ bwd16) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int UF = kWideF16Frags * 64, UB = kWideBwdFrags * 64;
+    if (u < UF) {
+        const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
+        int layer, mb, kk;
+        if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
+        else if (f < 148) { layer = 1 + (f - 20) / 32; mb = ((f - 20) % 32) / 8; kk = (f - 20) % 8; }
+        else { layer = 5; mb = 0; kk = f - 148; }
+        const int row = 32 * mb + r;
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x = 0.0f;
+            if (layer == 0) x = w[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
+            else if (layer < 5 || row < NRC_OUT_PADDED) x = w[wide_off(layer) + row * 128 + acc_row(kk, h, j)];
+            v[j] = (_Float16)x;
+        }
+        reinterpret_cast<h8*>(fwd16)[u] = v;
+    } else if (u < UF + UB) {
+        const int v8 = u - UF, f = v8 / 64, lane = v8 % 64, r = lane & 31, h = lane >> 5;
+        const int layer = f < 4 ? 5 : 1 + (f - 4) / 32, mb = f < 4 ? f : ((f - 4) % 32) / 8, kk = f < 4 ? 0 : (f - 4) % 8;
+        const int col = 32 * mb + r;  // row of W_l^T = input feature of layer l
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int row = acc_row(kk, h, j);  // output neuron of layer l
+            v[j] = (_Float16)w[wide_off(layer) + row * 128 + col];
+        }
+        reinterpret_cast<h8*>(bwd16)[v8] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
 static int num_cus() {
@@ -2393,6 +2644,42 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
     }
 #undef NRC_WIDE_MODES
 #undef NRC_WIDE_LAUNCH
+}
+
+int64_t wide_bpad(int64_t b) { return (b + 31) / 32 * 32; }
+int wide_chunks(int64_t b) { return (int)((wide_bpad(b) + kWideChunk - 1) / kWideChunk); }
+
+hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float* targets, int64_t b, float n_total,
+                                     float loss_scale, const _Float16* fwd16, const _Float16* bwd16, _Float16* ws_in,
+                                     _Float16* ws_d, float* slabs, float* loss_partials, hipStream_t s) {
+    if (b <= 0) return hipSuccess;
+    const int64_t bpad = wide_bpad(b);
+    const int tiles = (int)(bpad / 32);
+    if (enc == 2)
+        hipLaunchKernelGGL(wide_fwd_bwd_kernel<2>, dim3(tiles), dim3(64), 0, s, queries, targets, b, bpad, n_total,
+                           loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
+    else
+        hipLaunchKernelGGL(wide_fwd_bwd_kernel<0>, dim3(tiles), dim3(64), 0, s, queries, targets, b, bpad, n_total,
+                           loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
+    const int nch = wide_chunks(b);
+    hipLaunchKernelGGL(wide_dw_kernel, dim3((kWideTiles * nch + 3) / 4), dim3(256), 0, s, ws_in, ws_d, bpad, nch, slabs);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const float* loss_partials, int nlp,
+                            float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+    const float step = (float)(oa.step ? oa.step : 1);
+    const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
+    const float ema_debias = 1.0f - powf(oa.ema_decay, step);
+    hipLaunchKernelGGL(wide_adam_kernel, dim3((NRC_WIDE_NUM_PARAMS + 255) / 256), dim3(256), 0, s, mode, slabs, nchunks,
+                       loss_partials, nlp, grad_io, loss_out, mb, oa, lr_t, ema_debias);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_pack_train(const float* w, int enc, _Float16* fwd16, _Float16* bwd16, hipStream_t s) {
+    constexpr int units = (kWideF16Frags + kWideBwdFrags) * 64;
+    hipLaunchKernelGGL(wide_pack_train_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w, enc, fwd16, bwd16);
+    return hipGetLastError();
 }
 
 hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s) {

@@ -78,6 +78,10 @@ float orc_e4m3(float x);
 int orc_fp8_row_exponent(float amax);
 /* FP8 inference weights (values incl. their row scale) and the row exponents exps[5][128] of W1..W5 */
 void orc_wide_quantize(const float* params, float* q, int32_t* exps);
+/* loss-scaled gradient + loss of one minibatch (ORC_FP32 / ORC_MIXED), as orc_grad_enc at width 128; the optimizer
+ * step is orc_adam_ema with n = NRC_WIDE_NUM_PARAMS. */
+double orc_wide_grad(int kind, const float* params, const float* queries, const float* targets, int64_t b,
+                     double n_total, float loss_scale, int mode, float* grad, int nthreads);
 
 /* ---- per-frame kernels around the network (nrc_frame_oracle.c) ---- */
 void orc_accumulate(const float* radiance, const float* throughput, float* rgba, int64_t n, int mode,

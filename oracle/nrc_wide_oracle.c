@@ -1,6 +1,7 @@
 /*
  * nrc_wide_oracle.c — CPU restatement of the width-128 network of BASELINE.json configs[4] (SURVEY.md §8 C5:
- * "128-wide MLP, CDNA4 fp8 MFMA"), for the inference path of csrc/nrc_kernels.hip infer_wide_kernel.
+ * "128-wide MLP, CDNA4 fp8 MFMA"): forward (csrc/nrc_kernels.hip infer_wide_kernel) and training gradient
+ * (wide_fwd_bwd_kernel + wide_dw_kernel).
  *
  * TEST INFRASTRUCTURE ONLY (see nrc_oracle.h): only tests/, smoke() and bench.py's cpu_baseline leg load it.
  *
@@ -155,4 +156,120 @@ void orc_wide_forward(int kind, const float* params, const float* queries, int64
     if (nthreads > 1)
         for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     free(w);
+}
+
+/* ---- training (ORC_FP32 / ORC_MIXED): the 64-wide grad_job of nrc_oracle.c at width 128 ----
+ * forward as orc_wide_forward; RelativeL2Luminance gradient (loss-scaled, f16 in MIXED), ReLU output gate;
+ * delta chain delta_{l-1} = relu'(a_{l-1}) (W_l^T delta_l), f16-rounded in MIXED; dW_l = sum_s delta_l in_l^T in f64. */
+typedef struct {
+    const float* w;
+    const float* queries;
+    const float* targets;
+    int64_t begin, end;
+    int mode, kind;
+    float n_total, loss_scale;
+    double* grad;
+    double loss;
+} wide_grad_job;
+
+static void* wide_grad_run(void* arg) {
+    wide_grad_job* J = (wide_grad_job*)arg;
+    const int mode = J->mode;
+    float enc[NRC_ENC_WIDTH], act[5][NRC_WIDE_WIDTH], y[NRC_OUT_PADDED];
+    float d[2][NRC_WIDE_WIDTH];
+    for (int64_t s = J->begin; s < J->end; ++s) {
+        const float* q = J->queries + s * NRC_INPUT_DIMS;
+        if (J->kind == NRC_ENCODING_FREQUENCY_SH) orc_encode_sh(q, 1, enc);
+        else orc_encode(q, 1, enc);
+        if (mode != ORC_FP32)
+            for (int f = 0; f < NRC_ENC_WIDTH; ++f) enc[f] = orc_f16_round(enc[f]);
+        const float* in = enc;
+        for (int l = 0; l < NRC_NUM_LAYERS; ++l) {
+            float* o = l < 5 ? act[l] : y;
+            for (int r = 0; r < kWOut[l]; ++r) {
+                const float* wr = J->w + kWOff[l] + r * kWIn[l];
+                double acc = 0.0;
+                for (int k = 0; k < kWIn[l]; ++k) acc += (double)wr[k] * (double)in[k];
+                const float a = (float)acc > 0.0f ? (float)acc : 0.0f;
+                o[r] = mode == ORC_FP32 ? a : orc_f16_round(a);
+            }
+            in = o;
+        }
+        const float* t = J->targets + s * NRC_OUTPUT_DIMS;
+        const float lum = 0.299f * y[0] + 0.587f * y[1] + 0.114f * y[2];
+        const float denom = lum * lum + NRC_LUM_EPS;
+        float* delta = d[1];
+        for (int c = 0; c < NRC_OUT_PADDED; ++c) delta[c] = 0.0f;
+        for (int c = 0; c < NRC_OUTPUT_DIMS; ++c) {
+            const float diff = y[c] - t[c];
+            J->loss += (double)(diff * diff / denom / J->n_total);
+            float g = J->loss_scale * 2.0f * diff / denom / J->n_total;
+            if (mode != ORC_FP32) g = orc_f16_round(g);
+            delta[c] = y[c] > 0.0f ? g : 0.0f;
+        }
+        int dout = NRC_OUT_PADDED;
+        for (int l = NRC_NUM_LAYERS - 1; l >= 0; --l) {
+            const float* inl = l == 0 ? enc : act[l - 1];
+            const int in_dim = kWIn[l];
+            double* gW = J->grad + kWOff[l];
+            for (int o = 0; o < dout; ++o) {
+                const double dd = (double)delta[o];
+                if (dd == 0.0) continue;
+                for (int k = 0; k < in_dim; ++k) gW[o * in_dim + k] += dd * (double)inl[k];
+            }
+            if (l == 0) break;
+            float* nd = delta == d[0] ? d[1] : d[0];
+            for (int k = 0; k < in_dim; ++k) {
+                double acc = 0.0;
+                for (int o = 0; o < dout; ++o) acc += (double)J->w[kWOff[l] + o * in_dim + k] * (double)delta[o];
+                const float v = inl[k] > 0.0f ? (float)acc : 0.0f;
+                nd[k] = mode == ORC_FP32 ? v : orc_f16_round(v);
+            }
+            delta = nd;
+            dout = in_dim;
+        }
+    }
+    return NULL;
+}
+
+double orc_wide_grad(int kind, const float* params, const float* queries, const float* targets, int64_t b,
+                     double n_total, float loss_scale, int mode, float* grad, int nthreads) {
+    for (int i = 0; i < NRC_WIDE_NUM_PARAMS; ++i) grad[i] = 0.0f;
+    if (b <= 0) return 0.0;
+    float* w = (float*)malloc(sizeof(float) * NRC_WIDE_NUM_PARAMS);
+    for (int i = 0; i < NRC_WIDE_NUM_PARAMS; ++i) w[i] = mode == ORC_FP32 ? params[i] : orc_f16_round(params[i]);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((int64_t)nthreads > b) nthreads = (int)b;
+    wide_grad_job* jobs = (wide_grad_job*)calloc((size_t)nthreads, sizeof(wide_grad_job));
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].w = w;
+        jobs[t].queries = queries;
+        jobs[t].targets = targets;
+        jobs[t].begin = b * t / nthreads;
+        jobs[t].end = b * (t + 1) / nthreads;
+        jobs[t].mode = mode;
+        jobs[t].kind = kind;
+        jobs[t].n_total = (float)n_total;
+        jobs[t].loss_scale = loss_scale;
+        jobs[t].grad = (double*)calloc(NRC_WIDE_NUM_PARAMS, sizeof(double));
+        if (nthreads > 1) pthread_create(&th[t], NULL, wide_grad_run, &jobs[t]);
+        else wide_grad_run(&jobs[t]);
+    }
+    if (nthreads > 1)
+        for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    double loss = 0.0;
+    for (int i = 0; i < NRC_WIDE_NUM_PARAMS; ++i) {
+        double acc = 0.0;
+        for (int t = 0; t < nthreads; ++t) acc += jobs[t].grad[i];
+        grad[i] = (float)acc;
+    }
+    for (int t = 0; t < nthreads; ++t) {
+        loss += jobs[t].loss;
+        free(jobs[t].grad);
+    }
+    free(jobs);
+    free(w);
+    return loss;
 }

@@ -71,6 +71,9 @@ def lib() -> ctypes.CDLL:
         L.orc_fp8_row_exponent.restype = ctypes.c_int
         L.orc_fp8_row_exponent.argtypes = [ctypes.c_float]
         L.orc_wide_quantize.argtypes = [vp, vp, vp]
+        L.orc_wide_grad.restype = ctypes.c_double
+        L.orc_wide_grad.argtypes = [ctypes.c_int, vp, vp, vp, i64, ctypes.c_double, ctypes.c_float, ctypes.c_int, vp,
+                                    ctypes.c_int]
         _lib = L
     return _lib
 
@@ -307,3 +310,14 @@ def wide_quantize(params):
     e = np.zeros((5, 128), np.int32)
     lib().orc_wide_quantize(_v(params), _v(q), _v(e))
     return q, e
+
+
+def wide_grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, threads=None, encoding=FREQUENCY):
+    """(loss-scaled gradient [77824], loss) of one width-128 minibatch"""
+    params, queries, targets = _f32(params), _f32(queries), _f32(targets)
+    b = queries.shape[0]
+    g = np.zeros(WIDE_NUM_PARAMS, np.float32)
+    loss = lib().orc_wide_grad(int(encoding), _v(params), _v(queries), _v(targets), b,
+                               float(n_total if n_total is not None else 3.0 * b), float(loss_scale), mode, _v(g),
+                               threads or default_threads())
+    return g, loss

@@ -122,3 +122,42 @@ def test_wide_quantize_values(orc):
         np.testing.assert_array_equal(Q[l] / s, e4m3_np(W[l] / s))
         assert (np.abs(Q[l] / s) <= 448).all()
     assert (e[4, 16:] == 0).all()
+
+
+def _np_loss_grad(params, q, t, loss_scale=128.0):
+    """float64 RelativeL2Luminance loss and loss-scaled gradient of the width-128 model (denominator constant)"""
+    import oracle_np
+
+    W = _unpack(params)
+    a = oracle_np.encode(q)
+    acts = [a]
+    for l in range(5):
+        a = np.maximum(a @ W[l].T, 0.0)
+        acts.append(a)
+    y = np.maximum(a @ W[5].T, 0.0)
+    b = len(q)
+    lum = 0.299 * y[:, 0] + 0.587 * y[:, 1] + 0.114 * y[:, 2]
+    den = lum * lum + 0.01
+    diff = y[:, :3] - t
+    loss = float(np.sum(diff * diff / den[:, None]) / (3 * b))
+    d = np.zeros_like(y)
+    d[:, :3] = loss_scale * 2 * diff / den[:, None] / (3 * b)
+    d *= y > 0
+    grads = [None] * 6
+    for l in range(5, -1, -1):
+        grads[l] = d.T @ acts[l]
+        if l:
+            d = (d @ W[l]) * (acts[l] > 0)
+    return loss, np.concatenate([g.reshape(-1) for g in grads])
+
+
+def test_wide_grad_matches_numpy(nrc, orc):
+    q, t = nrc.synthetic.cornell_batch(512, seed=31)
+    p = _params(7)
+    loss_ref, g_ref = _np_loss_grad(p, q, t)
+    g, loss = orc.wide_grad(p, q, t, mode=orc.FP32)
+    assert abs(loss - loss_ref) <= 1e-5 * abs(loss_ref)
+    assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-5
+    gm, lm = orc.wide_grad(p, q, t, mode=orc.MIXED)
+    assert abs(lm - loss_ref) <= 1e-2 * abs(loss_ref)
+    assert np.linalg.norm(gm - g_ref) / np.linalg.norm(g_ref) < 2e-2

@@ -53,6 +53,22 @@ def main() -> None:
             rows.append({"precision": name, "queries": n, "infer_us": round(us, 2), "Gq_per_s": round(n / us / 1e3, 3),
                          "tflops_alg": round(tf, 1), "frac_of_dense_peak": round(tf / peak, 4), "peak_tflops": peak})
             print(json.dumps(rows[-1]), flush=True)
+    # training step: 16,384 samples (fwd + loss + bwd + dW + Adam/EMA + image repacks)
+    tq, tt = nrc.synthetic.cornell_batch(4 * nrc.BATCH_SIZE, seed=2)
+    tq, tt = torch.from_numpy(tq).to(dev), torch.from_numpy(tt).to(dev)
+    for i in range(4):
+        net.train(tq[i * nrc.BATCH_SIZE:], tt[i * nrc.BATCH_SIZE:])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for i in range(40):
+        net.train(tq[(i % 4) * nrc.BATCH_SIZE:], tt[(i % 4) * nrc.BATCH_SIZE:])
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 40 * 1e3
+    train_flop = nrc.BATCH_SIZE * (3 * FLOP_Q - 2 * 66 * 128)  # fwd + dW + dX of layers 1..5
+    print(json.dumps({"train_step_us": round(us, 2), "train_tflops_alg": round(train_flop / (us * 1e-6) / 1e12, 1)}),
+          flush=True)
     net.destroy()
 
 
