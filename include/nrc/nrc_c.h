@@ -145,7 +145,7 @@ nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
 nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 
 /* ---- test / tuning entries ---- */
-/* Inference through a specific kernel variant (0..23, see nrc_kernels.hip) for in-process A/B timing;
+/* Inference through a specific kernel variant (0..25, see nrc_kernels.hip) for in-process A/B timing;
  * results are identical in meaning to nrc_infer_stream. */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
                                    hipStream_t stream);

@@ -792,6 +792,13 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
     }
+    if constexpr ((ABL & (64 | 128)) != 0) {
+        // stagger the waves that share a SIMD (wave slot from HW_ID) so that their encoders do not run in lockstep:
+        // ABL 64: slot & 3 quarter-tile steps, ABL 128: odd slots half a tile
+        const uint32_t slot = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4 /* hwreg(HW_REG_HW_ID, 0, 4) */);
+        const uint32_t steps = (ABL & 64) ? (slot & 3u) : 2u * (slot & 1u);
+        for (uint32_t i = 0; i < steps; ++i) __builtin_amdgcn_s_sleep(25);
+    }
     uint64_t ph[kInferPhases] = {};
     uint64_t tprev = 0;
     if constexpr ((ABL & 256) != 0) tprev = stamp_now();
@@ -2550,6 +2557,9 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 22: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 16>, 512, bpc[22], ntiles, queries, out, n, wf, s);
         // variant 22 + branch-free prefetch and buffer-store epilogue (exact vmcnt waits)
         case 23: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48>, 512, bpc[23], ntiles, queries, out, n, wf, s);
+        // variant 23 + staggered start of the waves sharing a SIMD (quarter-tile steps / odd slots half a tile)
+        case 24: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 64>, 512, bpc[24], ntiles, queries, out, n, wf, s);
+        case 25: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 128>, 512, bpc[25], ntiles, queries, out, n, wf, s);
         // v4: explicit layer-ahead weight prefetch
         case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
         case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
