@@ -412,7 +412,7 @@ int wide_enc(const nrc_net* net) { return net->encoding == NRC_ENCODING_FREQUENC
 
 hipError_t infer_wide(nrc_net* net, int prec, const float* in, float* out, uint32_t n, const float* thr, float* rgba,
                       uint32_t n_acc, int mode, float w, hipStream_t s) {
-    return launch_infer_wide(prec, wide_enc(net), in, out, n, prec ? net->wide_img8 : net->wide_img16, net->wide_scales,
+    return launch_infer_wide(prec, wide_enc(net), in, out, n, (prec & 15) ? net->wide_img8 : net->wide_img16, net->wide_scales,
                              thr, rgba, n_acc, mode, w, s);
 }
 
@@ -912,8 +912,11 @@ nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* i
     return guarded([&] {
         check_live(net);
         if (!net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "precision selection is for the width-128 network");
-        if (precision != NRC_PRECISION_F16 && precision != NRC_PRECISION_FP8)
+        // bits 4+: kernel variant (0 = production; 1 = 1024-thread blocks, Frequency only)
+        const int prec = precision & 15, variant = precision >> 4;
+        if ((prec != NRC_PRECISION_F16 && prec != NRC_PRECISION_FP8) || variant < 0 || variant > 1)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown precision");
+        if (variant && wide_enc(net) != 0) throw ApiError(NRC_ERR_UNSUPPORTED, "kernel variants are Frequency-only");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
         HIP_CHECK(infer_wide(net, precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, stream));

@@ -1181,11 +1181,13 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
 
 // ENC 0 = Frequency, 2 = FrequencySH (both 80-wide); EPI -1 plain, 0 / 2 fused accumulate_render_radiance.
 // Persistent waves, 2 per SIMD (one 512-thread block per CU: the f16 image takes 156 KiB of LDS).
-template <int ENC, int PREC, int EPI>
-__global__ __launch_bounds__(512, 2) void infer_wide_kernel(const float* __restrict__ q, float* __restrict__ out,
-                                                            int64_t n, const h8* __restrict__ img, InferEpilogue epi,
-                                                            const uint32_t* __restrict__ wscale) {
-    constexpr int THREADS = 512;
+// THREADS 1024 (debug variant 1): 4 waves per SIMD within 128 VGPRs.
+template <int ENC, int PREC, int EPI, int THREADS = 512>
+__global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(const float* __restrict__ q,
+                                                                            float* __restrict__ out, int64_t n,
+                                                                            const h8* __restrict__ img,
+                                                                            InferEpilogue epi,
+                                                                            const uint32_t* __restrict__ wscale) {
     constexpr int NH8 = (PREC == 0 ? kWideF16Bytes : kWide8Bytes) / 16;
     __shared__ __attribute__((aligned(16))) h8 lw[NH8];
     fp32_flush_output_denorms();  // the omod doubling-chain encoder
@@ -2483,6 +2485,219 @@ __global__ void wide_pack_train_kernel(const float* __restrict__ w, int enc, _Fl
 }
 
 // ------------------------------------------------------------------------------------------------
+// Ping-pong inference (variant 26). One wave owns two 32-query tiles A and B per iteration and runs them
+// through the network half a layer apart: while tile A's MFMAs of layer l issue, the VALU converts tile B's
+// layer l-1 accumulators (ReLU + f16 pack) into its next B operand, and vice versa. The next iteration's two tiles
+// are encoded in slices spread over the same phases, so every phase carries MFMAs and VALU of independent chains
+// and a wave can fill its own MFMA gaps (cdna_hip_programming.md T19); both tiles share each weight-fragment read,
+// which halves the LDS traffic per MFMA. Same arithmetic as infer_v2_body (bit-identical outputs).
+// ------------------------------------------------------------------------------------------------
+// encode_fast<CHAIN = true> split into slices: 0-2 triangle wave of position dim d, 3-5 OneBlob input i, 6 identity
+// and pads. FAST: the wave's OneBlob inputs satisfy -3 <= 4x < 7 (blob_many's in-range branch).
+template <int K, bool FAST>
+__device__ __forceinline__ void enc_slice(const QLane& Q, int h, uint32_t (&w)[20]) {
+    if constexpr (K < 3) {
+        const float hs = h ? 64.0f : 1.0f;
+        const float p = (K == 0 ? Q.p0 : K == 1 ? Q.p1 : Q.p2) * hs;
+        float g[6];
+        g[0] = fract2_abs(p);
+#pragma unroll
+        for (int k = 1; k < 6; ++k) g[k] = fract2(g[k - 1]);
+#pragma unroll
+        for (int k = 0; k < 6; k += 2) w[(K * 6 + k) >> 1] = pk2_abs(g[k] - 1.0f, g[k + 1] - 1.0f);
+    } else if constexpr (K < 6) {
+        const float x = K == 3 ? Q.b0 : K == 4 ? Q.b1 : Q.b2;
+        blob_fast<FAST>(x, w[9 + 2 * (K - 3)], w[10 + 2 * (K - 3)]);
+    } else {
+        w[15] = pk2(Q.i0, Q.i1);
+        w[16] = pk2(Q.i2, 1.0f);
+        w[17] = w[18] = w[19] = 0x3C003C00u;
+    }
+}
+
+__device__ __forceinline__ void enc_words_to_frags(const uint32_t (&w)[20], h8 (&x)[5]) {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+        u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
+        x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
+__device__ __forceinline__ bool blob_in_range(const QLane& Q) {
+    const float t0 = Q.b0 * 4.0f, t1 = Q.b1 * 4.0f, t2 = Q.b2 * 4.0f;
+    return t0 >= -3.0f && t0 < 7.0f && t1 >= -3.0f && t1 < 7.0f && t2 >= -3.0f && t2 < 7.0f;
+}
+
+// one layer's MFMAs for one tile: M-block 0's K chain, then M-block 1's
+template <int KK>
+__device__ __forceinline__ void pp_mfma(const h8 (&a)[2][KK], const h8 (&in)[KK], f16v (&c)[2]) {
+    c[0] = zero16();
+    c[1] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) c[0] = mfma(a[0][kk], in[kk], c[0]);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) c[1] = mfma(a[1][kk], in[kk], c[1]);
+}
+__device__ __forceinline__ void pp_relu(const f16v (&c)[2], h8 (&y)[4]) {
+    y[0] = relu_h8(c[0], 0);
+    y[1] = relu_h8(c[0], 8);
+    y[2] = relu_h8(c[1], 0);
+    y[3] = relu_h8(c[1], 8);
+}
+// interleave: per MFMA one group of NV VALU (LLVM SchedGroupMask: MFMA 0x8, VALU 0x2)
+template <int NM, int NV>
+__device__ __forceinline__ void pp_pattern() {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, NV, 0);
+    }
+}
+#define PP_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// One iteration: tiles (xA, xB) through the network into oA/oB; (QA, QB) encoded into (nA, nB) meanwhile.
+template <bool FAST, int SCHED>
+__device__ __forceinline__ void pp_iteration(lds_h8* lw_lane, const h8 (&xA)[5], const h8 (&xB)[5], const QLane& QA,
+                                             const QLane& QB, int h, h8 (&nA)[5], h8 (&nB)[5], f16v& oA, f16v& oB) {
+    uint32_t wA[20], wB[20];
+    f16v cA[2], cB[2];
+    h8 yA[4], yB[4];
+    lds_h8* wl = launder(lw_lane);
+    h8 a0[2][5];
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+        a0[0][kk] = wl[fwd_frag(0, 0, kk) * 64];
+        a0[1][kk] = wl[fwd_frag(0, 1, kk) * 64];
+    }
+    // P1: layer 0 (A) | encode: identity of both, OneBlob 2 and triangle dim 0 of A
+    PP_FENCE();
+    pp_mfma<5>(a0, xA, cA);
+    enc_slice<6, FAST>(QA, h, wA);
+    enc_slice<6, FAST>(QB, h, wB);
+    enc_slice<5, FAST>(QA, h, wA);
+    enc_slice<0, FAST>(QA, h, wA);
+    if constexpr (SCHED) pp_pattern<10, 5>();
+    PP_FENCE();
+    // P2: layer 0 (B) | ReLU(A), triangle dim 0 of B
+    pp_mfma<5>(a0, xB, cB);
+    pp_relu(cA, yA);
+    enc_slice<0, FAST>(QB, h, wB);
+    h8 a[2][4];
+    wl = launder(lw_lane);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        a[0][kk] = wl[fwd_frag(1, 0, kk) * 64];
+        a[1][kk] = wl[fwd_frag(1, 1, kk) * 64];
+    }
+    if constexpr (SCHED) pp_pattern<10, 5>();
+    PP_FENCE();
+#pragma unroll
+    for (int l = 1; l <= 4; ++l) {
+        // layer l (A) | ReLU(B of layer l-1), an encoder slice of A
+        pp_mfma<4>(a, yA, cA);
+        pp_relu(cB, yB);
+        if (l == 1) enc_slice<1, FAST>(QA, h, wA);
+        if (l == 2) enc_slice<2, FAST>(QA, h, wA);
+        if (l == 3) enc_slice<3, FAST>(QA, h, wA);
+        if (l == 4) enc_slice<4, FAST>(QA, h, wA);
+        if constexpr (SCHED) pp_pattern<8, 6>();
+        PP_FENCE();
+        // layer l (B) | ReLU(A of layer l), an encoder slice of B; next layer's fragments
+        pp_mfma<4>(a, yB, cB);
+        pp_relu(cA, yA);
+        if (l == 1) enc_slice<1, FAST>(QB, h, wB);
+        if (l == 2) enc_slice<2, FAST>(QB, h, wB);
+        if (l == 3) enc_slice<3, FAST>(QB, h, wB);
+        if (l == 4) enc_slice<4, FAST>(QB, h, wB);
+        wl = launder(lw_lane);
+        if (l < 4) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                a[0][kk] = wl[fwd_frag(l + 1, 0, kk) * 64];
+                a[1][kk] = wl[fwd_frag(l + 1, 1, kk) * 64];
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) a[0][kk] = wl[fwd_frag(5, 0, kk) * 64];
+        }
+        if constexpr (SCHED) pp_pattern<8, 6>();
+        PP_FENCE();
+    }
+    // output layer (A) | ReLU(B of layer 4), OneBlob 2 of B
+    oA = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) oA = mfma(a[0][kk], yA[kk], oA);
+    pp_relu(cB, yB);
+    enc_slice<5, FAST>(QB, h, wB);
+    if constexpr (SCHED) pp_pattern<4, 10>();
+    PP_FENCE();
+    oB = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) oB = mfma(a[0][kk], yB[kk], oB);
+    enc_words_to_frags(wA, nA);
+    enc_words_to_frags(wB, nB);
+    PP_FENCE();
+}
+
+// radiance of tile t (32 rows from s0) leaves through a raw buffer store whose descriptor covers its valid rows
+__device__ __forceinline__ void pp_store(float* __restrict__ out, int64_t n, int64_t s0, int r, int h, const f16v& o) {
+    const float L0 = (float)(_Float16)fmaxf(o[0], 0.0f);
+    const float L1 = (float)(_Float16)fmaxf(o[1], 0.0f);
+    const float L2 = (float)(_Float16)fmaxf(o[2], 0.0f);
+    const u3 ov = {__builtin_bit_cast(uint32_t, L0), __builtin_bit_cast(uint32_t, L1), __builtin_bit_cast(uint32_t, L2)};
+    __builtin_amdgcn_raw_buffer_store_b96(ov, buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12),
+                                          h == 0 ? r * 12 : kBufferOff, 0, 0);
+}
+
+template <int THREADS, int SCHED>
+__global__ __launch_bounds__(THREADS, 2) void infer_pp_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                              int64_t n, const h8* __restrict__ wf) {
+    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    fp32_flush_output_denorms();
+    copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    const int64_t npairs = (((n + 31) >> 5) + 1) >> 1;
+    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
+    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (g >= npairs) return;
+    const int64_t last = n - 1;
+    auto qrow = [&](int64_t pair, int t) { return min((pair * 2 + t) * 32 + r, last); };
+    lds_h8* lw_lane = (lds_h8*)(lw + lane);
+
+    // prologue: encode the first pair, prefetch the second
+    h8 xA[5], xB[5];
+    {
+        const QLane QA = load_q(q, qrow(g, 0), h), QB = load_q(q, qrow(g, 1), h);
+        encode_fast<true>(QA, h, xA);
+        encode_fast<true>(QB, h, xB);
+    }
+    QLane QA = load_q(q, qrow(g + wstride, 0), h), QB = load_q(q, qrow(g + wstride, 1), h);
+    __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);  // see variant 23
+    for (; g < npairs; g += wstride) {
+        const QLane NA = load_q(q, qrow(g + 2 * wstride, 0), h), NB = load_q(q, qrow(g + 2 * wstride, 1), h);
+        h8 nA[5], nB[5];
+        f16v oA, oB;
+        if (__all(blob_in_range(QA) && blob_in_range(QB)))
+            pp_iteration<true, SCHED>(lw_lane, xA, xB, QA, QB, h, nA, nB, oA, oB);
+        else {
+            asm volatile("; OneBlob wrap path");
+            pp_iteration<false, SCHED>(lw_lane, xA, xB, QA, QB, h, nA, nB, oA, oB);
+        }
+        pp_store(out, n, g * 64, r, h, oA);
+        pp_store(out, n, g * 64 + 32, r, h, oB);
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) {
+            xA[kk] = nA[kk];
+            xB[kk] = nB[kk];
+        }
+        QA = NA;
+        QB = NB;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
 static int num_cus() {
@@ -2560,6 +2775,10 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         // variant 23 + staggered start of the waves sharing a SIMD (quarter-tile steps / odd slots half a tile)
         case 24: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 64>, 512, bpc[24], ntiles, queries, out, n, wf, s);
         case 25: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 128>, 512, bpc[25], ntiles, queries, out, n, wf, s);
+        // ping-pong: two tiles per wave half a layer apart, encoder slices spread over the phases
+        case 26: return launch_persistent_infer(infer_pp_kernel<512, 0>, 512, bpc[26], pairs, queries, out, n, wf, s);
+        case 27: return launch_persistent_infer(infer_pp_kernel<512, 1>, 512, bpc[27], pairs, queries, out, n, wf, s);
+        case 28: return launch_persistent_infer(infer_pp_kernel<256, 1>, 256, bpc[28], pairs, queries, out, n, wf, s);
         // v4: explicit layer-ahead weight prefetch
         case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
         case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
@@ -2632,9 +2851,21 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
                              const uint32_t* scales, const float* thr, float* rgba, int64_t n_acc, int mode, float w,
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    if ((prec != 0 && prec != 1) || (enc != 0 && enc != 2) || (mode != -1 && mode != 0 && mode != 2))
+    const int variant = prec >> 4;  // debug: kernel variant (nrc_debug_infer_precision)
+    prec &= 15;
+    if ((prec != 0 && prec != 1) || (enc != 0 && enc != 2) || (mode != -1 && mode != 0 && mode != 2) || variant > 1)
         return hipErrorInvalidValue;
     const int64_t ntiles = (n + 31) / 32;
+    if (variant == 1) {
+        if (enc != 0 || mode != -1) return hipErrorInvalidValue;
+        static int bv[2] = {};
+        const InferEpilogue e{};
+        if (prec == 0)
+            return launch_persistent_infer(infer_wide_kernel<0, 0, -1, 1024>, 1024, bv[0], ntiles, queries, out, n,
+                                           reinterpret_cast<const _Float16*>(img), s, e, scales);
+        return launch_persistent_infer(infer_wide_kernel<0, 1, -1, 1024>, 1024, bv[1], ntiles, queries, out, n,
+                                       reinterpret_cast<const _Float16*>(img), s, e, scales);
+    }
     static int bpc[2][2][3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     const _Float16* im = reinterpret_cast<const _Float16*>(img);

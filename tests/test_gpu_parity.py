@@ -86,7 +86,7 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every production-eligible kernel variant at sizes
     that exercise partial tiles / single blocks."""

@@ -268,3 +268,20 @@ def test_wide_training_learns_and_fp8_on_trained_weights(nrc, orc, dev):
         assert r <= 0.1
     finally:
         net.destroy()
+
+
+@pytest.mark.parametrize("n", [1, 1000, 4097, 70001])
+def test_wide_kernel_variant_bit_identical(nrc, dev, n):
+    """The 1024-thread-block debug variant (4 waves per SIMD) computes exactly what the production kernel does."""
+    import torch
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Frequency,
+             config=nrc.default_config(nrc.InputEncoding.Frequency, width=128))
+    try:
+        q = nrc.synthetic.cornell_queries(n, seed=n)
+        for prec in (nrc._lib.PRECISION_F16, nrc._lib.PRECISION_FP8):
+            base = run(net, nrc, dev, q, prec)
+            var = run(net, nrc, dev, q, prec | (1 << 4))
+            assert np.array_equal(base, var), f"precision {prec}: variant differs"
+    finally:
+        net.destroy()
