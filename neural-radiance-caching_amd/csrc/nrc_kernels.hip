@@ -1724,23 +1724,58 @@ __host__ __device__ constexpr int w_offset() {
                                 : NRC_W5_OFFSET);
 }
 
+// Lane offsets of the transposed reads. tr_frag(img, fb, kk) reads img + img_off(s0, c) and img + img_off(s0 + 4, c)
+// with s0 = 16 kk + (lane part): the k step only adds 16 rows = 2048 bytes (the swizzle uses s mod 8), and the x_hi
+// image's rows are 32 bytes, so every read of a layer step is a per-lane base plus an immediate offset. Computed once
+// per kernel and hidden from the optimiser, which otherwise rebuilds each address with 3-4 VALU (v_or does not fold
+// into the ds_read offset field).
+struct TrOffs {
+    int a[2][2];  // feature block fb, read 0/1
+    int x[2];     // x_hi image, read 0/1
+};
+__device__ __forceinline__ TrOffs make_tr_offs(int lane) {
+    const int g = lane >> 4, idx = lane & 15, q = idx >> 2, p = idx & 3;
+    const int s0 = 8 * (g >> 1) + q;
+    TrOffs o;
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb) {
+        const int c = 32 * fb + 16 * (g & 1) + 4 * p;
+        o.a[fb][0] = img_off(s0, c);
+        o.a[fb][1] = img_off(s0 + 4, c);
+        asm volatile("" : "+v"(o.a[fb][0]), "+v"(o.a[fb][1]));
+    }
+    o.x[0] = s0 * 32 + 8 * p;
+    o.x[1] = (s0 + 4) * 32 + 8 * p;
+    asm volatile("" : "+v"(o.x[0]), "+v"(o.x[1]));
+    return o;
+}
+__device__ __forceinline__ h8 tr_frag_o(const char* img, int o0, int o1, int kk) {
+    return cat(tr_read(img + o0 + 2048 * kk), tr_read(img + o1 + 2048 * kk));
+}
+
 // dW output block (mb, nb) of layer L: A = delta image (features = output rows), B = activation image.
 // Split into the MFMA chain and the slab store so that a layer step can issue the delta chain between them: the
 // wave issues in order, and a store placed right after the dW MFMAs would hold it until their results are out.
+// All 32 transposed reads are issued before the first MFMA, so the chain waits on them once instead of once per k step.
 template <int L, int ENC = 0>
 __device__ __forceinline__ f16v dw_block_mfma(const char* img_d, const char* img_a, const char* img_xh, int mb, int nb,
-                                              int lane) {
-    f16v acc = zero16();
+                                              int lane, const TrOffs& to) {
     const bool zero_a = (L == 5) && (lane & 16);  // rows 16..31 of the 16-row output delta do not exist
+    const bool xhi = ENC != 1 && L == 0 && nb == 2;
+    const int da0 = mb ? to.a[1][0] : to.a[0][0], da1 = mb ? to.a[1][1] : to.a[0][1];
+    const int db0 = nb ? to.a[1][0] : to.a[0][0], db1 = nb ? to.a[1][1] : to.a[0][1];
+    h8 A[8], B[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-        h8 A = tr_frag(img_d, mb, kk, lane);
-        if (zero_a) A = h8{};
-        h8 B;
-        if (ENC != 1 && L == 0 && nb == 2) B = tr_frag_xhi(img_xh, kk, lane);
-        else B = tr_frag(img_a, nb, kk, lane);
-        acc = mfma(A, B, acc);
+        A[kk] = tr_frag_o(img_d, da0, da1, kk);
+        if (L == 0 && ENC != 1 && xhi)
+            B[kk] = cat(tr_read(img_xh + to.x[0] + 512 * kk), tr_read(img_xh + to.x[1] + 512 * kk));
+        else
+            B[kk] = tr_frag_o(img_a, db0, db1, kk);
     }
+    f16v acc = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) acc = mfma(zero_a ? h8{} : A[kk], B[kk], acc);
     return acc;
 }
 
@@ -1764,14 +1799,14 @@ template <int L, int ENC = 0>
 struct DwAcc {
     f16v a0, a1;
     __device__ __forceinline__ void mfma_all(const char* img_d, const char* img_a, const char* img_xh, int wave,
-                                             int lane) {
+                                             int lane, const TrOffs& to) {
         if (L == 5) {
-            if (wave < 2) a0 = dw_block_mfma<5, ENC>(img_d, img_a, img_xh, 0, wave, lane);
+            if (wave < 2) a0 = dw_block_mfma<5, ENC>(img_d, img_a, img_xh, 0, wave, lane, to);
         } else if (L == 0 && ENC != 1) {
-            a0 = dw_block_mfma<0, ENC>(img_d, img_a, img_xh, wave / 3, wave % 3, lane);
-            if (wave < 2) a1 = dw_block_mfma<0, ENC>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane);
+            a0 = dw_block_mfma<0, ENC>(img_d, img_a, img_xh, wave / 3, wave % 3, lane, to);
+            if (wave < 2) a1 = dw_block_mfma<0, ENC>(img_d, img_a, img_xh, (wave + 4) / 3, (wave + 4) % 3, lane, to);
         } else {
-            a0 = dw_block_mfma<L, ENC>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane);
+            a0 = dw_block_mfma<L, ENC>(img_d, img_a, img_xh, wave >> 1, wave & 1, lane, to);
         }
     }
     __device__ __forceinline__ void store_all(int wave, int lane, float* __restrict__ slab) const {
@@ -1786,13 +1821,6 @@ struct DwAcc {
     }
 };
 
-template <int L, int ENC = 0>
-__device__ __forceinline__ void dw_layer(const char* img_d, const char* img_a, const char* img_xh, int wave, int lane,
-                                         float* __restrict__ slab) {
-    DwAcc<L, ENC> d;
-    d.mfma_all(img_d, img_a, img_xh, wave, lane);
-    d.store_all(wave, lane, slab);
-}
 
 // Backward ReLU on packed halves: d = f16(acc) where the forward activation a > 0, else +0. One dword (two
 // features) costs v_cvt_pk_f16_f32 + v_pk_max_i16 + v_pk_min_i16 + v_pk_mul_lo_u16: the activation bits as i16
@@ -1836,6 +1864,22 @@ __device__ __forceinline__ void bwd_chain(W wfrag, const h8 (&d)[4], const h8 (&
     }
     mask_pack_pk(c0, a[0], a[1], dn[0], dn[1]);
     mask_pack_pk(c1, a[2], a[3], dn[2], dn[3]);
+}
+
+// The same with the layer's backward fragments read ahead (before the step's dW operand reads), so the chain's
+// MFMAs do not each wait on their own ds_read_b128.
+template <int L, class W>
+__device__ __forceinline__ void load_bwd(W wfrag, h8 (&w)[2][4]) {
+    constexpr int KK = (L == 5) ? 1 : 4;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+        w[0][kk] = wfrag(bwd_frag(L, 0, kk));
+        w[1][kk] = wfrag(bwd_frag(L, 1, kk));
+    }
+}
+template <int L>
+__device__ __forceinline__ void bwd_chain_pre(const h8 (&w)[2][4], const h8 (&d)[4], const h8 (&a)[4], h8 (&dn)[4]) {
+    bwd_chain<L>([&](int i) { return i < 2 ? w[i][0] : w[((i - 2) >> 2) & 1][(i - 2) & 3]; }, d, a, dn);
 }
 
 // grid_grad[e] += (half2){a, b}: each product rounded to f16, accumulated in f16 at the memory side
@@ -1883,6 +1927,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, r = lane & 31;
     const int sl = wave * 32 + r;
+    const TrOffs to = make_tr_offs(lane);
     const int64_t s = (int64_t)blockIdx.x * kTrainSamplesPerBlock + sl;
     const bool valid = s < b;
     const int64_t sc = valid ? s : b - 1;
@@ -1918,6 +1963,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 #pragma unroll
     for (int kk = 0; kk < KK0; ++kk) asm volatile("" : "+v"(x[kk]));
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int i = threadIdx.x + k * 256;
@@ -1994,8 +2040,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     h8 d4[4], d3[4], d2[4], d1[4], d0[4];
     {
         DwAcc<5, ENC> dw;
-        dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
-        bwd_chain<5>(wfrag, g, a[4], d4);
+        h8 wbf[2][4];
+        load_bwd<5>(wfrag, wbf);
+        dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane, to);
+        bwd_chain_pre<5>(wbf, g, a[4], d4);
         write_rows64(img_d[0], sl, h, d4);
         write_rows64(img_a[0], sl, h, a[3]);
         dw.store_all(wave, lane, slab);
@@ -2004,8 +2052,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     stamp();
     {
         DwAcc<4, ENC> dw;
-        dw.mfma_all(img_d[0], img_a[0], img_xh, wave, lane);
-        bwd_chain<4>(wfrag, d4, a[3], d3);
+        h8 wbf[2][4];
+        load_bwd<4>(wfrag, wbf);
+        dw.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
+        bwd_chain_pre<4>(wbf, d4, a[3], d3);
         write_rows64(img_d[1], sl, h, d3);
         write_rows64(img_a[1], sl, h, a[2]);
         dw.store_all(wave, lane, slab);
@@ -2014,8 +2064,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     stamp();
     {
         DwAcc<3, ENC> dw;
-        dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
-        bwd_chain<3>(wfrag, d3, a[2], d2);
+        h8 wbf[2][4];
+        load_bwd<3>(wfrag, wbf);
+        dw.mfma_all(img_d[1], img_a[1], img_xh, wave, lane, to);
+        bwd_chain_pre<3>(wbf, d3, a[2], d2);
         write_rows64(img_d[0], sl, h, d2);
         write_rows64(img_a[0], sl, h, a[1]);
         dw.store_all(wave, lane, slab);
@@ -2024,8 +2076,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     stamp();
     {
         DwAcc<2, ENC> dw;
-        dw.mfma_all(img_d[0], img_a[0], img_xh, wave, lane);
-        bwd_chain<2>(wfrag, d2, a[1], d1);
+        h8 wbf[2][4];
+        load_bwd<2>(wfrag, wbf);
+        dw.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
+        bwd_chain_pre<2>(wbf, d2, a[1], d1);
         write_rows64(img_d[1], sl, h, d1);
         write_rows64(img_a[1], sl, h, a[0]);
         dw.store_all(wave, lane, slab);
@@ -2033,8 +2087,10 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     lds_barrier();
     stamp();
     DwAcc<1, ENC> dw1;
-    dw1.mfma_all(img_d[1], img_a[1], img_xh, wave, lane);
-    bwd_chain<1>(wfrag, d1, a[0], d0);
+    h8 wbf[2][4];
+    load_bwd<1>(wfrag, wbf);
+    dw1.mfma_all(img_d[1], img_a[1], img_xh, wave, lane, to);
+    bwd_chain_pre<1>(wbf, d1, a[0], d0);
     // layer-0 operands: delta_0 and the encoded input x (K order; x_lo -> img_a[0], x_hi -> img_xh)
     write_rows64(img_d[0], sl, h, d0);
 #pragma unroll
@@ -2082,7 +2138,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
             tkey[i] = 0xFFFFFFFFu;
             tval[2 * i] = tval[2 * i + 1] = 0.0f;
         }
-        dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+        {
+            DwAcc<0, ENC> dw0;
+            dw0.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
+            dw0.store_all(wave, lane, slab);
+        }
         lds_barrier();
         if (valid && h == 0) {
 #pragma unroll
@@ -2117,7 +2177,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
             grid_atomic(grid_grad, e, tval[2 * i], tval[2 * i + 1]);
         }
     } else {
-        dw_layer<0, ENC>(img_d[0], img_a[0], img_xh, wave, lane, slab);
+        {
+            DwAcc<0, ENC> dw0;
+            dw0.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
+            dw0.store_all(wave, lane, slab);
+        }
     }
     stamp();
 }
