@@ -2230,6 +2230,37 @@ __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const
     if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
 }
 
+// adam_pack_one (mode kReduceFused) split into its loads and the rest, same float operations
+struct AdamIn {
+    float w, m, v, ema;
+    int fp, bp;
+};
+__device__ __forceinline__ AdamIn adam_load(int p, const ModelBuffers& mb) {
+    return AdamIn{mb.params[p], mb.m[p], mb.v[p], mb.ema[p], mb.fwd_pos[p], mb.bwd_pos[p]};
+}
+__device__ __forceinline__ void adam_pack_pre(int p, float gsum, const AdamIn& in, const ModelBuffers& mb,
+                                              const OptimArgs& oa, float lr_t, float ema_debias) {
+#pragma clang fp contract(off)
+    float gradient = gsum / oa.loss_scale;
+    float w = in.w;
+    gradient += oa.l2_reg * w;
+    const float gsq = gradient * gradient;
+    const float m1 = oa.beta1 * in.m + (1.0f - oa.beta1) * gradient;
+    const float v1 = oa.beta2 * in.v + (1.0f - oa.beta2) * gsq;
+    mb.m[p] = m1;
+    mb.v[p] = v1;
+    const float eff = lr_t / (sqrtf(v1) + oa.eps);
+    w = w - eff * m1;
+    mb.params[p] = w;
+    const float e = in.ema * oa.ema_decay + w * (1.0f - oa.ema_decay);
+    mb.ema[p] = e;
+    const float inf = e / ema_debias;
+    mb.infer[p] = inf;
+    mb.wf_train[in.fp] = (_Float16)w;
+    mb.wf_infer[in.fp] = (_Float16)inf;
+    if (in.bp >= 0) mb.wb_train[in.bp] = (_Float16)w;
+}
+
 // The per-slab loss partials are summed by wave 0 of block 0: a strided per-lane sum and a fixed xor
 // butterfly (one load latency instead of a serial chain of nslabs loads).
 __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
@@ -2256,6 +2287,14 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         }
     }
     if (mode == kReduceFused || mode == kReduceOnly) {
+        // the combining threads fetch their parameter's optimizer state before the slab loads, so Adam does not
+        // wait for a second round trip after the reduction
+        int pp = -1;
+        AdamIn ain{};
+        if (threadIdx.x < kRedParams * kRedVec) {
+            pp = mb.slab_param[blockIdx.x * kRedParams * kRedVec + threadIdx.x];
+            if (mode == kReduceFused && pp >= 0) ain = adam_load(pp, mb);
+        }
         f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         int i = grp;
         for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
@@ -2283,13 +2322,13 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 #pragma unroll
         for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][lp][comp] + part[2 * u + 1][lp][comp];
         const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
-        const int p = mb.slab_param[blockIdx.x * kRedParams * kRedVec + threadIdx.x];
+        const int p = pp;
         if (p < 0) return;  // padding position (x_hi block lanes past the 80 inputs)
         if (mode == kReduceOnly) {
             grad_io[p] = g1;
             return;
         }
-        adam_pack_one(mode, p, g1, mb, oa, lr_t, ema_debias);
+        adam_pack_pre(p, g1, ain, mb, oa, lr_t, ema_debias);
         return;
     }
     if (threadIdx.x >= kRedParams * kRedVec) return;
