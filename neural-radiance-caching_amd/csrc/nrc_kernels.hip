@@ -1954,6 +1954,11 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         if (i < NBF * 64) vb[k] = wb[i];
     }
     auto wfrag = [&](int i) { return lwb[i * 64 + lane]; };
+    if constexpr (STAMP) {  // diagnostic: wait for the sample loads here, so the encoder is timed on its own
+        asm volatile("" ::"v"(Q.p0), "v"(Q.p1), "v"(Q.p2), "v"(Q.b0), "v"(Q.b1), "v"(Q.b2), "v"(Q.i0), "v"(Q.i1),
+                     "v"(Q.i2));
+        stamp();
+    }
     h8 x[KK0];
     if constexpr (ENC == 1) encode_hash(Q, h, grid, x);
     else if constexpr (ENC == 2) encode_sh(Q, h, x);

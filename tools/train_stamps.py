@@ -9,7 +9,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import nrc_loader  # noqa: E402
 
-PHASES = ["start", "encode", "weights", "forward", "loss+img5", "L5", "L4", "L3", "L2", "L1", "L0"]
+PHASES = ["start", "sample loads", "encode", "weights", "forward", "loss+img5", "L5", "L4", "L3", "L2", "L1", "L0"]
 
 
 def main():
