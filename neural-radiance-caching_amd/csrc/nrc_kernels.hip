@@ -1262,42 +1262,41 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
     }
 }
 
-// Per-row E8M0 exponents of W1..W5 (oracle orc_fp8_row_exponent): one thread per (layer, row).
-__global__ void wide_row_exp_kernel(const float* __restrict__ w, int32_t* __restrict__ exps,
-                                    uint32_t* __restrict__ scales) {
-    const int t = threadIdx.x;  // one block of 640 threads
+// Per-row E8M0 exponents of W1..W5 (oracle orc_fp8_row_exponent): one wave per (layer, row), 2 weights per lane and a
+// max butterfly (a single-block version with one thread walking each 128-weight row took 18 us).
+__global__ __launch_bounds__(256) void wide_row_exp_kernel(const float* __restrict__ w, int32_t* __restrict__ exps) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // t = (layer - 1) * 128 + row
+    if (t >= 5 * 128) return;
     const int layer = 1 + t / 128, row = t % 128;
+    const bool live = layer < 5 || row < NRC_OUT_PADDED;
+    const float* wr = w + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;  // W5 rows follow W4's
+    float amax = live ? fmaxf(fabsf(wr[lane]), fabsf(wr[lane + 64])) : 0.0f;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
     int e = 0;
-    if (layer < 5 || row < NRC_OUT_PADDED) {
-        const float* wr = w + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;  // W5 rows follow W4's
-        float amax = 0.0f;
-        for (int k = 0; k < 128; ++k) amax = fmaxf(amax, fabsf(wr[k]));
-        if (amax > 0.0f) {
-            int E = 0;
-            const float M = frexpf(amax, &E);
-            e = M <= 0.875f ? E - 9 : E - 8;
-            e = max(-127, min(127, e));
-        }
+    if (amax > 0.0f) {
+        int E = 0;
+        const float M = frexpf(amax, &E);
+        e = M <= 0.875f ? E - 9 : E - 8;
+        e = max(-127, min(127, e));
     }
-    __shared__ int se[5 * 128];
-    exps[t] = e;
-    se[t] = e;
-    __syncthreads();
-    // scale words: lane r of layer l holds bytes e(l, 32 mb + r) + 127, mb = 0..3
-    if (t < 5 * 32) {
-        const int l = t / 32, rr = t % 32;
-        uint32_t word = 0;
-        for (int mb = 0; mb < 4; ++mb) word |= (uint32_t)(se[l * 128 + 32 * mb + rr] + 127) << (8 * mb);
-        scales[t] = word;
-    }
+    if (lane == 0) exps[t] = e;
 }
 
 // f16 image (img16, 156 fragments) and FP8 image (img8: 20 f16 layer-0 fragments + 34 fp8 fragments) from the f32
 // inference weights; one thread per 16-byte unit of either image.
+// Threads 0..159 also assemble the per-layer scale words (lane r of layer l holds bytes e(l, 32 mb + r) + 127).
 __global__ void wide_pack_kernel(const float* __restrict__ w, int enc, const int32_t* __restrict__ exps,
-                                 _Float16* __restrict__ img16, uint8_t* __restrict__ img8) {
+                                 _Float16* __restrict__ img16, uint8_t* __restrict__ img8,
+                                 uint32_t* __restrict__ scales) {
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     constexpr int U16 = kWideF16Bytes / 16, U8 = kWide8Frags * 128;
+    if (u < 5 * 32) {
+        const int l = u / 32, rr = u % 32;
+        uint32_t word = 0;
+        for (int mb = 0; mb < 4; ++mb) word |= (uint32_t)(exps[l * 128 + 32 * mb + rr] + 127) << (8 * mb);
+        scales[u] = word;
+    }
     if (u < U16) {
         const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
         int layer, mb, kk;
@@ -2949,9 +2948,9 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
 
 hipError_t launch_wide_pack(const float* w, int enc, _Float16* img16, uint8_t* img8, uint32_t* scales, int32_t* exps,
                             hipStream_t s) {
-    hipLaunchKernelGGL(wide_row_exp_kernel, dim3(1), dim3(5 * 128), 0, s, w, exps, scales);
+    hipLaunchKernelGGL(wide_row_exp_kernel, dim3(5 * 128 / 4), dim3(256), 0, s, w, exps);
     constexpr int units = kWideF16Bytes / 16 + kWide8Frags * 128;
-    hipLaunchKernelGGL(wide_pack_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w, enc, exps, img16, img8);
+    hipLaunchKernelGGL(wide_pack_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w, enc, exps, img16, img8, scales);
     return hipGetLastError();
 }
 
