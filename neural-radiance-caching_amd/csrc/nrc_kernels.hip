@@ -2492,8 +2492,36 @@ __global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict
     const int64_t k0 = (int64_t)chunk * kWideChunk, k1 = min<int64_t>(bpad, k0 + kWideChunk);
     f16v acc[2] = {zero16(), zero16()};
     const h8 z = {};
-    int u = 0;
-    for (int64_t k = k0; k < k1; k += 16, u ^= 1) {
+    // batches of 8 k steps with the next batch's 16 loads in flight during this batch's MFMAs (the operands come
+    // from L2: a load -> MFMA chain one k step at a time waited a full L2 round trip per step)
+    constexpr int KB = 8;
+    int64_t k = k0;
+    const int64_t kfull = k0 + (k1 - k0) / (16 * KB) * (16 * KB);
+    if (k < kfull) {
+        h8 A[KB], B[KB];
+#pragma unroll
+        for (int j = 0; j < KB; ++j) {
+            A[j] = oa ? pa[(k >> 3) + 2 * j] : z;
+            B[j] = ib ? pb[(k >> 3) + 2 * j] : z;
+        }
+        for (; k < kfull; k += 16 * KB) {
+            h8 An[KB], Bn[KB];
+            const int64_t kn = k + 16 * KB < kfull ? k + 16 * KB : k;  // clamped: the last batch re-reads itself
+#pragma unroll
+            for (int j = 0; j < KB; ++j) {
+                An[j] = oa ? pa[(kn >> 3) + 2 * j] : z;
+                Bn[j] = ib ? pb[(kn >> 3) + 2 * j] : z;
+            }
+#pragma unroll
+            for (int j = 0; j < KB; ++j) acc[j & 1] = mfma(A[j], B[j], acc[j & 1]);
+#pragma unroll
+            for (int j = 0; j < KB; ++j) {
+                A[j] = An[j];
+                B[j] = Bn[j];
+            }
+        }
+    }
+    for (int u = 0; k < k1; k += 16, u ^= 1) {
         const h8 av = oa ? pa[k >> 3] : z;
         const h8 bv = ib ? pb[k >> 3] : z;
         acc[u] = mfma(av, bv, acc[u]);
@@ -2534,7 +2562,15 @@ __global__ __launch_bounds__(256) void wide_adam_kernel(int mode, const float* _
     if (mode == kApplyOnly) {
         gsum = grad_io[p];
     } else {
-        for (int c = 0; c < nchunks; ++c) gsum += slabs[(int64_t)c * NRC_WIDE_NUM_PARAMS + p];
+        // 16 chunk loads in flight, summed in chunk order (adding +0 for absent chunks leaves the sum unchanged)
+        for (int c0 = 0; c0 < nchunks; c0 += 16) {
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                v[j] = c0 + j < nchunks ? slabs[(int64_t)(c0 + j) * NRC_WIDE_NUM_PARAMS + p] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) gsum += v[j];
+        }
         if (mode == kReduceOnly) {
             grad_io[p] = gsum;
             return;
