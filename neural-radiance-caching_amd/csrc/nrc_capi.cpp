@@ -238,6 +238,8 @@ struct nrc_net {
     _Float16* grid_grad = nullptr;  // f16 [n_grid]: half2 per entry, packed-half atomics (tcnn)
     uint32_t* grid_steps = nullptr;
     _Float16 *table_train = nullptr, *table_infer = nullptr;
+    HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
+    int scatter_blocks = 0;
 
     // width-128 network (BASELINE configs[4]): inference images (f16, FP8 + row scales), training images (f16
     // forward / backward from the master weights) and the training workspace
@@ -263,6 +265,9 @@ struct nrc_net {
         f(fwd_pos); f(bwd_pos); f(slab_param);
         f(slabs); f(loss_partials); f(loss_dev);
         f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
+        f(scatter.pos); f(scatter.dy);
+        scatter = HashScatter{};
+        scatter_blocks = 0;
         f(wide_img16); f(wide_img8); f(wide_scales); f(wide_exps);
         f(wide_fwd_train); f(wide_bwd_train); f(wide_ws_in); f(wide_ws_d); f(wide_slabs); f(wide_loss_partials);
         wide_img16 = wide_img8 = nullptr;
@@ -324,6 +329,20 @@ struct nrc_net {
         HIP_CHECK(hipMalloc(&wide_slabs, sizeof(float) * NRC_WIDE_NUM_PARAMS * (size_t)wide_chunks(bpad)));
         HIP_CHECK(hipMalloc(&wide_loss_partials, sizeof(float) * (size_t)(bpad / 32)));
         wide_ws_bpad = bpad;
+    }
+    const HashScatter* ensure_scatter(int blocks) {
+        if (blocks > scatter_blocks) {
+            if (scatter.pos) HIP_CHECK(hipFree(scatter.pos));
+            if (scatter.dy) HIP_CHECK(hipFree(scatter.dy));
+            scatter = HashScatter{};
+            scatter_blocks = 0;
+            const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
+            HIP_CHECK(hipMalloc(&scatter.pos, sizeof(float4) * (size_t)bcap));
+            HIP_CHECK(hipMalloc(&scatter.dy, sizeof(uint32_t) * NRC_HASH_LEVELS * (size_t)bcap));
+            scatter.bcap = bcap;
+            scatter_blocks = blocks;
+        }
+        return &scatter;
     }
     void ensure_slabs(int blocks) {
         if (blocks <= slab_blocks) return;
@@ -393,7 +412,8 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     net->ensure_slabs(blocks);
     if (net->hash())
         HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                    net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream));
+                                    net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
+                                    net->ensure_scatter(blocks)));
     else
         HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                        net->slabs, net->loss_partials, net->stream, net->encoding));
@@ -758,7 +778,7 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
             // f32 into the caller's buffer after the MLP part; the export zeroes the f16 buffer again
             HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
                                         net->wb_train, net->table_train, net->grid_grad, net->slabs, net->loss_partials,
-                                        net->stream));
+                                        net->stream, net->ensure_scatter(blocks)));
             HIP_CHECK(launch_grid_grad_export(net->grid_grad, grad_d + net->n_mlp, net->n_grid, net->stream));
         } else {
             HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,

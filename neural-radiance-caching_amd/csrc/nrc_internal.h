@@ -193,12 +193,19 @@ struct GridBuffers {
     int n;
 };
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
+// Hash training workspace: per sample its position and the 16 levels' (dy0, dy1) f16 pairs ([level][sample]),
+// written by the training kernel and consumed by grid_scatter_kernel.
+struct HashScatter {
+    float4* pos;   // [bcap]
+    uint32_t* dy;  // [NRC_HASH_LEVELS][bcap]
+    int64_t bcap;
+};
 hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t s);
 hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
                                 int64_t* waves, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
-                             float* slabs, float* loss_partials, hipStream_t s);
+                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);

@@ -1899,7 +1899,9 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
                                                        float* __restrict__ slabs, float* __restrict__ loss_partials,
                                                        uint64_t* __restrict__ stamps,
                                                        const uint32_t* __restrict__ grid = nullptr,
-                                                       h2v* __restrict__ grid_grad = nullptr) {
+                                                       h2v* __restrict__ grid_grad = nullptr,
+                                                       float4* __restrict__ gpos = nullptr,
+                                                       uint32_t* __restrict__ gdy = nullptr, int64_t bcap = 0) {
     constexpr int KK0 = ENC == 1 ? 4 : 5;
     constexpr int NBF = ENC == 1 ? kBwdFragsHash : kBwdFrags;
     constexpr int SLAB = slab_floats(ENC);
@@ -2102,90 +2104,28 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
 #pragma unroll
         for (int jg = 0; jg < 2; ++jg) store_h4(img_a[0], img_off(sl, 16 * kk + 8 * h + 4 * jg), x[kk], 4 * jg);
     if constexpr (ENC != 1) *(h8*)(img_xh + sl * 32 + 16 * h) = x[KK0 - 1];
-    // Grid gradient (Hash): dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample sl, then the trilinear scatter
-    // of tcnn's kernel_grid_backward, grad[entry][f] += w_corner * dy_f. Fine levels (l >= kCoarseLevels) go straight
-    // to f32 global atomics, which drain while the layer-0 dW runs. The coarse levels cover the scene with a handful of cells
-    // (position * 0.005 spans ~1.6 * 2^l cells per axis), so every sample of the batch would hit the same few
-    // entries: they are pre-summed per block in an LDS hash table (below) and flushed with one atomic per entry.
-    constexpr int kCoarseLevels = 5;
-    float dyc[2 * kCoarseLevels] = {};
+    // Grid gradient (Hash): dL/d(grid feature 16h + r) = (W0^T delta_0)[.] for sample s. The trilinear scatter of
+    // tcnn's kernel_grid_backward (grad[entry][f] += w_corner * dy_f) runs afterwards in grid_scatter_kernel: here
+    // each sample leaves its position and its 16 levels' (dy0, dy1) as f16 pairs, level-major [level][sample]
+    // (zeros for the padding samples).
     if constexpr (ENC == 1) {
         f16v c = zero16();
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) c = mfma(wfrag(kBwdFrags + kk), d0[kk], c);
 #pragma unroll
-        for (int k = 0; k < 2 * kCoarseLevels; ++k) dyc[k] = (float)(_Float16)c[k];
-        if (valid) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                if (h == 0 && i < kCoarseLevels) continue;
-                const float dy0 = (float)(_Float16)c[2 * i], dy1 = (float)(_Float16)c[2 * i + 1];
-                if (dy0 == 0.0f && dy1 == 0.0f) continue;
-                HashCorners C;
-                if (i <= 1) hash_corners<true>(Q.p0, Q.p1, Q.p2, 8 * h + i, C);
-                else hash_corners<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, C);
-#pragma unroll
-                for (int cc = 0; cc < 8; ++cc) grid_atomic(grid_grad, C.entry[cc], C.w[cc] * dy0, C.w[cc] * dy1);
-            }
+        for (int i = 0; i < 8; ++i) {
+            const h2v dv = {valid ? (_Float16)c[2 * i] : (_Float16)0.0f, valid ? (_Float16)c[2 * i + 1] : (_Float16)0.0f};
+            gdy[(int64_t)(8 * h + i) * bcap + s] = __builtin_bit_cast(uint32_t, dv);
         }
+        if (h == 0) gpos[s] = float4{Q.p0, Q.p1, Q.p2, 0.0f};
     }
     dw1.store_all(wave, lane, slab);
     lds_barrier();
     stamp();
-    if constexpr (ENC == 1) {
-        // every wave is past its last weight-image read: the weight region becomes the coarse-level table
-        constexpr int kSlots = 4096;
-        uint32_t* tkey = (uint32_t*)smem;
-        float* tval = (float*)(smem + 4 * kSlots);  // [slot][2]
-        static_assert(12 * kSlots <= kLdsWf + kLdsWb, "coarse-level table must fit the weight-image region");
-        for (int i = threadIdx.x; i < kSlots; i += 256) {
-            tkey[i] = 0xFFFFFFFFu;
-            tval[2 * i] = tval[2 * i + 1] = 0.0f;
-        }
-        {
-            DwAcc<0, ENC> dw0;
-            dw0.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
-            dw0.store_all(wave, lane, slab);
-        }
-        lds_barrier();
-        if (valid && h == 0) {
-#pragma unroll
-            for (int i = 0; i < kCoarseLevels; ++i) {
-                const float dy0 = dyc[2 * i], dy1 = dyc[2 * i + 1];
-                if (dy0 == 0.0f && dy1 == 0.0f) continue;
-                HashCorners C;
-                if (i <= 1) hash_corners<true>(Q.p0, Q.p1, Q.p2, i, C);
-                else hash_corners<false>(Q.p0, Q.p1, Q.p2, i, C);
-#pragma unroll
-                for (int cc = 0; cc < 8; ++cc) {
-                    const uint32_t e = C.entry[cc];
-                    uint32_t slot = (e * 2654435761u) >> 20;  // 12-bit multiplicative hash
-                    bool done = false;
-                    for (int probe = 0; probe < 32 && !done; ++probe) {  // bounded: every lane exits
-                        const uint32_t k = atomicCAS(&tkey[slot], 0xFFFFFFFFu, e);
-                        if (k == 0xFFFFFFFFu || k == e) {
-                            atomicAdd(&tval[2 * slot], C.w[cc] * dy0);
-                            atomicAdd(&tval[2 * slot + 1], C.w[cc] * dy1);
-                            done = true;
-                        }
-                        slot = (slot + 1) & (kSlots - 1);
-                    }
-                    if (!done) grid_atomic(grid_grad, e, C.w[cc] * dy0, C.w[cc] * dy1);  // table crowded
-                }
-            }
-        }
-        lds_barrier();
-        for (int i = threadIdx.x; i < kSlots; i += 256) {
-            const uint32_t e = tkey[i];
-            if (e == 0xFFFFFFFFu) continue;
-            grid_atomic(grid_grad, e, tval[2 * i], tval[2 * i + 1]);
-        }
-    } else {
-        {
-            DwAcc<0, ENC> dw0;
-            dw0.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
-            dw0.store_all(wave, lane, slab);
-        }
+    {
+        DwAcc<0, ENC> dw0;
+        dw0.mfma_all(img_d[0], img_a[0], img_xh, wave, lane, to);
+        dw0.store_all(wave, lane, slab);
     }
     stamp();
 }
@@ -3195,13 +3135,108 @@ hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t
     return hipGetLastError();
 }
 
+// Trilinear grid-gradient scatter (tcnn kernel_grid_backward). Block = (level, half of the level's table, slice of
+// the step's samples): it recomputes each sample's 8 corners at its level and adds w_corner * dy (each product
+// rounded to f16) into an f16 LDS copy of its half table with packed-half LDS atomics (ds_pk_add_f16: f16
+// accumulation, as tcnn's half2 atomicAdd; 64 KiB, two blocks per CU), then flushes the touched entries of the half
+// table with one packed-half global atomic each, issued in entry order. On MI355X device-scope float atomics
+// execute at the memory side and 64 lanes adding to 64 random rows run ~17x below the contiguous rate
+// (MI355X_MICROARCH.md § Global float atomics): the in-kernel version of this scatter (2 M random half2 atomics per
+// 16,384-sample step) dominated the step; here the random adds stay in the CU and the global ones walk the table in
+// order. The slice length is per level: the coarse levels cover the scene
+// with a handful of cells (position * 0.005 spans ~1.6 * 2^l cells per axis), so their LDS adds collide on a few
+// addresses and serialise -- a block's time grows with (slice samples / touched entries) -- while a fine level's
+// block costs mostly its half-table flush. So the slice doubles per level from `min` to `max`.
+constexpr int kScatterThreads = 1024, kScatterHalf = NRC_HASH_T / 2, kScatterPer = 2;
+struct ScatterPlan {
+    int first_block[NRC_HASH_LEVELS + 1];  // level l owns blocks [first_block[l], first_block[l + 1])
+    int slice[NRC_HASH_LEVELS];            // samples per block at level l
+};
+__global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const float4* __restrict__ pos,
+                                                                       const uint32_t* __restrict__ dy, int64_t bcap,
+                                                                       ScatterPlan plan, h2v* __restrict__ grad) {
+    __shared__ h2v acc[kScatterHalf];  // 64 KiB: two blocks per CU
+    int level = 0;
+#pragma unroll
+    for (int l = 1; l < NRC_HASH_LEVELS; ++l) level += (int)blockIdx.x >= plan.first_block[l];
+    const int local = (int)blockIdx.x - plan.first_block[level];
+    const int half = level == 0 ? 0 : local & 1;  // level 0 (4,096 entries) has one half
+    const int64_t slice = plan.slice[level], s0 = (int64_t)(level == 0 ? local : local >> 1) * slice;
+    const uint32_t lbase = NRC_HASH_LEVEL_ENTRY_OFFSET(level), lsize = level == 0 ? 4096u : (uint32_t)NRC_HASH_T;
+    const uint32_t e0 = (uint32_t)half * kScatterHalf;
+    const uint32_t ne = min((uint32_t)kScatterHalf, lsize - e0);
+    const uint32_t* dyl = dy + (int64_t)level * bcap;
+    const int64_t s1 = min(bcap, s0 + slice);
+    // the first batch's loads are issued before the table is zeroed (their latency hides behind it)
+    uint32_t dv[kScatterPer];
+    float4 p[kScatterPer];
+    int64_t s = s0 + threadIdx.x;
+    auto load = [&]() {
+#pragma unroll
+        for (int j = 0; j < kScatterPer; ++j) {
+            const int64_t sj = s + (int64_t)j * kScatterThreads;
+            dv[j] = sj < s1 ? dyl[sj] : 0u;
+            p[j] = sj < s1 ? pos[sj] : float4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    load();
+    for (uint32_t i = threadIdx.x; i < ne / 4; i += kScatterThreads) ((float4*)acc)[i] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    __syncthreads();
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j < kScatterPer; ++j) {
+            const h2v d = __builtin_bit_cast(h2v, dv[j]);
+            const float dy0 = (float)d[0], dy1 = (float)d[1];
+            if (dy0 == 0.0f && dy1 == 0.0f) continue;  // also the samples past the slice
+            HashCorners C;
+            if (level <= 1) hash_corners<true>(p[j].x, p[j].y, p[j].z, level, C);
+            else hash_corners<false>(p[j].x, p[j].y, p[j].z, level, C);
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const uint32_t e = C.entry[cc] - lbase - e0;
+                if (e < ne)
+                    __builtin_amdgcn_ds_atomic_fadd_v2f16((__attribute__((address_space(3))) h2v*)&acc[e],
+                                                          h2v{(_Float16)(C.w[cc] * dy0), (_Float16)(C.w[cc] * dy1)});
+            }
+        }
+        s += (int64_t)kScatterPer * kScatterThreads;
+        if (s0 + (s - s0 - threadIdx.x) >= s1) break;  // block-uniform
+        load();
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads) {
+        const h2v v = acc[i];
+        if (__builtin_bit_cast(uint32_t, v) & 0x7FFF7FFFu)
+            __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v*)(grad + lbase + e0 + i), v);
+    }
+}
+
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
-                             float* slabs, float* loss_partials, hipStream_t s) {
+                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc) {
     if (b <= 0) return hipSuccess;
-    hipLaunchKernelGGL((train_kernel<false, 1>), dim3(train_blocks(b)), dim3(256), 0, s, queries, targets, b, n_total,
+    const int blocks = train_blocks(b);
+    const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
+    if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((train_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
-                       reinterpret_cast<const uint32_t*>(grid), reinterpret_cast<h2v*>(grid_grad));
+                       reinterpret_cast<const uint32_t*>(grid), reinterpret_cast<h2v*>(grid_grad), sc->pos, sc->dy,
+                       bcap);
+    static const int smin_env = getenv("NRC_SCATTER_MIN") ? atoi(getenv("NRC_SCATTER_MIN")) : 0;
+    static const int smax_env = getenv("NRC_SCATTER_MAX") ? atoi(getenv("NRC_SCATTER_MAX")) : 0;
+    // tuning overrides (A/B only); defaults from the sweep in profiles/r01_hash/README.md
+    const int smin = smin_env > 0 ? smin_env : 1024, smax = smax_env > 0 ? smax_env : 2048;
+    ScatterPlan plan;
+    int nb = 0;
+    for (int l = 0; l < NRC_HASH_LEVELS; ++l) {
+        const int sl = (int)std::min<int64_t>((int64_t)smax, (int64_t)smin << l);
+        plan.first_block[l] = nb;
+        plan.slice[l] = sl;
+        nb += (l == 0 ? 1 : 2) * (int)((bcap + sl - 1) / sl);
+    }
+    plan.first_block[NRC_HASH_LEVELS] = nb;
+    hipLaunchKernelGGL(grid_scatter_kernel, dim3(nb), dim3(kScatterThreads), 0, s, sc->pos, sc->dy, bcap, plan,
+                       reinterpret_cast<h2v*>(grid_grad));
     return hipGetLastError();
 }
 
