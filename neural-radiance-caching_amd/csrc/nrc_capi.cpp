@@ -237,6 +237,7 @@ struct nrc_net {
     int n_mlp = NRC_NUM_PARAMS, n_grid = 0;
     _Float16* grid_grad = nullptr;  // f16 [n_grid]: half2 per entry, packed-half atomics (tcnn)
     uint32_t* grid_steps = nullptr;
+    float2* grid_bias = nullptr;  // Adam bias-correction table of the grid parameters (GridBuffers::bias)
     _Float16 *table_train = nullptr, *table_infer = nullptr;
     HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
     int scatter_blocks = 0;
@@ -264,7 +265,7 @@ struct nrc_net {
         f(wf_train); f(wb_train); f(wf_infer);
         f(fwd_pos); f(bwd_pos); f(slab_param);
         f(slabs); f(loss_partials); f(loss_dev);
-        f(grid_grad); f(grid_steps); f(table_train); f(table_infer);
+        f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer);
         f(scatter.pos); f(scatter.dy);
         scatter = HashScatter{};
         scatter_blocks = 0;
@@ -278,6 +279,7 @@ struct nrc_net {
         wide_ws_bpad = 0;
         grid_grad = nullptr;
         grid_steps = nullptr;
+        grid_bias = nullptr;
         table_train = table_infer = nullptr;
         if (loss_host) (void)hipHostFree(loss_host);
         params = m = v = ema = infer = nullptr;
@@ -305,6 +307,7 @@ struct nrc_net {
         g.params = params + n_mlp; g.m = m + n_mlp; g.v = v + n_mlp; g.ema = ema + n_mlp; g.infer = infer + n_mlp;
         g.grad16 = grid_grad; g.grad32 = nullptr; g.steps = grid_steps;
         g.table_train = table_train; g.table_infer = table_infer;
+        g.bias = grid_bias; g.bias_len = grid_bias ? kGridBiasLen : 0;
         g.n = n_grid;
         return g;
     }
@@ -583,6 +586,11 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->table_infer, sizeof(_Float16) * ng));
             HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(_Float16) * ng));
             HIP_CHECK(hipMemset(net->grid_steps, 0, sizeof(uint32_t) * ng));
+            std::vector<float2> bias(kGridBiasLen + 1, float2{0.0f, 0.0f});
+            for (uint32_t st = 1; st <= kGridBiasLen; ++st)
+                bias[st] = float2{sqrtf(1.0f - powf(net->cfg.beta2, (float)st)), 1.0f - powf(net->cfg.beta1, (float)st)};
+            HIP_CHECK(hipMalloc(&net->grid_bias, sizeof(float2) * bias.size()));
+            HIP_CHECK(hipMemcpy(net->grid_bias, bias.data(), sizeof(float2) * bias.size(), hipMemcpyHostToDevice));
         }
         HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
         HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));

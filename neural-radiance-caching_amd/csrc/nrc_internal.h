@@ -190,8 +190,15 @@ struct GridBuffers {
     const float* grad32;  // kApplyOnly: the all-reduced data-parallel gradient (f32 [n], read-only)
     uint32_t* steps;  // per-entry Adam step counters
     _Float16 *table_train, *table_infer;
+    // Adam bias corrections per step count st = 1..bias_len: bias[st] = (sqrtf(1 - beta2^st), 1 - beta1^st), host
+    // glibc powf as in the oracle (the kernel falls back to device powf past bias_len)
+    const float2* bias;
+    uint32_t bias_len;
     int n;
 };
+// steps covered by the bias table (past it the kernel calls powf; for the default betas 0.9 / 0.999 both
+// corrections are exactly 1.0f there)
+constexpr uint32_t kGridBiasLen = 1u << 16;
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
 // Hash training workspace: per sample its position and the 16 levels' (dy0, dy1) f16 pairs ([level][sample]),
 // written by the training kernel and consumed by grid_scatter_kernel.
