@@ -231,8 +231,20 @@ struct nrc_net {
     float* slabs = nullptr;
     int slab_blocks = 0;
     float* loss_partials = nullptr;
-    float* loss_dev = nullptr;
-    float* loss_host = nullptr;  // pinned
+    // minibatch-loss slots: host-mapped fine-grained (coherent) pinned memory written directly by the reduce/Adam
+    // kernels, so reading a loss back costs one stream sync and no D2H copy launch (the copy was ~4.5 us)
+    float* loss_dev = nullptr;   // device view of loss_host
+    float* loss_host = nullptr;
+    void alloc_loss_slots() {
+        HIP_CHECK(hipHostMalloc(&loss_host, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_CHECK(hipHostGetDevicePointer((void**)&loss_dev, loss_host, 0));
+        for (int i = 0; i < 4; ++i) loss_host[i] = 0.0f;
+    }
+    // stream-ordered read of loss slot 0 (blocks the host, as the reference's Trainer::loss does)
+    float read_loss() {
+        HIP_CHECK(hipStreamSynchronize(stream));
+        return loss_host[0];
+    }
     // InputEncoding::Hash: grid part of the model arrays starts at n_mlp
     int n_mlp = NRC_NUM_PARAMS, n_grid = 0;
     _Float16* grid_grad = nullptr;  // f16 [n_grid]: half2 per entry, packed-half atomics (tcnn)
@@ -264,7 +276,7 @@ struct nrc_net {
         f(params); f(m); f(v); f(ema); f(infer);
         f(wf_train); f(wb_train); f(wf_infer);
         f(fwd_pos); f(bwd_pos); f(slab_param);
-        f(slabs); f(loss_partials); f(loss_dev);
+        f(slabs); f(loss_partials);  // loss_dev aliases loss_host (freed below)
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer);
         f(scatter.pos); f(scatter.dy);
         scatter = HashScatter{};
@@ -405,9 +417,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
                                    net->optim(net->step), net->stream));
         repack(net, net->stream);
         if (loss_h) {
-            HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
-            HIP_CHECK(hipStreamSynchronize(net->stream));
-            *loss_h = *net->loss_host;
+            *loss_h = net->read_loss();
         }
         return;
     }
@@ -425,9 +435,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
                                  loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
     if (net->hash()) HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
     if (loss_h) {
-        HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
-        HIP_CHECK(hipStreamSynchronize(net->stream));
-        *loss_h = *net->loss_host;
+        *loss_h = net->read_loss();
     }
 }
 
@@ -549,9 +557,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->wide_exps, sizeof(int32_t) * 5 * 128));
             HIP_CHECK(hipMalloc(&net->wide_fwd_train, kWideF16Bytes));
             HIP_CHECK(hipMalloc(&net->wide_bwd_train, kWideBwdBytes));
-            HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
-            HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
-            HIP_CHECK(hipMemset(net->loss_dev, 0, sizeof(float) * 4));
+            net->alloc_loss_slots();
             std::vector<float> p(net->n_total());
             init_params_wide(p, net->cfg.seed);
             upload_all(net, p, p);
@@ -592,15 +598,13 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->grid_bias, sizeof(float2) * bias.size()));
             HIP_CHECK(hipMemcpy(net->grid_bias, bias.data(), sizeof(float2) * bias.size(), hipMemcpyHostToDevice));
         }
-        HIP_CHECK(hipMalloc(&net->loss_dev, sizeof(float) * 4));
-        HIP_CHECK(hipHostMalloc(&net->loss_host, sizeof(float) * 4, hipHostMallocDefault));
+        net->alloc_loss_slots();
         HIP_CHECK(hipMemset(net->m, 0, pb));
         HIP_CHECK(hipMemset(net->v, 0, pb));
         HIP_CHECK(hipMemset(net->ema, 0, pb));
         HIP_CHECK(hipMemset(net->wf_train, 0, sizeof(_Float16) * kFwdHalves));
         HIP_CHECK(hipMemset(net->wb_train, 0, sizeof(_Float16) * kBwdHalvesHash));
         HIP_CHECK(hipMemset(net->wf_infer, 0, sizeof(_Float16) * kFwdHalves));
-        HIP_CHECK(hipMemset(net->loss_dev, 0, sizeof(float) * 4));
         std::vector<int> fwd, bwd;
         build_scatter_maps(fwd, bwd, net->encoding);
         HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
@@ -807,10 +811,7 @@ nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
                                        net->buffers(), net->optim(net->step), net->stream));
             repack(net, net->stream);
             if (loss_h) {
-                HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost,
-                                         net->stream));
-                HIP_CHECK(hipStreamSynchronize(net->stream));
-                *loss_h = *net->loss_host;
+                *loss_h = net->read_loss();
             }
             return;
         }
@@ -822,9 +823,7 @@ nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
             HIP_CHECK(launch_grid_adam(kApplyOnly, gb, net->optim(net->step), net->stream));
         }
         if (loss_h) {
-            HIP_CHECK(hipMemcpyAsync(net->loss_host, net->loss_dev, sizeof(float), hipMemcpyDeviceToHost, net->stream));
-            HIP_CHECK(hipStreamSynchronize(net->stream));
-            *loss_h = *net->loss_host;
+            *loss_h = net->read_loss();
         }
     });
 }

@@ -150,7 +150,7 @@ nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nr
                                      p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],
                                      fb->train_targets_d[1], NRC_NUM_TRAINING_RECORDS_PER_FRAME, s));
         // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss. The minibatch losses
-        // land in device slots and are read back with one copy + one sync at the end (the reference syncs after
+        // land in host-mapped slots and are read after one sync at the end (the reference syncs after
         // every minibatch, Device.cpp:1504); summed in the same order, so the mean is the same float.
         const nrc_loss_slots slots = net_loss_slots(net);
         for (int b = 0; b < NRC_NUM_BATCHES; ++b)
@@ -158,8 +158,7 @@ nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nr
                                   reinterpret_cast<const float*>(fb->train_targets_d[1] + (size_t)b * NRC_BATCH_SIZE),
                                   NRC_BATCH_SIZE, slots.dev + b));
         if (loss_h) {
-            HIP_CHECK(hipMemcpyAsync(slots.host, slots.dev, sizeof(float) * NRC_NUM_BATCHES, hipMemcpyDeviceToHost, s));
-            HIP_CHECK(hipStreamSynchronize(s));
+            HIP_CHECK(hipStreamSynchronize(s));  // the slots are host-mapped: the kernels wrote them directly
             float total = 0.0f;
             for (int b = 0; b < NRC_NUM_BATCHES; ++b) total += slots.host[b];
             *loss_h = total * (1.0f / NRC_NUM_BATCHES);

@@ -219,9 +219,9 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
 
 // ---- per-handle scratch used by the frame driver (nrc_capi.cpp): NRC_NUM_BATCHES loss slots on the device and a
 // pinned host mirror
-struct nrc_loss_slots {
-    float* dev;
-    float* host;
+struct nrc_loss_slots {  // four minibatch-loss slots in host-mapped coherent pinned memory
+    float* dev;   // device view (what the kernels write)
+    float* host;  // host view (valid after a stream sync)
 };
 }  // namespace nrc_amd
 struct nrc_net;
