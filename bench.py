@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-wide", action="store_true", help="skip the configs[4] width-128 f16/FP8 inference lines")
+    ap.add_argument("--no-hash", action="store_true", help="skip the InputEncoding::Hash line")
     ap.add_argument("--frame-iters", type=int, default=20, help="timed 1080p post-trace frames (0: skip)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one "
@@ -131,6 +132,44 @@ def frame_bench(nrc, net, dev, iters: int) -> dict:
     return {"frame_ms": ms, "queries": S + T, "train_records": f.num_training_records, "iters": iters,
             "what": "nrc_process_frame: fused infer+accumulate, propagate, Feistel shuffle, 4 x 16384 train with "
                     "loss read-back; synthetic 1920x1080 Cornell frame, 8x8 tiles"}
+
+
+def hash_bench(nrc, dev, iters: int) -> dict:
+    """SURVEY §8(f) row 3: the InputEncoding::Hash model (16-level HashGrid + OneBlob + Identity -> 64x5 MLP) on
+    one GPU: 2^21-query inference and the 16,384-sample training step (encode -> fwd -> loss -> bwd -> grid scatter
+    -> Adam), HIP events on the network's stream, after 8 warm-up steps (random-init weights)."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    net = nrc.Network()
+    net.init(stream=stream, encoding=nrc.InputEncoding.Hash)
+    n = QUERIES_PER_GPU
+    q = torch.from_numpy(nrc.synthetic.cornell_queries(n, seed=nrc.synthetic.SEED + 2000)).to(dev)
+    out = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    tq, tt = nrc.synthetic.cornell_batch(4 * nrc.BATCH_SIZE, seed=nrc.synthetic.SEED + 2001)
+    tq, tt = torch.from_numpy(tq).to(dev), torch.from_numpy(tt).to(dev)
+    B = nrc.BATCH_SIZE
+
+    def timed(fn, k: int) -> float:
+        for i in range(3):
+            fn(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(k):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / k
+
+    for f in range(8):
+        net.train(tq[(f % 4) * B:], tt[(f % 4) * B:])
+    infer_ms = timed(lambda i: net.infer(q, out, n), iters)
+    train_ms = timed(lambda i: net.train(tq[(i % 4) * B:], tt[(i % 4) * B:]), 4 * iters)
+    net.destroy()
+    return {"workload": "SURVEY 8(f) row 3: InputEncoding::Hash, 2^21-query inference + 16384-sample train step",
+            "M_queries_per_s": n / (infer_ms * 1e-3) / 1e6, "infer_kernel_ms": infer_ms, "train_step_ms": train_ms,
+            "bound": "L1/TA gather rate (128 random table reads per query), DESIGN.md section 10"}
 
 
 def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
@@ -285,6 +324,7 @@ def main() -> None:
         frame = frame_bench(nrc, net, dev, args.frame_iters)
 
     wide = None if args.no_wide else wide_bench(nrc, dev, world, rank, max(10, args.steps // 4), barrier)
+    hashgrid = hash_bench(nrc, dev, max(10, args.steps // 10)) if world == 1 and not args.no_hash else None
 
     achieved = FLOP_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e12
     result = {
@@ -310,6 +350,7 @@ def main() -> None:
         "infer_kernel_ms": kernel_ms,
         "frame": frame,
         "wide_c5": wide,
+        "hash": hashgrid,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F16_TFLOPS, "traffic": pmc_traffic(),
                      "algorithmic_bytes_per_launch": BYTES_PER_QUERY * nq,
