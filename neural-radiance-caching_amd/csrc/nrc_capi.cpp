@@ -339,8 +339,9 @@ struct nrc_net {
         wide_ws_in = wide_ws_d = nullptr;
         wide_slabs = wide_loss_partials = nullptr;
         wide_ws_bpad = 0;
-        HIP_CHECK(hipMalloc(&wide_ws_in, sizeof(_Float16) * kWideInRows * bpad));
-        HIP_CHECK(hipMalloc(&wide_ws_d, sizeof(_Float16) * kWideDRows * bpad));
+        // rows of wide_ld(bpad) >= bpad samples (the row stride; see wide_ld)
+        HIP_CHECK(hipMalloc(&wide_ws_in, sizeof(_Float16) * kWideInRows * wide_ld(bpad)));
+        HIP_CHECK(hipMalloc(&wide_ws_d, sizeof(_Float16) * kWideDRows * wide_ld(bpad)));
         HIP_CHECK(hipMalloc(&wide_slabs, sizeof(float) * NRC_WIDE_NUM_PARAMS * (size_t)wide_chunks(bpad)));
         HIP_CHECK(hipMalloc(&wide_loss_partials, sizeof(float) * (size_t)(bpad / 32)));
         wide_ws_bpad = bpad;

@@ -116,6 +116,7 @@ constexpr int kWideBwdBytes = kWideBwdFrags * 1024;
 // workspace rows ([feature][bpad] f16): inputs x (80) + a_0..a_4 (5 x 128) = 720; deltas 5 x 128 + 16 = 656
 constexpr int kWideInRows = 80 + 5 * 128, kWideDRows = 5 * 128 + 16;
 int64_t wide_bpad(int64_t b);
+int64_t wide_ld(int64_t b);  // row stride (f16 elements) of the width-128 training workspace
 int wide_chunks(int64_t b);
 hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float* targets, int64_t b, float n_total,
                                      float loss_scale, const _Float16* fwd16, const _Float16* bwd16, _Float16* ws_in,

@@ -2282,10 +2282,10 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 
 // ------------------------------------------------------------------------------------------------
 // Width-128 training step (BASELINE configs[4]; oracle/nrc_wide_oracle.c orc_wide_grad + orc_adam_ema):
-//   wide_fwd_bwd_kernel  one wave per 32 samples: encode, forward (f16 MFMA chain, A fragments straight from the
-//                        L2-resident training images), RelativeL2Luminance, delta chain through W_l^T; stores every
-//                        layer's input and delta as f16 [feature][sample] rows of a workspace;
-//   wide_dw_kernel       dW_l = sum_s delta_l in_l^T as 32x32 tiles x 1024-sample chunks (A and B fragments are
+//   wide_fwd_bwd_lds_kernel  two waves (64 samples) per block: encode, forward (f16 MFMA chain, A fragments from the
+//                        LDS-staged training images), RelativeL2Luminance, delta chain through W_l^T; stores every
+//                        layer's input and delta as f16 [feature][sample] rows of a workspace (row stride wide_ld);
+//   wide_dw_kernel       dW_l = sum_s delta_l in_l^T as 32x32 tiles x 512-sample chunks (A and B fragments are
 //                        16-byte loads of those rows), partial sums per chunk in canonical parameter order;
 //   wide_adam_kernel     fixed-order chunk sum + tcnn Adam + EMA per parameter (same float operations as
 //                        adam_pack_one), then the f16 / FP8 images are repacked (launch_wide_pack, wide_pack_train).
@@ -2308,15 +2308,40 @@ __device__ __forceinline__ void store_frag_rows(_Float16* __restrict__ ws, int64
         for (int j = 0; j < 8; ++j) ws[(int64_t)acc_row(kk, h, j) * bpad + s] = y[kk][j];
 }
 
+// Copy COUNT h8 (1-KiB fragments of 64 lanes) global -> LDS with LDS-DMA (global_load_lds_dwordx4: no VGPRs, all
+// of a thread's copies in flight at once); fragment c goes to wave c % W's instruction c / W. The caller waits
+// (s_waitcnt vmcnt(0)) and synchronises before reading.
+template <int W, int FRAGS>
+__device__ __forceinline__ void dma_frags_to_lds(h8* lds, const h8* __restrict__ src) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+#pragma unroll 4
+    for (int c = wave; c < FRAGS; c += W)
+        __builtin_amdgcn_global_load_lds((const void*)(src + c * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(lds + c * 64), 16, 0, 0);
+}
+
+// Width-128 forward + loss + delta chain, the weight images staged in LDS: a block of 2 waves (64 samples, one wave
+// per 32) per CU stages the 156-KiB forward image by LDS-DMA, encodes, runs the forward pass and the loss, then
+// stages the 132-KiB backward image over it for the delta chain. Every layer's input and delta go to the workspace
+// as f16 [feature][sample] rows for wide_dw_kernel. (The first version ran one wave per block and read every A
+// fragment from L2 -- 288 KiB per wave, a round trip per layer: 39.5 us per 16,384-sample step; this one 26.5 us.)
 template <int ENC>
-__global__ __launch_bounds__(64, 1) void wide_fwd_bwd_kernel(const float* __restrict__ q, const float* __restrict__ t,
-                                                             int64_t b, int64_t bpad, float n_total, float loss_scale,
-                                                             const h8* __restrict__ wf, const h8* __restrict__ wb,
-                                                             _Float16* __restrict__ ws_in, _Float16* __restrict__ ws_d,
-                                                             float* __restrict__ loss_partials) {
+__global__ __launch_bounds__(128, 1) void wide_fwd_bwd_lds_kernel(const float* __restrict__ q,
+                                                                  const float* __restrict__ t, int64_t b,
+                                                                  int64_t bpad, int64_t ld, float n_total,
+                                                                  float loss_scale, const h8* __restrict__ wf,
+                                                                  const h8* __restrict__ wb,
+                                                                  _Float16* __restrict__ ws_in,
+                                                                  _Float16* __restrict__ ws_d,
+                                                                  float* __restrict__ loss_partials) {
+    __shared__ __attribute__((aligned(16))) h8 lw[kWideF16Bytes / 16];
+    static_assert(kWideBwdBytes <= kWideF16Bytes, "backward image reuses the forward image's LDS");
+    dma_frags_to_lds<2, kWideF16Frags>(lw, wf);
     fp32_flush_output_denorms();  // the omod doubling-chain encoder (as the inference kernels)
-    const int lane = threadIdx.x, h = lane >> 5, r = lane & 31;
-    const int64_t s = (int64_t)blockIdx.x * 32 + r;  // s < bpad
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    const int64_t tile = (int64_t)blockIdx.x * 2 + wave;
+    const bool live = tile * 32 < bpad;        // the last block's second wave may have no samples (bpad % 64 == 32)
+    const int64_t s = tile * 32 + r;           // < bpad + 32 <= ld: a dead wave's stores land in the row padding
     const bool valid = s < b;
     const int64_t sc = valid ? s : b - 1;
     const QLane Q = load_q_enc<ENC>(q, sc, h);
@@ -2332,22 +2357,27 @@ __global__ __launch_bounds__(64, 1) void wide_fwd_bwd_kernel(const float* __rest
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ws_in[(int64_t)enc_k0_feature(ENC, 16 * kk + 8 * h + j) * bpad + s] = x[kk][j];
+        for (int j = 0; j < 8; ++j) ws_in[(int64_t)enc_k0_feature(ENC, 16 * kk + 8 * h + j) * ld + s] = x[kk][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
-    const h8* wl = wf + lane;
     h8 a[5][8];
     f16v c[4];
+    {
+        lds_h8* wl = launder((lds_h8*)(lw + lane));
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
+        for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
 #pragma unroll
-    for (int kk = 0; kk < 5; ++kk)
+        for (int kk = 0; kk < 5; ++kk)
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(0, mb, kk) * 64], x[kk], c[mb]);
+            for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(0, mb, kk) * 64], x[kk], c[mb]);
+    }
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) a[0][kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
-    store_frag_rows(ws_in + wide_in_row(1) * bpad, bpad, s, h, a[0]);
+    store_frag_rows(ws_in + wide_in_row(1) * ld, ld, s, h, a[0]);
 #pragma unroll
     for (int l = 1; l < 5; ++l) {
+        lds_h8* wl = launder((lds_h8*)(lw + lane));
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
 #pragma unroll
@@ -2356,11 +2386,17 @@ __global__ __launch_bounds__(64, 1) void wide_fwd_bwd_kernel(const float* __rest
             for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(l, mb, kk) * 64], a[l - 1][kk], c[mb]);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) a[l][kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
-        store_frag_rows(ws_in + wide_in_row(l + 1) * bpad, bpad, s, h, a[l]);
+        store_frag_rows(ws_in + wide_in_row(l + 1) * ld, ld, s, h, a[l]);
     }
     f16v o = zero16();
+    {
+        lds_h8* wl = launder((lds_h8*)(lw + lane));
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) o = mfma(wl[wide_frag(5, 0, kk) * 64], a[4][kk], o);
+        for (int kk = 0; kk < 8; ++kk) o = mfma(wl[wide_frag(5, 0, kk) * 64], a[4][kk], o);
+    }
+    // every wave is past its last forward-image read: stage the backward image while the loss is computed
+    __syncthreads();
+    dma_frags_to_lds<2, kWideBwdFrags>(lw, wb);
 
     // RelativeL2Luminance on the f16 prediction, loss-scaled f16 gradient, ReLU-masked (as train_kernel)
     float lossv = 0.0f;
@@ -2382,21 +2418,26 @@ __global__ __launch_bounds__(64, 1) void wide_fwd_bwd_kernel(const float* __rest
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) lossv += __shfl_xor(lossv, off);
-    if (lane == 0) loss_partials[blockIdx.x] = lossv;
+    if (lane == 0 && live) loss_partials[tile] = lossv;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ws_d[(wide_d_row(5) + acc_row(0, h, j)) * bpad + s] = g[j];
+    for (int j = 0; j < 8; ++j) ws_d[(wide_d_row(5) + acc_row(0, h, j)) * ld + s] = g[j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
 
     // delta chain: d_{l-1} = relu'(a_{l-1}) (W_l^T d_l); accumulator block mb regs 0-7 / 8-15 are the rows of the
     // B fragments 2 mb / 2 mb + 1, so the gate takes the activation fragments as they are
-    const h8* bl = wb + lane;
     h8 d[8];
+    {
+        lds_h8* bl = launder((lds_h8*)(lw + lane));
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(bl[wide_bwd_frag(5, mb, 0) * 64], g, zero16());
+        for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(bl[wide_bwd_frag(5, mb, 0) * 64], g, zero16());
+    }
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) mask_pack_pk(c[mb], a[4][2 * mb], a[4][2 * mb + 1], d[2 * mb], d[2 * mb + 1]);
-    store_frag_rows(ws_d + wide_d_row(4) * bpad, bpad, s, h, d);
+    store_frag_rows(ws_d + wide_d_row(4) * ld, ld, s, h, d);
 #pragma unroll
     for (int l = 4; l >= 1; --l) {
+        lds_h8* bl = launder((lds_h8*)(lw + lane));
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
 #pragma unroll
@@ -2406,17 +2447,25 @@ __global__ __launch_bounds__(64, 1) void wide_fwd_bwd_kernel(const float* __rest
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
             mask_pack_pk(c[mb], a[l - 1][2 * mb], a[l - 1][2 * mb + 1], d[2 * mb], d[2 * mb + 1]);
-        store_frag_rows(ws_d + wide_d_row(l - 1) * bpad, bpad, s, h, d);
+        store_frag_rows(ws_d + wide_d_row(l - 1) * ld, ld, s, h, d);
     }
 }
 
 // One wave per (32x32 tile of dW_l, chunk of kWideChunk samples). Tiles: layer 0 4 x 3 (80 inputs), layers 1-4
 // 4 x 4, layer 5 1 x 4 (16 outputs) = 80.
 constexpr int kWideTiles = 12 + 64 + 4;
-constexpr int kWideChunk = 1024;
+constexpr int kWideChunk = 512;  // 1,024: 85.5 us per step, 512: 81.3, 256: 84.0 (latency vs Adam's chunk sums)
 __global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict__ ws_in, const _Float16* __restrict__ ws_d,
-                                                      int64_t bpad, int nchunks, float* __restrict__ slabs) {
-    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                      int64_t bpad, int64_t ld, int nchunks, float* __restrict__ slabs) {
+    // Blocks are dealt to the 8 XCDs round-robin (physical block p runs on XCD p % 8): 4 consecutive logical blocks
+    // -- the 4 row blocks of one (layer, chunk), which read the same input rows -- go to one XCD's L2 (L2 hit rate
+    // 30 -> 68 %, HBM/Infinity-Cache fetch 103 -> 45 MB per step). A chunk is 20 blocks (W0 = blocks 0-2, W1..W4 =
+    // 4 blocks each from block 3, W5 = block 19): rotated by 3 so that every aligned group of 4 is one hidden
+    // layer's 4 row blocks. The grid is rounded up to whole groups of 32 (the extra blocks return).
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int logical = ((slot >> 2) * 8 + xcd) * 4 + (slot & 3);
+    const int blk = logical / 20 * 20 + (logical % 20 + 3) % 20;
+    const int task = blk * 4 + (threadIdx.x >> 6);
     if (task >= kWideTiles * nchunks) return;
     const int tile = task % kWideTiles, chunk = task / kWideTiles;
     int layer, mb, nb;
@@ -2427,13 +2476,14 @@ __global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict
     const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
     const int o = 32 * mb + r, i = 32 * nb + r;  // this lane's A row / B column
     const bool oa = o < out_dim, ib = i < in_dim;
-    const h8* pa = reinterpret_cast<const h8*>(ws_d + (wide_d_row(layer) + (oa ? o : 0)) * bpad + 8 * h);
-    const h8* pb = reinterpret_cast<const h8*>(ws_in + (wide_in_row(layer) + (ib ? i : 0)) * bpad + 8 * h);
+    const h8* pa = reinterpret_cast<const h8*>(ws_d + (wide_d_row(layer) + (oa ? o : 0)) * ld + 8 * h);
+    const h8* pb = reinterpret_cast<const h8*>(ws_in + (wide_in_row(layer) + (ib ? i : 0)) * ld + 8 * h);
     const int64_t k0 = (int64_t)chunk * kWideChunk, k1 = min<int64_t>(bpad, k0 + kWideChunk);
     f16v acc[2] = {zero16(), zero16()};
     const h8 z = {};
     // batches of 8 k steps with the next batch's 16 loads in flight during this batch's MFMAs (the operands come
-    // from L2: a load -> MFMA chain one k step at a time waited a full L2 round trip per step)
+    // from L2: a load -> MFMA chain one k step at a time waited a full L2 round trip per step; 16-step batches
+    // measured slower)
     constexpr int KB = 8;
     int64_t k = k0;
     const int64_t kfull = k0 + (k1 - k0) / (16 * KB) * (16 * KB);
@@ -2971,22 +3021,29 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
 }
 
 int64_t wide_bpad(int64_t b) { return (b + 31) / 32 * 32; }
+// Workspace row stride: 32 samples (64 B) past bpad. With a power-of-two stride (bpad = 16,384 -> 32 KiB) the 32 rows
+// of one MFMA operand load all map to the same L2 channel; the pad spreads them (wide_dw_kernel 36.1 -> 28.8 us per
+// 16,384-sample step; pads of 8 / 16 / 48 / 64 / 128 / 160 samples measured 87.8 / 85.0 / 87.1 / 92.7 / 95 / 85 us
+// per step against 84.9 for 32 and 92.0 unpadded).
+int64_t wide_ld(int64_t b) { return wide_bpad(b) + 32; }
 int wide_chunks(int64_t b) { return (int)((wide_bpad(b) + kWideChunk - 1) / kWideChunk); }
 
 hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float* targets, int64_t b, float n_total,
                                      float loss_scale, const _Float16* fwd16, const _Float16* bwd16, _Float16* ws_in,
                                      _Float16* ws_d, float* slabs, float* loss_partials, hipStream_t s) {
     if (b <= 0) return hipSuccess;
-    const int64_t bpad = wide_bpad(b);
+    const int64_t bpad = wide_bpad(b), ld = wide_ld(b);
     const int tiles = (int)(bpad / 32);
+    const int blocks = (tiles + 1) / 2;
     if (enc == 2)
-        hipLaunchKernelGGL(wide_fwd_bwd_kernel<2>, dim3(tiles), dim3(64), 0, s, queries, targets, b, bpad, n_total,
-                           loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
+        hipLaunchKernelGGL(wide_fwd_bwd_lds_kernel<2>, dim3(blocks), dim3(128), 0, s, queries, targets, b, bpad, ld,
+                           n_total, loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
     else
-        hipLaunchKernelGGL(wide_fwd_bwd_kernel<0>, dim3(tiles), dim3(64), 0, s, queries, targets, b, bpad, n_total,
-                           loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
+        hipLaunchKernelGGL(wide_fwd_bwd_lds_kernel<0>, dim3(blocks), dim3(128), 0, s, queries, targets, b, bpad, ld,
+                           n_total, loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
     const int nch = wide_chunks(b);
-    hipLaunchKernelGGL(wide_dw_kernel, dim3((kWideTiles * nch + 3) / 4), dim3(256), 0, s, ws_in, ws_d, bpad, nch, slabs);
+    const int nblk = (kWideTiles * nch + 3) / 4;
+    hipLaunchKernelGGL(wide_dw_kernel, dim3((nblk + 31) / 32 * 32), dim3(256), 0, s, ws_in, ws_d, bpad, ld, nch, slabs);
     return hipGetLastError();
 }
 
