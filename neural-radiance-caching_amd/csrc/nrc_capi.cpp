@@ -258,7 +258,6 @@ struct nrc_net {
     // forward / backward from the master weights) and the training workspace
     uint8_t *wide_img16 = nullptr, *wide_img8 = nullptr;
     uint32_t* wide_scales = nullptr;
-    int32_t* wide_exps = nullptr;
     _Float16 *wide_fwd_train = nullptr, *wide_bwd_train = nullptr;
     _Float16 *wide_ws_in = nullptr, *wide_ws_d = nullptr;
     float *wide_slabs = nullptr, *wide_loss_partials = nullptr;
@@ -281,11 +280,10 @@ struct nrc_net {
         f(scatter.pos); f(scatter.dy);
         scatter = HashScatter{};
         scatter_blocks = 0;
-        f(wide_img16); f(wide_img8); f(wide_scales); f(wide_exps);
+        f(wide_img16); f(wide_img8); f(wide_scales);
         f(wide_fwd_train); f(wide_bwd_train); f(wide_ws_in); f(wide_ws_d); f(wide_slabs); f(wide_loss_partials);
         wide_img16 = wide_img8 = nullptr;
         wide_scales = nullptr;
-        wide_exps = nullptr;
         wide_fwd_train = wide_bwd_train = wide_ws_in = wide_ws_d = nullptr;
         wide_slabs = wide_loss_partials = nullptr;
         wide_ws_bpad = 0;
@@ -389,9 +387,8 @@ void upload_all(nrc_net* net, const std::vector<float>& params, const std::vecto
 void repack(nrc_net* net, hipStream_t s) {
     if (net->wide()) {
         const int enc = net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0;
-        HIP_CHECK(launch_wide_pack(net->infer, enc, reinterpret_cast<_Float16*>(net->wide_img16), net->wide_img8,
-                                   net->wide_scales, net->wide_exps, s));
-        HIP_CHECK(launch_wide_pack_train(net->params, enc, net->wide_fwd_train, net->wide_bwd_train, s));
+        HIP_CHECK(launch_wide_pack(net->infer, net->params, enc, reinterpret_cast<_Float16*>(net->wide_img16),
+                                   net->wide_img8, net->wide_scales, net->wide_fwd_train, net->wide_bwd_train, s));
         return;
     }
     HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
@@ -555,7 +552,6 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->wide_img16, kWideF16Bytes));
             HIP_CHECK(hipMalloc(&net->wide_img8, kWide8Bytes));
             HIP_CHECK(hipMalloc(&net->wide_scales, sizeof(uint32_t) * 5 * 32));
-            HIP_CHECK(hipMalloc(&net->wide_exps, sizeof(int32_t) * 5 * 128));
             HIP_CHECK(hipMalloc(&net->wide_fwd_train, kWideF16Bytes));
             HIP_CHECK(hipMalloc(&net->wide_bwd_train, kWideBwdBytes));
             net->alloc_loss_slots();

@@ -104,8 +104,9 @@ __host__ __device__ constexpr int wide8_frag(int layer, int mb, int s) {
 __host__ __device__ constexpr int f8_row(int s, int h, int j) {
     return 64 * s + 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
 }
-hipError_t launch_wide_pack(const float* w, int enc, _Float16* img16, uint8_t* img8, uint32_t* scales, int32_t* exps,
-                            hipStream_t s);
+// every width-128 image: inference f16 + FP8 (+ row scales) from w_infer, training fwd/bwd from w_train
+hipError_t launch_wide_pack(const float* w_infer, const float* w_train, int enc, _Float16* img16, uint8_t* img8,
+                            uint32_t* scales, _Float16* fwd16, _Float16* bwd16, hipStream_t s);
 // prec 0 = f16, 1 = fp8; enc 0 = Frequency, 2 = FrequencySH; mode -1 plain, 0 / 2 fused accumulation
 hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out, int64_t n, const void* img,
                              const uint32_t* scales, const float* thr, float* rgba, int64_t n_acc, int mode, float w,
@@ -124,7 +125,6 @@ hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float*
 hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const float* loss_partials, int nlp,
                             float* grad_io, float* loss_out, const struct ModelBuffers& mb, const struct OptimArgs& oa,
                             hipStream_t s);
-hipError_t launch_wide_pack_train(const float* w, int enc, _Float16* fwd16, _Float16* bwd16, hipStream_t s);
 // diagnostic: e4m3 conversion exactly as the FP8 kernels do it (clamp to [lo, 448], v_cvt_pk_fp8_f32)
 hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s);
 

@@ -1262,42 +1262,30 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
     }
 }
 
-// Per-row E8M0 exponents of W1..W5 (oracle orc_fp8_row_exponent): one wave per (layer, row), 2 weights per lane and a
-// max butterfly (a single-block version with one thread walking each 128-weight row took 18 us).
-__global__ __launch_bounds__(256) void wide_row_exp_kernel(const float* __restrict__ w, int32_t* __restrict__ exps) {
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // t = (layer - 1) * 128 + row
-    if (t >= 5 * 128) return;
-    const int layer = 1 + t / 128, row = t % 128;
-    const bool live = layer < 5 || row < NRC_OUT_PADDED;
-    const float* wr = w + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;  // W5 rows follow W4's
-    float amax = live ? fmaxf(fabsf(wr[lane]), fabsf(wr[lane + 64])) : 0.0f;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
-    int e = 0;
-    if (amax > 0.0f) {
-        int E = 0;
-        const float M = frexpf(amax, &E);
-        e = M <= 0.875f ? E - 9 : E - 8;
-        e = max(-127, min(127, e));
-    }
-    if (lane == 0) exps[t] = e;
+// All width-128 weight images in one launch, after every optimizer step (or set_state):
+//   fp8 part, one wave per (layer 1..5, row block mb): lane (r, h) loads the 64 weights of row 32 mb + r that its
+//     e4m3 bytes carry (lanes h = 0 / 1 hold complementary halves of the row), so the row's E8M0 exponent (oracle
+//     orc_fp8_row_exponent: max |w| of the row) is a lane max and one xor-32 shuffle; the wave then converts and
+//     stores its 4 16-byte units and byte mb of the row's scale word (W5: the whole word);
+//   f16 inference image (img16, and its 20 layer-0 fragments into img8) from the EMA weights;
+//   training images fwd16 / bwd16 (W_l^T) from the master weights.
+// One thread per 16-byte unit in the f16 parts. (It replaced three launches -- row exponents, inference images,
+// training images -- of ~5 us each.)
+// width-128 training layout helpers: backward-image fragment, workspace rows, parameter offsets
+__host__ __device__ constexpr int wide_bwd_frag(int layer, int mb, int kk) {
+    return layer == 5 ? mb : 4 + (layer - 1) * 32 + mb * 8 + kk;
+}
+__host__ __device__ constexpr int64_t wide_in_row(int layer) { return layer == 0 ? 0 : 80 + (layer - 1) * 128; }
+__host__ __device__ constexpr int64_t wide_d_row(int layer) { return (int64_t)layer * 128; }
+__host__ __device__ constexpr int wide_off(int layer) {
+    return layer == 0 ? NRC_WIDE_W0_OFFSET : layer <= 4 ? NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 : NRC_WIDE_W5_OFFSET;
 }
 
-// f16 image (img16, 156 fragments) and FP8 image (img8: 20 f16 layer-0 fragments + 34 fp8 fragments) from the f32
-// inference weights; one thread per 16-byte unit of either image.
-// Threads 0..159 also assemble the per-layer scale words (lane r of layer l holds bytes e(l, 32 mb + r) + 127).
-__global__ void wide_pack_kernel(const float* __restrict__ w, int enc, const int32_t* __restrict__ exps,
-                                 _Float16* __restrict__ img16, uint8_t* __restrict__ img8,
-                                 uint32_t* __restrict__ scales) {
-    const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    constexpr int U16 = kWideF16Bytes / 16, U8 = kWide8Frags * 128;
-    if (u < 5 * 32) {
-        const int l = u / 32, rr = u % 32;
-        uint32_t word = 0;
-        for (int mb = 0; mb < 4; ++mb) word |= (uint32_t)(exps[l * 128 + 32 * mb + rr] + 127) << (8 * mb);
-        scales[u] = word;
-    }
-    if (u < U16) {
+// training images from the f32 master weights: forward (as the inference img16) and backward W_l^T fragments
+__device__ __forceinline__ void wide_pack_train_unit(const float* __restrict__ w, int enc,
+                                                     _Float16* __restrict__ fwd16, _Float16* __restrict__ bwd16, int u) {
+    constexpr int UF = kWideF16Frags * 64, UB = kWideBwdFrags * 64;
+    if (u < UF) {
         const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
         int layer, mb, kk;
         if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
@@ -1309,33 +1297,105 @@ __global__ void wide_pack_kernel(const float* __restrict__ w, int enc, const int
         for (int j = 0; j < 8; ++j) {
             float x = 0.0f;
             if (layer == 0) x = w[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
+            else if (layer < 5 || row < NRC_OUT_PADDED) x = w[wide_off(layer) + row * 128 + acc_row(kk, h, j)];
+            v[j] = (_Float16)x;
+        }
+        reinterpret_cast<h8*>(fwd16)[u] = v;
+    } else if (u < UF + UB) {
+        const int v8 = u - UF, f = v8 / 64, lane = v8 % 64, r = lane & 31, h = lane >> 5;
+        const int layer = f < 4 ? 5 : 1 + (f - 4) / 32, mb = f < 4 ? f : ((f - 4) % 32) / 8, kk = f < 4 ? 0 : (f - 4) % 8;
+        const int col = 32 * mb + r;  // row of W_l^T = input feature of layer l
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int row = acc_row(kk, h, j);  // output neuron of layer l
+            v[j] = (_Float16)w[wide_off(layer) + row * 128 + col];
+        }
+        reinterpret_cast<h8*>(bwd16)[v8] = v;
+    }
+}
+
+constexpr int kPackFp8Waves = 4 * 4 + 1;
+__global__ __launch_bounds__(256) void wide_pack_all_kernel(const float* __restrict__ wi, const float* __restrict__ wt,
+                                                            int enc, _Float16* __restrict__ img16,
+                                                            uint8_t* __restrict__ img8, uint32_t* __restrict__ scales,
+                                                            _Float16* __restrict__ fwd16, _Float16* __restrict__ bwd16) {
+    constexpr int UC = kPackFp8Waves * 64, U16 = kWideF16Bytes / 16, UF = kWideF16Frags * 64, UB = kWideBwdFrags * 64;
+    int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < UC) {
+        const int t = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
+        const int layer = t < 16 ? 1 + t / 4 : 5, mb = t < 16 ? t % 4 : 0;
+        const int row = 32 * mb + r;
+        const bool live = layer < 5 || row < NRC_OUT_PADDED;
+        const float* wr = wi + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;  // W5 rows follow W4's
+        float v[2][2][16];
+        float amax = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int plane = 0; plane < 2; ++plane)
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const float x = live ? wr[f8_row(s, h, 16 * plane + k)] : 0.0f;
+                    v[s][plane][k] = x;
+                    amax = fmaxf(amax, fabsf(x));
+                }
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        int e = 0;
+        if (amax > 0.0f) {
+            int E = 0;
+            const float M = frexpf(amax, &E);
+            e = M <= 0.875f ? E - 9 : E - 8;
+            e = max(-127, min(127, e));
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int plane = 0; plane < 2; ++plane) {
+                uint32_t wd[4];
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    float a[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        a[i] = live ? __builtin_amdgcn_fmed3f(ldexpf(v[s][plane][4 * d + i], -e), -448.0f, 448.0f)
+                                    : 0.0f;
+                    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+                    wd[d] = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], lo, true);
+                }
+                const int f = wide8_frag(layer, mb, s);
+                reinterpret_cast<u4*>(img8 + 20 * 1024)[f * 128 + plane * 64 + lane] = u4{wd[0], wd[1], wd[2], wd[3]};
+            }
+        // scale word of (layer, r): byte mb = E8M0 of row 32 mb + r (rows past W5's 16 outputs: exponent 0)
+        if (h == 0) {
+            if (layer < 5) reinterpret_cast<uint8_t*>(scales)[((layer - 1) * 32 + r) * 4 + mb] = (uint8_t)(e + 127);
+            else scales[4 * 32 + r] = (uint32_t)(e + 127) | (127u << 8) | (127u << 16) | (127u << 24);
+        }
+        return;
+    }
+    u -= UC;
+    if (u < U16) {
+        const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
+        int layer, mb, kk;
+        if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
+        else if (f < 148) { layer = 1 + (f - 20) / 32; mb = ((f - 20) % 32) / 8; kk = (f - 20) % 8; }
+        else { layer = 5; mb = 0; kk = f - 148; }
+        const int row = 32 * mb + r;
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float x = 0.0f;
+            if (layer == 0) x = wi[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
             else if (layer < 5 || row < NRC_OUT_PADDED)
-                x = w[NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128 + acc_row(kk, h, j)];
+                x = wi[NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128 + acc_row(kk, h, j)];
             v[j] = (_Float16)x;
         }
         reinterpret_cast<h8*>(img16)[u] = v;
         if (f < 20) reinterpret_cast<h8*>(img8)[u] = v;
-    } else if (u < U16 + U8) {
-        const int v8 = u - U16, f = v8 / 128, plane = (v8 / 64) % 2, lane = v8 % 64, r = lane & 31, h = lane >> 5;
-        const int layer = f < 32 ? 1 + f / 8 : 5, mb = f < 32 ? (f % 8) / 2 : 0, s = f < 32 ? f % 2 : f - 32;
-        const int row = 32 * mb + r;
-        const bool live = layer < 5 || row < NRC_OUT_PADDED;
-        const int e = live ? exps[(layer - 1) * 128 + row] : 0;
-        const float* wr = w + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;
-        uint32_t wd[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            float a[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = 16 * plane + 4 * d + i;
-                a[i] = live ? __builtin_amdgcn_fmed3f(ldexpf(wr[f8_row(s, h, j)], -e), -448.0f, 448.0f) : 0.0f;
-            }
-            const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
-            wd[d] = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], lo, true);
-        }
-        reinterpret_cast<u4*>(img8 + 20 * 1024)[v8] = u4{wd[0], wd[1], wd[2], wd[3]};
+        return;
     }
+    u -= U16;
+    if (u < UF + UB) wide_pack_train_unit(wt, enc, fwd16, bwd16, u);
 }
 
 // e4m3 conversion as the FP8 kernels do it (diagnostic entry for the exhaustive conversion test)
@@ -2288,17 +2348,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 //   wide_dw_kernel       dW_l = sum_s delta_l in_l^T as 32x32 tiles x 512-sample chunks (A and B fragments are
 //                        16-byte loads of those rows), partial sums per chunk in canonical parameter order;
 //   wide_adam_kernel     fixed-order chunk sum + tcnn Adam + EMA per parameter (same float operations as
-//                        adam_pack_one), then the f16 / FP8 images are repacked (launch_wide_pack, wide_pack_train).
+//                        adam_pack_one), then the f16 / FP8 images are repacked (wide_pack_all_kernel).
 // ------------------------------------------------------------------------------------------------
-__host__ __device__ constexpr int wide_bwd_frag(int layer, int mb, int kk) {
-    return layer == 5 ? mb : 4 + (layer - 1) * 32 + mb * 8 + kk;
-}
-__host__ __device__ constexpr int64_t wide_in_row(int layer) { return layer == 0 ? 0 : 80 + (layer - 1) * 128; }
-__host__ __device__ constexpr int64_t wide_d_row(int layer) { return (int64_t)layer * 128; }
-__host__ __device__ constexpr int wide_off(int layer) {
-    return layer == 0 ? NRC_WIDE_W0_OFFSET : layer <= 4 ? NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 : NRC_WIDE_W5_OFFSET;
-}
-
 // f16 B fragments (rows acc_row(kk, h, j)) -> ws[(row0 + row) * bpad + s]
 __device__ __forceinline__ void store_frag_rows(_Float16* __restrict__ ws, int64_t bpad, int64_t s, int h,
                                                 const h8 (&y)[8]) {
@@ -2582,40 +2633,6 @@ __global__ __launch_bounds__(256) void wide_adam_kernel(int mode, const float* _
     mb.infer[p] = e / ema_debias;
 }
 
-// training images from the f32 master weights: forward (img16, as wide_pack_kernel) and backward W_l^T fragments
-__global__ void wide_pack_train_kernel(const float* __restrict__ w, int enc, _Float16* __restrict__ fwd16,
-                                       _Float16* __restrict__ bwd16) {
-    const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    constexpr int UF = kWideF16Frags * 64, UB = kWideBwdFrags * 64;
-    if (u < UF) {
-        const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
-        int layer, mb, kk;
-        if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
-        else if (f < 148) { layer = 1 + (f - 20) / 32; mb = ((f - 20) % 32) / 8; kk = (f - 20) % 8; }
-        else { layer = 5; mb = 0; kk = f - 148; }
-        const int row = 32 * mb + r;
-        h8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float x = 0.0f;
-            if (layer == 0) x = w[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
-            else if (layer < 5 || row < NRC_OUT_PADDED) x = w[wide_off(layer) + row * 128 + acc_row(kk, h, j)];
-            v[j] = (_Float16)x;
-        }
-        reinterpret_cast<h8*>(fwd16)[u] = v;
-    } else if (u < UF + UB) {
-        const int v8 = u - UF, f = v8 / 64, lane = v8 % 64, r = lane & 31, h = lane >> 5;
-        const int layer = f < 4 ? 5 : 1 + (f - 4) / 32, mb = f < 4 ? f : ((f - 4) % 32) / 8, kk = f < 4 ? 0 : (f - 4) % 8;
-        const int col = 32 * mb + r;  // row of W_l^T = input feature of layer l
-        h8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int row = acc_row(kk, h, j);  // output neuron of layer l
-            v[j] = (_Float16)w[wide_off(layer) + row * 128 + col];
-        }
-        reinterpret_cast<h8*>(bwd16)[v8] = v;
-    }
-}
 
 // ------------------------------------------------------------------------------------------------
 // Ping-pong inference (variant 26). One wave owns two 32-query tiles A and B per iteration and runs them
@@ -2972,11 +2989,11 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
     }
 }
 
-hipError_t launch_wide_pack(const float* w, int enc, _Float16* img16, uint8_t* img8, uint32_t* scales, int32_t* exps,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(wide_row_exp_kernel, dim3(5 * 128 / 4), dim3(256), 0, s, w, exps);
-    constexpr int units = kWideF16Bytes / 16 + kWide8Frags * 128;
-    hipLaunchKernelGGL(wide_pack_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w, enc, exps, img16, img8, scales);
+hipError_t launch_wide_pack(const float* w_infer, const float* w_train, int enc, _Float16* img16, uint8_t* img8,
+                            uint32_t* scales, _Float16* fwd16, _Float16* bwd16, hipStream_t s) {
+    constexpr int units = kPackFp8Waves * 64 + kWideF16Bytes / 16 + (kWideF16Frags + kWideBwdFrags) * 64;
+    hipLaunchKernelGGL(wide_pack_all_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w_infer, w_train, enc, img16,
+                       img8, scales, fwd16, bwd16);
     return hipGetLastError();
 }
 
@@ -3057,11 +3074,6 @@ hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const flo
     return hipGetLastError();
 }
 
-hipError_t launch_wide_pack_train(const float* w, int enc, _Float16* fwd16, _Float16* bwd16, hipStream_t s) {
-    constexpr int units = (kWideF16Frags + kWideBwdFrags) * 64;
-    hipLaunchKernelGGL(wide_pack_train_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w, enc, fwd16, bwd16);
-    return hipGetLastError();
-}
 
 hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s) {
     if (n <= 0) return hipSuccess;
