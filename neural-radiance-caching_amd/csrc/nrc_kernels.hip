@@ -2350,13 +2350,31 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 //   wide_adam_kernel     fixed-order chunk sum + tcnn Adam + EMA per parameter (same float operations as
 //                        adam_pack_one), then the f16 / FP8 images are repacked (wide_pack_all_kernel).
 // ------------------------------------------------------------------------------------------------
-// f16 B fragments (rows acc_row(kk, h, j)) -> ws[(row0 + row) * bpad + s]
-__device__ __forceinline__ void store_frag_rows(_Float16* __restrict__ ws, int64_t bpad, int64_t s, int h,
+// f16 B fragments (rows acc_row(kk, h, j), sample s) -> ws[row * ld + s] with 4-byte stores: adjacent lanes
+// (samples 2p, 2p + 1) swap half of their 8 rows (one DPP quad_perm [1,0,3,2] per dword), so each lane holds 4 rows x
+// 2 samples and writes 4 words instead of 8 halves (wide_fwd_bwd_lds_kernel 67.4 -> 64.4 us per training step in
+// A/B; 8-byte stores after a second exchange with lane ^ 2: 65.1)
+__device__ __forceinline__ void store_frag_rows(_Float16* __restrict__ ws, int64_t ld, int64_t s, int h,
                                                 const h8 (&y)[8]) {
+    const bool odd = threadIdx.x & 1;
+    const int64_t s0 = s & ~(int64_t)1;
+    const int jb = odd ? 4 : 0;
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
+    for (int kk = 0; kk < 8; ++kk) {
+        const u4 d = __builtin_bit_cast(u4, y[kk]);  // (j0, j1), (j2, j3), (j4, j5), (j6, j7)
+        const uint32_t give0 = odd ? d.x : d.z, give1 = odd ? d.y : d.w;
+        const uint32_t keep0 = odd ? d.z : d.x, keep1 = odd ? d.w : d.y;
+        const uint32_t got0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)give0, 0xB1, 0xF, 0xF, false);
+        const uint32_t got1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)give1, 0xB1, 0xF, 0xF, false);
+        // sample s0 in the low half of each word, s0 + 1 in the high half
+        const uint32_t lo0 = odd ? got0 : keep0, hi0 = odd ? keep0 : got0;
+        const uint32_t lo1 = odd ? got1 : keep1, hi1 = odd ? keep1 : got1;
+        const uint32_t w[4] = {__builtin_amdgcn_perm(hi0, lo0, 0x05040100u), __builtin_amdgcn_perm(hi0, lo0, 0x07060302u),
+                               __builtin_amdgcn_perm(hi1, lo1, 0x05040100u), __builtin_amdgcn_perm(hi1, lo1, 0x07060302u)};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ws[(int64_t)acc_row(kk, h, j) * bpad + s] = y[kk][j];
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint32_t*>(ws + (int64_t)acc_row(kk, h, jb + i) * ld + s0) = w[i];
+    }
 }
 
 // Copy COUNT h8 (1-KiB fragments of 64 lanes) global -> LDS with LDS-DMA (global_load_lds_dwordx4: no VGPRs, all
