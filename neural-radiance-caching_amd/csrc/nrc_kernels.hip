@@ -3059,7 +3059,9 @@ int64_t wide_bpad(int64_t b) { return (b + 31) / 32 * 32; }
 // Workspace row stride: 32 samples (64 B) past bpad. With a power-of-two stride (bpad = 16,384 -> 32 KiB) the 32 rows
 // of one MFMA operand load all map to the same L2 channel; the pad spreads them (wide_dw_kernel 36.1 -> 28.8 us per
 // 16,384-sample step; pads of 8 / 16 / 48 / 64 / 128 / 160 samples measured 87.8 / 85.0 / 87.1 / 92.7 / 95 / 85 us
-// per step against 84.9 for 32 and 92.0 unpadded).
+// per step against 84.9 for 32 and 92.0 unpadded; later, with the other changes in: pads of 256 / 1,024 / 2,048
+// samples 70.9 us, 2,080 / 3,104 / 4,128 samples 63.4-64.4, 32 samples 63.1 -- the channel interleave is finer than
+// 512 B).
 int64_t wide_ld(int64_t b) { return wide_bpad(b) + 32; }
 int wide_chunks(int64_t b) { return (int)((wide_bpad(b) + kWideChunk - 1) / kWideChunk); }
 
