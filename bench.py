@@ -207,6 +207,22 @@ def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
         tf = FLOP_PER_QUERY_WIDE * nq / (kms * 1e-3) / 1e12
         res[name] = {"M_queries_per_s": world * nq * steps / float(wall.item()) / 1e6, "kernel_ms": kms,
                      "achieved_tflops": tf, "peak_tflops": peak, "frac": tf / peak}
+    if world == 1:
+        # the width-128 training step (16,384 samples: encode -> fwd -> loss -> bwd -> dW -> Adam/EMA -> repack)
+        B = nrc.BATCH_SIZE
+        tq, tt = nrc.synthetic.cornell_batch(4 * B, seed=nrc.synthetic.SEED + 1001)
+        tq, tt = torch.from_numpy(tq).to(dev), torch.from_numpy(tt).to(dev)
+        for i in range(4):
+            net.train(tq[i * B:], tt[i * B:])
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k = 4 * max(5, steps // 2)
+        ev0.record(stream)
+        for i in range(k):
+            net.train(tq[(i % 4) * B:], tt[(i % 4) * B:])
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        res["train_step_ms"] = ev0.elapsed_time(ev1) / k
     net.destroy()
     return res
 
