@@ -190,6 +190,25 @@ def test_wide_grad_matches_oracle(nrc, orc, dev, wnet):
         assert rel(g[offs[l]:offs[l + 1]], g_ref[offs[l]:offs[l + 1]]) <= 5e-3, l
 
 
+@pytest.mark.parametrize("b", [1000, 4000, 4001])
+def test_wide_grad_ragged_batch(nrc, orc, dev, wnet, b):
+    """Batches that are not a multiple of the 64-sample forward/backward block or of the 512-sample dW chunk: the
+    last block's second wave has no samples (b = 4000, 4001) and the last chunk is partial."""
+    import torch
+    net, enc = wnet
+    params = wide_params(24, gain=1.2)
+    net.set_state(nrc.StateSlot.PARAMS, params)
+    q, t = nrc.synthetic.cornell_batch(b, seed=64)
+    grad = torch.full((net.grad_floats,), 7.0, device=dev)  # stale contents must be overwritten
+    net.train_grad(_t(q, dev), _t(t, dev), b, b, grad)
+    torch.cuda.synchronize()
+    g = grad.cpu().numpy()
+    g_ref, l_ref = orc.wide_grad(params, q, t, mode=orc.MIXED, encoding=int(enc))
+    n = nrc.WIDE_NUM_PARAMS
+    assert rel(g[:n], g_ref) <= 2e-3, rel(g[:n], g_ref)
+    assert abs(g[n] - l_ref) <= 1e-3 * abs(l_ref)
+
+
 def test_wide_train_step_matches_oracle(nrc, orc, dev, wnet):
     import torch
     net, enc = wnet
