@@ -276,7 +276,7 @@ def main() -> None:
     grad = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
     trainer = nrc.dp.DataParallelTrainer(net, grad) if distributed else None
     if distributed:
-        trainer.broadcast_state(net.get_state, net.set_state, [nrc.StateSlot.PARAMS, nrc.StateSlot.INFER], dev)
+        trainer.broadcast_state(net, dev)
 
     def train_frame(fi: int) -> None:
         tq, tt = frames_q[fi % 4], frames_t[fi % 4]

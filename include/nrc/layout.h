@@ -21,7 +21,7 @@ extern "C" {
 #define NRC_NUM_BATCHES                    4
 #define NRC_NUM_TRAINING_RECORDS_PER_FRAME 65536
 #define NRC_BATCH_SIZE                     (NRC_NUM_TRAINING_RECORDS_PER_FRAME / NRC_NUM_BATCHES) /* 16384 */
-/* tcnn::BATCH_SIZE_GRANULARITY, used by NRCNetwork.cu:124-125, :147-148 */
+/* tcnn::BATCH_SIZE_GRANULARITY, used by NRCNetwork.cu:48-49, :72 */
 #define NRC_BATCH_SIZE_GRANULARITY         256
 
 /* ---- network I/O dims: neural_radiance_caching.h:33-41 (compact query) ---- */

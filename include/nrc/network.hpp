@@ -43,7 +43,7 @@ struct TrainingStat {
 class Network {
 public:
     Network() { check(nrc_create(&m_net)); }
-    ~Network() { nrc_free(m_net); }  // warns like NRCNetwork.cu:105-109 if destroy() was skipped
+    ~Network() { nrc_free(m_net); }  // warns like NRCNetwork.cu:29-33 if destroy() was skipped
     Network(const Network&) = delete;
     Network& operator=(const Network&) = delete;
 
@@ -107,7 +107,7 @@ private:
         if (s != NRC_OK) throw std::runtime_error(std::string("nrc: ") + nrc_last_error());
     }
     static void quiet(nrc_status s) {
-        if (s == NRC_ERR_DESTROYED) return;  // NRCNetwork.cu:119, :142
+        if (s == NRC_ERR_DESTROYED) return;  // NRCNetwork.cu:43, :66
         check(s);
     }
 

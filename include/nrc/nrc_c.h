@@ -9,7 +9,7 @@
  * Buffers are the reference's, byte for byte (include/nrc/layout.h): queries are packed 60-byte
  * RadianceQuery records (15 f32, 4-byte aligned), outputs and targets packed 12-byte float3.
  * All work is enqueued on a HIP stream and is asynchronous unless a host loss pointer is given
- * (that call blocks, as NRCNetwork.cu:130-131 does). A handle is not thread-safe.
+ * (that call blocks, as NRCNetwork.cu:54-55 does). A handle is not thread-safe.
  */
 #ifndef NRC_C_H
 #define NRC_C_H
@@ -27,8 +27,8 @@ extern "C" {
 
 typedef enum nrc_status {
     NRC_OK = 0,
-    NRC_ERR_INVALID_ARGUMENT = 1, /* std::invalid_argument in the reference (NRCNetworkConfigs.h:333-335) */
-    NRC_ERR_DESTROYED = 2,        /* call after destroy(): a silent no-op in the reference (NRCNetwork.cu:119, :142) */
+    NRC_ERR_INVALID_ARGUMENT = 1, /* std::invalid_argument in the reference (NRCNetworkConfigs.h:129-131) */
+    NRC_ERR_DESTROYED = 2,        /* call after destroy(): a silent no-op in the reference (NRCNetwork.cu:43, :66) */
     NRC_ERR_NOT_INITIALIZED = 3,
     NRC_ERR_HIP = 4,              /* HIP runtime failure (CU_CHECK -> std::runtime_error in the reference) */
     NRC_ERR_UNSUPPORTED = 5,
@@ -78,14 +78,14 @@ const char* nrc_last_error(void);
 nrc_config nrc_default_config(int encoding);
 
 /* Network() / ~Network() (NRCNetwork.h:22-24): allocate / free an empty handle. nrc_free on a handle
- * that was never destroyed prints the reference's warning (NRCNetwork.cu:105-109) and releases it. */
+ * that was never destroyed prints the reference's warning (NRCNetwork.cu:29-33) and releases it. */
 nrc_status nrc_create(nrc_net** out);
 nrc_status nrc_free(nrc_net* net);
 
-/* init<Verbose>(stream, encoding) (NRCNetwork.h:26-31, NRCNetwork.cu:182-188): set the stream,
+/* init<Verbose>(stream, encoding) (NRCNetwork.h:26-31, NRCNetwork.cu:106-112): set the stream,
  * select the encoding's config and (re)build the model with freshly initialised weights and
  * optimizer state. cfg may be NULL (reference defaults). verbose prints the config JSON
- * (printConfig_, NRCNetwork.cu:198-203). Re-init after destroy revives the handle. */
+ * (printConfig_, NRCNetwork.cu:122-127). Re-init after destroy revives the handle. */
 nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_config* cfg, int verbose);
 
 /* destroy() (NRCNetwork.h:41): release all device state; later calls return NRC_ERR_DESTROYED.
@@ -105,7 +105,7 @@ nrc_status nrc_train_batch(nrc_net* net, const float* inputs_d, const float* tar
 nrc_status nrc_train_async(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b, float* loss_d);
 
 /* infer(in, out, n) / infer(in, out, n, stream) (NRCNetwork.h:49-51). Processes exactly n queries
- * (the reference rounds n up to 256 and reads/writes past n, NRCNetwork.cu:147-148; this one never
+ * (the reference rounds n up to 256 and reads/writes past n, NRCNetwork.cu:72; this one never
  * touches the tail). n = 0 is a no-op. Uses the inference (EMA) weights. */
 nrc_status nrc_infer(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n);
 nrc_status nrc_infer_stream(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n, hipStream_t stream);
@@ -113,7 +113,10 @@ nrc_status nrc_infer_stream(nrc_net* net, const float* inputs_d, float* outputs_
 nrc_status nrc_set_stream(nrc_net* net, hipStream_t stream);           /* setStream (NRCNetwork.h:53) */
 nrc_status nrc_get_stream(const nrc_net* net, hipStream_t* stream);
 nrc_status nrc_set_hyper_params(nrc_net* net, const nrc_hyper_params* hp); /* setHyperParams (:55) */
-nrc_status nrc_set_config(nrc_net* net, int encoding);                 /* setConfig (:57): takes effect at next init */
+/* setConfig (:57, NRCNetwork.cu:96-99): like the reference it only replaces the config; on a live handle the
+ * model (encoding, weights, optimizer state, learning rate) is untouched and nrc_get_config_json reports the new
+ * encoding's default config. nrc_init always uses its own encoding argument. */
+nrc_status nrc_set_config(nrc_net* net, int encoding);
 nrc_status nrc_get_learning_rate(const nrc_net* net, float* lr);       /* getLearningRate (:61) */
 /* printConfig_ equivalent: the model config as JSON (tcnn's schema). Writes at most cap bytes incl. NUL;
  * *needed (optional) receives the full length + 1. */

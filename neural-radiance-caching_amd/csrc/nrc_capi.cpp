@@ -217,6 +217,7 @@ std::string config_json(int encoding, const nrc_config& c) {
 struct nrc_net {
     hipStream_t stream = nullptr;
     int encoding = NRC_ENCODING_FREQUENCY;
+    int config_encoding = NRC_ENCODING_FREQUENCY;  // what nrc_set_config last asked for (JSON only, see there)
     nrc_config cfg{};
     bool initialized = false;
     bool destroyed = false;
@@ -533,6 +534,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         net->release();
         net->stream = stream;
         net->encoding = encoding;
+        net->config_encoding = encoding;
         net->cfg = c;
         net->destroyed = false;
         net->step = 0;
@@ -736,8 +738,15 @@ nrc_status nrc_set_config(nrc_net* net, int encoding) {
         if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
         if (encoding != NRC_ENCODING_FREQUENCY && encoding != NRC_ENCODING_HASH && encoding != NRC_ENCODING_FREQUENCY_SH)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "Unsupported input encoding");
-        net->encoding = encoding;
-        net->cfg = nrc_default_config(encoding);
+        // The reference's setConfig only rewrites the config JSON (NRCNetwork.cu:96-99); the live model keeps its
+        // encoding, weights and optimizer state until the next init_ (:106-112), which re-derives the config from
+        // its own encoding argument. On a live handle this therefore changes only what nrc_get_config_json prints;
+        // the encoding, the hyper-parameters and every buffer layout the kernels depend on stay untouched.
+        net->config_encoding = encoding;
+        if (!net->initialized) {
+            net->encoding = encoding;
+            net->cfg = nrc_default_config(encoding);
+        }
     });
 }
 
@@ -752,7 +761,11 @@ nrc_status nrc_get_learning_rate(const nrc_net* net, float* lr) {
 nrc_status nrc_get_config_json(const nrc_net* net, char* buf, size_t cap, size_t* needed) {
     return guarded([&] {
         if (!net) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle");
-        const std::string s = config_json(net->encoding, net->cfg);
+        // after a setConfig on a live handle: the JSON of that encoding's default config (as the reference's
+        // printConfig_ would print it), otherwise the live model's config
+        const std::string s = net->config_encoding != net->encoding
+                                  ? config_json(net->config_encoding, nrc_default_config(net->config_encoding))
+                                  : config_json(net->encoding, net->cfg);
         if (needed) *needed = s.size() + 1;
         if (buf && cap) {
             const size_t k = s.size() < cap - 1 ? s.size() : cap - 1;

@@ -1,11 +1,11 @@
 // nrc_kernels.hip — gfx950 (CDNA4) kernels of the NRC query/train hot path.
 //
 // Replaces the tiny-cuda-nn calls the reference makes from /root/reference/nrc/src/NRCNetwork.cu:
-//   network->inference      (:152)  -> infer_kernel       (fused Composite encode + 64x5 MLP + cast)
-//   trainer->training_step  (:129)  -> train_kernel        (encode + fwd + RelativeL2Luminance + bwd +
+//   network->inference      (:76)    -> infer_kernel       (fused Composite encode + 64x5 MLP + cast)
+//   trainer->training_step  (:53)   -> train_kernel        (encode + fwd + RelativeL2Luminance + bwd +
 //                                                           per-block weight-gradient partials)
 //                                     reduce_adam_kernel  (fixed-order dW reduce + Adam + EMA + f16 repack)
-//   trainer->loss           (:131)  -> loss partials reduced in reduce_adam_kernel
+//   trainer->loss           (:55)   -> loss partials reduced in reduce_adam_kernel
 //
 // Design: every matmul is a chain of v_mfma_f32_32x32x16_f16 with samples on the MFMA
 // column (lane) axis and features on the row axis, so each layer's f32 accumulator converts in

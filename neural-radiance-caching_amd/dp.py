@@ -38,14 +38,24 @@ class DataParallelTrainer:
         self.group = group
         self._dist = dist
 
-    def broadcast_state(self, get_state, set_state, slots, device) -> None:
-        """Make every replica start from rank 0's state (weights, EMA, Adam moments)."""
+    def broadcast_state(self, net, device) -> None:
+        """Make every replica continue from rank 0's complete optimizer state: the five state slots (weights, the
+        inference/EMA weights, the raw EMA, Adam m and v) and the Adam step counter, which sets the bias
+        corrections of the next step. InputEncoding::Hash also keeps a step counter per grid entry that the C-ABI
+        does not export, so for a Hash network this is only allowed before the first step (all counters 0)."""
         import torch
 
-        for slot in slots:
-            t = torch.from_numpy(get_state(slot)).to(device)
+        from .network import InputEncoding, StateSlot
+
+        step = torch.tensor([int(net.step)], dtype=torch.int64, device=device)
+        self._dist.broadcast(step, src=0, group=self.group)
+        if getattr(net, "encoding", None) == InputEncoding.Hash and int(step.item()) != 0:
+            raise RuntimeError("broadcast_state: a Hash network can only be synchronised before its first step")
+        for slot in StateSlot:
+            t = torch.from_numpy(net.get_state(slot)).to(device)
             self._dist.broadcast(t, src=0, group=self.group)
-            set_state(slot, t.cpu().numpy())
+            net.set_state(slot, t.cpu().numpy())
+        net.step = int(step.item())
 
     def step(self, inputs, targets, b_local: int, global_b: int, loss: bool = False):
         self.backend.train_grad(inputs, targets, b_local, global_b, self.grad)

@@ -17,10 +17,10 @@ reference (NRCNetwork.h)               here
 ``setConfig`` / ``getLearningRate``    ``setConfig`` / ``getLearningRate``
 =====================================  =========================================================
 
-As in the reference (NRCNetwork.cu:119, :142), ``train`` / ``infer`` after ``destroy()`` are silent
+As in the reference (NRCNetwork.cu:43, :66), ``train`` / ``infer`` after ``destroy()`` are silent
 no-ops; the C-ABI reports them as ``NRC_ERR_DESTROYED``. Buffers are device pointers: a CUDA
 (HIP) ``torch.Tensor`` (float32, contiguous) or a raw integer address. ``train`` consumes exactly
-``BATCH_SIZE`` = 16384 samples (NRCNetwork.cu:127-128).
+``BATCH_SIZE`` = 16384 samples (NRCNetwork.cu:51-52).
 """
 from __future__ import annotations
 
@@ -106,6 +106,7 @@ class Network:
         s = _stream_ptr(stream)
         cfg = ctypes.byref(config) if config is not None else None
         check(self._lib.nrc_init(self._h, s, int(encoding), cfg, int(bool(verbose))))
+        self.encoding = InputEncoding(int(encoding))
 
     def destroy(self) -> None:
         check(self._lib.nrc_destroy(self._h))
@@ -189,13 +190,17 @@ class Network:
     # ---- extensions: any batch size, data-parallel split, state ---------------------------
     def train_batch(self, inputs, targets, b: int, loss: bool = False):
         lh = ctypes.c_float(float("nan"))
-        check(self._lib.nrc_train_batch(self._h, _dev_ptr(inputs, "inputs"), _dev_ptr(targets, "targets"), int(b),
+        b = int(b)
+        check(self._lib.nrc_train_batch(self._h, _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None),
+                                        _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None), b,
                                         ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
     def train_grad(self, inputs, targets, b: int, global_b: int, grad) -> None:
-        check(self._lib.nrc_train_grad(self._h, _dev_ptr(inputs, "inputs") if b else None,
-                                       _dev_ptr(targets, "targets") if b else None, int(b), int(global_b),
+        b = int(b)
+        check(self._lib.nrc_train_grad(self._h, _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None) if b else None,
+                                       _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None,
+                                       b, int(global_b),
                                        _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None)))
 
     def train_apply(self, grad, loss: bool = False):
@@ -254,8 +259,8 @@ def encode(inputs, encoded, n: int, stream=None) -> None:
 
 def default_config(encoding: InputEncoding = InputEncoding.Frequency, width: int = 64,
                    infer_precision: int = 0) -> NrcConfig:
-    """The reference's hyper-parameters for an encoding; width 128 / infer_precision PRECISION_FP8 select the
-    BASELINE configs[4] network (inference-only in this build)."""
+    """The reference's hyper-parameters for an encoding; width 128 selects the BASELINE configs[4] network (f16
+    training and inference), infer_precision PRECISION_FP8 its FP8 inference path (training stays f16)."""
     c = lib().nrc_default_config(int(encoding))
     c.width = int(width)
     c.infer_precision = int(infer_precision)

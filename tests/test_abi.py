@@ -46,6 +46,11 @@ def test_library_loads_and_host_entry_points(nrc):
     assert L.nrc_get_learning_rate(h, ctypes.byref(lr)) == 3
     assert L.nrc_set_config(h, 7) == 1  # std::invalid_argument("Unsupported input encoding")
     assert b"Unsupported input encoding" in L.nrc_last_error()
+    assert L.nrc_set_config(h, 1) == 0 and L.nrc_last_error() == b""
+    need = ctypes.c_size_t()
+    assert L.nrc_get_config_json(h, None, 0, ctypes.byref(need)) == 0
+    buf = ctypes.create_string_buffer(need.value)
+    assert L.nrc_get_config_json(h, buf, need.value, None) == 0 and b"HashGrid" in buf.value
     assert L.nrc_set_config(h, 0) == 0 and L.nrc_last_error() == b""
     need = ctypes.c_size_t()
     assert L.nrc_get_config_json(h, None, 0, ctypes.byref(need)) == 0

@@ -51,6 +51,23 @@ class OracleBackend:
         self.st.apply(grad[: self.st.params.size].numpy().astype(np.float32))
         return float(grad[self.st.params.size]) if loss else None
 
+    # state access with nrc_amd.Network's names (StateSlot order: PARAMS, INFER, EMA, ADAM_M, ADAM_V)
+    _SLOTS = ("params", "infer", "ema", "m", "v")
+
+    def get_state(self, slot):
+        return getattr(self.st, self._SLOTS[int(slot)]).copy()
+
+    def set_state(self, slot, values):
+        setattr(self.st, self._SLOTS[int(slot)], np.array(values, dtype=np.float32))
+
+    @property
+    def step(self):
+        return self.st.step
+
+    @step.setter
+    def step(self, v):
+        self.st.step = int(v)
+
 
 def _free_port() -> int:
     with socket.socket() as s:
@@ -136,3 +153,41 @@ def test_dp_step_equals_single_process_step_hash(tmp_path):
     moved, moved_ref = p0[M:] != _init_params(orc, True)[M:], st.params[M:] != _init_params(orc, True)[M:]
     assert moved_ref.sum() > 1000 and np.mean(moved == moved_ref) >= 0.9999
     np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
+
+
+def _bcast_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nrc = nrc_loader.load()
+    orc = nrc_loader.load_oracle()
+    backend = OracleBackend(orc.init_params(1337))
+    trainer = nrc.dp.DataParallelTrainer(backend, torch.zeros(backend.grad_floats))
+    # the replicas diverge first: different local steps (different moments, EMA and step counters)
+    for it in range(rank + 1):
+        q, t = nrc.synthetic.cornell_batch(128, seed=70 + 10 * rank + it)
+        backend.train_grad(q, t, 128, 128, trainer.grad)
+        backend.train_apply(trainer.grad)
+    trainer.broadcast_state(backend, "cpu")
+    # one more synchronised DP step from the broadcast state
+    q, t = nrc.synthetic.cornell_batch(256, seed=99)
+    s, c = nrc.dp.shard_range(256, rank, world)
+    trainer.step(q[s:s + c], t[s:s + c], c, 256)
+    for slot in range(5):
+        np.save(os.path.join(out_dir, f"slot{slot}_{rank}.npy"), backend.get_state(slot))
+    np.save(os.path.join(out_dir, f"step_{rank}.npy"), np.array([backend.step]))
+    dist.destroy_process_group()
+
+
+def test_broadcast_state_syncs_every_slot_and_the_step(tmp_path):
+    """after broadcast_state every replica holds rank 0's weights, EMA, Adam moments and step counter,
+    so the next data-parallel step keeps them bit-identical even when they had diverged before."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_bcast_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for slot in range(5):
+        np.testing.assert_array_equal(np.load(tmp_path / f"slot{slot}_0.npy"), np.load(tmp_path / f"slot{slot}_1.npy"))
+    assert int(np.load(tmp_path / "step_0.npy")[0]) == int(np.load(tmp_path / "step_1.npy")[0]) == 2

@@ -275,6 +275,62 @@ def test_train_step_matches_oracle_and_learns(nrc, orc, torch, dev, net, golden)
     assert losses[-1] < losses[0]
 
 
+def test_set_hyper_params_changes_the_step(nrc, orc, torch, dev, net, golden):
+    """setHyperParams (NRCNetwork.cu:90-94, changed at runtime from the GUI, Application.cpp:1032) takes effect on
+    the next step: 2 steps at the default LR 1e-3, LR -> 5e-4, 2 more steps; the oracle runs the same schedule."""
+    params = golden["params_b"]
+    net.set_state(nrc.StateSlot.PARAMS, params)
+    st = orc.AdamEmaState(params)
+    for it in range(4):
+        if it == 2:
+            net.setHyperParams(nrc.HyperParams(learningRate=5e-4))
+            st.lr = 5e-4
+            assert abs(net.getLearningRate() - 5e-4) < 1e-12
+        q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=900 + it)
+        net.train(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np))
+        g, _ = orc.grad(st.params, q_np, t_np, mode=orc.MIXED)
+        st.apply(g)
+    p_gpu = net.get_state(nrc.StateSlot.PARAMS)
+    assert rel(p_gpu, st.params) <= 1e-3
+    assert rel(net.get_state(nrc.StateSlot.INFER), st.infer) <= 1e-3
+    # and the LR change is visible in the update itself: the same 4-step schedule at a constant 1e-3 lands elsewhere
+    st_const = orc.AdamEmaState(params)
+    for it in range(4):
+        q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=900 + it)
+        g, _ = orc.grad(st_const.params, q_np, t_np, mode=orc.MIXED)
+        st_const.apply(g)
+    d_sched = np.abs(p_gpu - st.params).max()
+    d_const = np.abs(p_gpu - st_const.params).max()
+    assert d_const > 20 * d_sched, (d_sched, d_const)
+
+
+def test_set_config_on_a_live_handle_keeps_the_model(nrc, orc, torch, dev, net, golden):
+    """setConfig only replaces the config (NRCNetwork.cu:96-99): a live Frequency network that is asked for the Hash
+    config keeps inferring and training as the Frequency oracle, with its learning rate."""
+    import json
+
+    params = golden["params_b"]
+    net.set_state(nrc.StateSlot.PARAMS, params)
+    net.set_state(nrc.StateSlot.INFER, params)
+    net.setHyperParams(nrc.HyperParams(learningRate=7e-4))
+    net.setConfig(nrc.InputEncoding.Hash)
+    assert abs(net.getLearningRate() - 7e-4) < 1e-12
+    assert json.loads(net.config_json())["encoding"]["nested"][0]["otype"] == "HashGrid"
+    q_np = nrc.synthetic.cornell_queries(3000, seed=31)
+    y = run_infer(nrc, torch, dev, net, q_np)
+    assert rel(y, orc.forward(params, q_np, orc.MIXED)) <= 1e-3
+    st = orc.AdamEmaState(params, lr=7e-4)
+    q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=32)
+    net.train(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np))
+    g, _ = orc.grad(st.params, q_np, t_np, mode=orc.MIXED)
+    st.apply(g)
+    assert rel(net.get_state(nrc.StateSlot.PARAMS), st.params) <= 1e-3
+    assert net.num_params == nrc.NUM_PARAMS
+    # the next init uses its own encoding argument, as init_ does (NRCNetwork.cu:106-112)
+    net.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Frequency)
+    assert json.loads(net.config_json())["encoding"]["nested"][0]["otype"] == "TriangleWave"
+
+
 def test_training_is_deterministic(nrc, torch, dev, golden):
     q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=8)
     states = []
@@ -305,7 +361,7 @@ def test_error_behaviour(nrc, torch, dev):
     n.destroy()
     n.destroy()
     x = torch.zeros(16 * 15, device=dev)
-    assert n.infer(x, x, 16) is None  # silent after destroy, like NRCNetwork.cu:142
+    assert n.infer(x, x, 16) is None  # silent after destroy, like NRCNetwork.cu:66
     n.init(stream=torch.cuda.current_stream())  # re-init revives (Device.cpp:2415-2421)
     n.destroy()
 
