@@ -13,7 +13,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import platform
 import sys
 import time
 from pathlib import Path
@@ -57,11 +56,16 @@ def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train
     """The naive C oracle (FP32, scalar loops) on the host cores, bounded sample of the workload. Its first pass over
     the frame doubles as the checker of the timed GPU inference (gpu_out: the bench's last output buffer)."""
     orc = nrc_loader.load_oracle()
-    threads = orc.default_threads()
+    threads, cores_how = orc.host_cores()
+    # configs[0] (C1): the FP32 forward of 4096 queries on every host core (best of 3 after one warm-up)
     n = 4096
-    t0 = time.perf_counter()
     orc.forward(params, queries[:n], orc.FP32, threads)
-    dt = time.perf_counter() - t0
+    c1 = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        orc.forward(params, queries[:n], orc.FP32, threads)
+        c1.append(time.perf_counter() - t0)
+    dt = min(c1)
     # whole passes over the frame while they fit the budget, then a partial pass to reach ~target_s
     want = int(max(n, n * target_s / max(dt, 1e-6)))
     total = 0
@@ -92,10 +96,13 @@ def cpu_baseline(queries: np.ndarray, params: np.ndarray, target_s: float, train
     orc.AdamEmaState(params).apply(g)
     dt2 = time.perf_counter() - t2
     return {"value": total / dt / 1e6, "unit": "M queries/s", "cores": threads, "kind": "port",
+            "cpu_model": orc.cpu_model(), "cores_how": cores_how,
             "sample": f"{total} queries ({total / len(queries):.2f} passes over the {len(queries)}-query "
                       f"Cornell frame), oracle/nrc_oracle.c FP32 forward, "
-                      f"{threads} pthreads on {platform.processor() or platform.machine()} "
-                      f"({os.cpu_count()} logical CPUs visible), {dt:.1f} s",
+                      f"{threads} pthreads on {orc.cpu_model()} "
+                      f"({os.cpu_count()} logical CPUs on the host; {cores_how}), {dt:.1f} s",
+            "c1_ms": min(c1) * 1e3,
+            "c1_what": f"configs[0]: FP32 forward of 4096 Cornell queries, {threads} pthreads, best of 3",
             "value_1thread": n1 / dt1 / 1e6, "sample_1thread": f"{n1} queries on 1 thread, {dt1:.2f} s",
             "train_step_ms": dt2 * 1e3,
             "sample_train": f"one {len(tq)}-sample step: FP32 encode+fwd+loss+bwd ({threads} pthreads) + Adam/EMA",

@@ -152,6 +152,10 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
  * results are identical in meaning to nrc_infer_stream. */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
                                    hipStream_t stream);
+/* Diagnostic: after a launch of a clocked inference variant (31, 32, 34, 36, 38), per wave 6 uint64: s_memtime cycles
+ * of its persistent loop, s_memrealtime (100 MHz) at loop start, at loop end and at wave start, HW_ID, XCC_ID:
+ * 6 * *waves values into host_dst (at most cap_waves waves). */
+nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, uint32_t* waves);
 /* Diagnostic: the training fwd/bwd kernel with s_memtime phase stamps (16 uint64 per 128-sample block
  * written to stamps_d); performs no optimizer step. */
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
@@ -175,7 +179,8 @@ nrc_status nrc_debug_encode_fast(const float* inputs_d, float* encoded_d, uint32
 /* The production encoder of the handle's configured encoding, f32 canonical order: Frequency / FrequencySH [n][80],
  * Hash [n][64] (with the inference (EMA) grid table). */
 nrc_status nrc_debug_encode_net(nrc_net* net, const float* inputs_d, float* encoded_d, uint32_t n, hipStream_t stream);
-/* encoder variants: 0 = production (as nrc_debug_encode_fast), 1 = omod doubling-chain triangle wave */
+/* encoder variants: 0 = encode_fast, 1 = omod doubling-chain triangle wave, 2 = encoder v3 (tent-map triangle
+ * wave, clamped OneBlob wrap) */
 nrc_status nrc_debug_encode_fast_variant(int variant, const float* inputs_d, float* encoded_d, uint32_t n,
                                          hipStream_t stream);
 

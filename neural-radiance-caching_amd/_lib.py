@@ -37,7 +37,7 @@ EXPORTS = [
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
-    "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_train_stamps", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
+    "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
     "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         "nrc_set_step": (st, [vp, u32]),
         "nrc_encode": (st, [fp, fp, u32, vp]),
         "nrc_debug_infer_variant": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
+        "nrc_debug_read_infer_clock": (st, [vp, u32, ctypes.POINTER(u32)]),
         "nrc_debug_train_stamps": (st, [vp, fp, fp, u32, vp]),
         "nrc_debug_infer_stamps": (st, [vp, fp, fp, u32, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "nrc_debug_encode_fast": (st, [fp, fp, u32, vp]),

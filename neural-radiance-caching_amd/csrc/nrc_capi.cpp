@@ -234,9 +234,12 @@ struct nrc_net {
     float* loss_partials = nullptr;
     // minibatch-loss slots: host-mapped fine-grained (coherent) pinned memory written directly by the reduce/Adam
     // kernels, so reading a loss back costs one stream sync and no D2H copy launch (the copy was ~4.5 us)
+    uint32_t* work_queue = nullptr;  // inference work-queue counters {next tile, finished waves}; zero between launches
     float* loss_dev = nullptr;   // device view of loss_host
     float* loss_host = nullptr;
     void alloc_loss_slots() {
+        HIP_CHECK(hipMalloc(&work_queue, 256));
+        HIP_CHECK(hipMemset(work_queue, 0, 256));
         HIP_CHECK(hipHostMalloc(&loss_host, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_CHECK(hipHostGetDevicePointer((void**)&loss_dev, loss_host, 0));
         for (int i = 0; i < 4; ++i) loss_host[i] = 0.0f;
@@ -277,6 +280,8 @@ struct nrc_net {
         f(wf_train); f(wb_train); f(wf_infer);
         f(fwd_pos); f(bwd_pos); f(slab_param);
         f(slabs); f(loss_partials);  // loss_dev aliases loss_host (freed below)
+        f(work_queue);
+        work_queue = nullptr;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer);
         f(scatter.pos); f(scatter.dy);
         scatter = HashScatter{};
@@ -913,7 +918,17 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
         if (variant < 0 || variant >= kNumInferVariants) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown variant");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
-        HIP_CHECK(launch_infer_variant(variant, in, out, n, net->wf_infer, stream));
+        HIP_CHECK(launch_infer_variant(variant, in, out, n, net->wf_infer, stream, net->work_queue));
+    });
+}
+
+nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, uint32_t* waves) {
+    return guarded([&] {
+        if (!host_dst || !waves) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
+        int64_t w = 0;
+        HIP_CHECK(hipDeviceSynchronize());
+        HIP_CHECK(read_infer_clock(host_dst, (int64_t)cap_waves, &w));
+        *waves = (uint32_t)w;
     });
 }
 
@@ -986,10 +1001,10 @@ nrc_status nrc_debug_encode_fast(const float* in, float* enc, uint32_t n, hipStr
 
 nrc_status nrc_debug_encode_fast_variant(int variant, const float* in, float* enc, uint32_t n, hipStream_t stream) {
     return guarded([&] {
-        if (variant != 0 && variant != 1) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "encoder variant must be 0 or 1");
+        if (variant < 0 || variant > 2) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "encoder variant must be 0, 1 or 2");
         if (n == 0) return;
         if (!in || !enc) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
-        HIP_CHECK(launch_encode_fast(in, enc, n, stream, variant == 1));
+        HIP_CHECK(launch_encode_fast(in, enc, n, stream, variant));
     });
 }
 

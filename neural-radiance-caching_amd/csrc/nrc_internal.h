@@ -130,9 +130,12 @@ hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, h
 
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
+// wq: the handle's work-queue counters (2 x u32, zero between launches), needed by the queue variants (37, 38)
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
-                                hipStream_t s);
-constexpr int kNumInferVariants = 29;
+                                hipStream_t s, uint32_t* wq = nullptr);
+constexpr int kNumInferVariants = 41;
+// per-wave (cycles, 100 MHz ticks) of the last clocked variant launch (31, 32)
+hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves);
 // inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
@@ -145,7 +148,7 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
                            float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
 hipError_t launch_encode_sh(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
-hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, bool chain = false);
+hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, int variant = 0);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.
 hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int64_t b, float n_total,
                                 float loss_scale, const _Float16* wf, const _Float16* wb, float* slabs,

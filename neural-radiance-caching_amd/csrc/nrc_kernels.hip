@@ -405,6 +405,83 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Encoder v3 (round 2): fewer VALU for the same 40 K slots per lane half (slot map unchanged, slot_feature()).
+//
+// TriangleWave by the tent map. With x_k = 2 frac(2^k u) - 1, tri_k = |x_k| and x_{k+1} = 2 |x_k| - 1 (doubling a
+// point of the period-1 triangle wave folds it: frac(2^(k+1) u) = 2 frac(2^k u) - [frac(2^k u) >= 1/2]), so each
+// further octave is ONE v_fma_f32 with an |.| input modifier, and |x_k| is the cvt's input modifier: 1.5 VALU per
+// feature instead of 2.5 (fract, subtract, half a cvt). x_0 = 2 frac(|u|) - 1 (the wave is even). Rounding: 2|x| - 1
+// is exact unless |x| < 1/4, where it rounds by <= 2^-25; the doubling carries an error e to 2e, so after the five
+// steps of a lane half the features are within 2^-19 (1.9e-6) absolute of the directly evaluated wave.
+//
+// OneBlob with the wrap folded into two clamps. The closed form of blob_fast puts the masses A, B - A, 1 - B of the
+// intervals j0 = floor(4x) - 1 .. j0 + 2 into bins (j0 + i) & 3; tcnn's formula sends an interval outside
+// [-4, 7] to bin 3 instead. For t = 4x clamped to [-5, 8] that is exactly: A -> 0 when t < -4, A -> 1 when t >= 8,
+// B -> 1 when t >= 7 (every other out-of-range case is equivalent to one of these at the clamp ends), i.e. a med3 of
+// A and a max of B against step functions of t; the masses are rotated into place as before. The reference feeds
+// raw angles (theta in [0, pi], phi in (-pi, pi]) to OneBlob, so Cornell waves always take the wrap: this replaces
+// blob_many's wave-uniform branch (~25 extra VALU per input on the wrap side) by ~6 VALU per input on one path.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float tent_step(float x) { return __builtin_fmaf(__builtin_fabsf(x), 2.0f, -1.0f); }
+
+__device__ __forceinline__ float step01(float t, float edge) {  // 1 for t >= edge, else 0 (t, edge on the 2^-21 grid)
+    return __builtin_amdgcn_fmed3f(__builtin_fmaf(t, 0x1p21f, 1.0f - edge * 0x1p21f), 0.0f, 1.0f);
+}
+
+__device__ __forceinline__ void blob_v3(float x, uint32_t& lo, uint32_t& hi) {
+    const float t = __builtin_amdgcn_fmed3f(x * 4.0f, -5.0f, 8.0f);
+    const float fr = __builtin_amdgcn_fractf(t);
+    uint32_t sh;  // 16 * ((floor(t) - 1) & 3) in the low 6 bits: v_cvt_flr_i32_f32 + v_lshl_add_u32 (the compiler
+                  // emits floor + cvt + shift + add for the C form)
+    asm("v_cvt_flr_i32_f32 %0, %1\n\tv_lshl_add_u32 %0, %0, 4, 48" : "=&v"(sh) : "v"(t));
+    const float fr2 = fr * fr;
+    float A = fmaf(-fr, fmaf(fr2, fmaf(fr2, 3.0f / 16.0f, -10.0f / 16.0f), 15.0f / 16.0f), 0.5f);
+    const float w = 1.0f - fr;
+    const float w2 = w * w;
+    float B = fmaf(w, fmaf(w2, fmaf(w2, 3.0f / 16.0f, -10.0f / 16.0f), 15.0f / 16.0f), 0.5f);
+    A = __builtin_amdgcn_fmed3f(A, step01(t, 8.0f), step01(t, -4.0f));
+    B = fmaxf(B, step01(t, 7.0f));
+    const float M1 = B - A, M2 = 1.0f - B;
+    const uint64_t v = (uint64_t)pk2(A, M1) | ((uint64_t)pk2(M2, 0.0f) << 32);
+    const uint64_t r = (v << (sh & 63u)) | (v >> ((64u - sh) & 63u));
+    lo = (uint32_t)r;
+    hi = (uint32_t)(r >> 32);
+}
+
+__device__ __forceinline__ void encode_v3(const QLane& Q, int h, h8 (&x)[5]) {
+    uint32_t w[20];
+    const float hs = h ? 64.0f : 1.0f;  // octaves 6..11 for the upper half
+    const float p[3] = {Q.p0 * hs, Q.p1 * hs, Q.p2 * hs};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        float g[6];
+        g[0] = fmaf(__builtin_amdgcn_fractf(__builtin_fabsf(p[d])), 2.0f, -1.0f);
+#pragma unroll
+        for (int k = 1; k < 6; ++k) g[k] = tent_step(g[k - 1]);
+#pragma unroll
+        for (int k = 0; k < 6; k += 2) w[(d * 6 + k) >> 1] = pk2_abs(g[k], g[k + 1]);
+    }
+    blob_v3(Q.b0, w[9], w[10]);
+    blob_v3(Q.b1, w[11], w[12]);
+    blob_v3(Q.b2, w[13], w[14]);
+    w[15] = pk2(Q.i0, Q.i1);
+    w[16] = pk2(Q.i2, 1.0f);
+    w[17] = w[18] = w[19] = 0x3C003C00u;  // pad features = 1.0
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+        typedef uint32_t w4 __attribute__((ext_vector_type(4)));
+        w4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
+        x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
+// Diagnostic clock of the inference kernels (ABL & 512): per wave (s_memtime cycles of the persistent loop, the
+// s_memrealtime 100 MHz ticks at loop start, loop end and wave start, HW_ID and XCC_ID), read back by
+// nrc_debug_read_infer_clock.
+constexpr int kInferClockWavesMax = 8192;
+__device__ uint64_t g_infer_clock[6 * kInferClockWavesMax];
+
+// ------------------------------------------------------------------------------------------------
 // HashGrid (InputEncoding::Hash, NRCNetworkConfigs.h:94-103; spec in oracle/nrc_hash_oracle.c): lane half h
 // encodes levels 8h..8h+7 of its query. Table: f16 [entry][2] (one 4-B half2 gather per corner).
 // ------------------------------------------------------------------------------------------------
@@ -422,6 +499,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base, 
 __device__ __forceinline__ int tile_rows(int64_t n, int64_t s0) {
     const int64_t left = n - s0;
     return (int)(left >= 32 ? 32 : left > 0 ? left : 0);
+}
+
+// A tile's 32 RadianceQuery rows (60 B each) through raw buffer loads: the descriptor (scalar: tile base, valid rows)
+// returns 0 past n, so there is no per-lane clamp or 64-bit address arithmetic; vo = this lane's constant byte
+// offsets of its three 12-byte pieces (position, OneBlob inputs 3+3h.., Identity inputs 9+3h..).
+struct QOffsets {
+    int p, b, i;
+};
+__device__ __forceinline__ QLane load_q_tile(const float* __restrict__ q, int64_t n, int64_t tile, const QOffsets& vo) {
+    typedef float f3 __attribute__((ext_vector_type(3)));
+    const int64_t s0 = tile * 32;
+    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(q + s0 * NRC_INPUT_DIMS, tile_rows(n, s0) * (NRC_INPUT_DIMS * 4));
+    // whole-vector bit_casts (clang 22 element bit_cast bug, see infer_v2_body)
+    const f3 a = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.p, 0, 0));
+    const f3 b = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.b, 0, 0));
+    const f3 c = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.i, 0, 0));
+    QLane Q;
+    Q.p0 = a.x; Q.p1 = a.y; Q.p2 = a.z;
+    Q.b0 = b.x; Q.b1 = b.y; Q.b2 = b.z;
+    Q.i0 = c.x; Q.i1 = c.y; Q.i2 = c.z;
+    Q.x3 = 0.0f;
+    return Q;
 }
 
 // element i (0..3) of a 16-byte load, by named components (see the bit_cast note in infer_v2_body)
@@ -755,6 +854,7 @@ struct InferEpilogue {
     int64_t n_acc;
     float w;           // 1 / (iterationIndex + 1)
     uint64_t* stamps = nullptr;  // diagnostic build only (ABL & 256): per-wave phase cycle sums
+    uint32_t* wq = nullptr;      // ABL & 4096: the handle's work-queue counters {next tile, finished waves}, zero at launch
 };
 
 
@@ -765,26 +865,75 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
                                               const h8* __restrict__ wf, const InferEpilogue& epi,
                                               const uint32_t* __restrict__ grid = nullptr) {
     constexpr int KK0 = ENC == 1 ? 4 : 5;
+    uint64_t rstart = 0;
+    if constexpr ((ABL & 512) != 0) rstart = __builtin_amdgcn_s_memrealtime();
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
     // ABL & 8: per-wave staging of a tile's 32 x 12-B results so they leave as 24 contiguous 16-B stores
     __shared__ __attribute__((aligned(16))) float ostage[(ABL & 8) ? THREADS / 64 : 1][96];
+    // ABL & 2048: a per-block work queue in LDS. With a fixed share of tiles per wave, the waves that share a SIMD do
+    // not progress at the same rate (the oldest wave issues first): at 2^21 queries the first waves finished their 16
+    // tiles at 36 us and the last at 82 us, the SIMDs running the tail at 1-2 waves. The block takes a contiguous
+    // range of tiles and its waves draw the next tile from an LDS counter, so every SIMD stays loaded to the end.
+    __shared__ uint32_t wq_next;
     if constexpr ((ABL & 16) != 0) fp32_flush_output_denorms();
+    if constexpr ((ABL & 2048) != 0) {
+        if (threadIdx.x == 0) wq_next = 0;
+    }
     copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const int h = lane >> 5, r = lane & 31;
     const bool out16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-    const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
-    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
+    const int64_t ngroups_all = (((n + 31) >> 5) + TILES - 1) / TILES;
+    int64_t ngroups = ngroups_all, wstride = (int64_t)gridDim.x * (THREADS / 64), gbase = 0;
     // wave-uniform tile index (readfirstlane: scalar address arithmetic, scalar buffer descriptors)
     int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (g >= ngroups) return;
+    auto draw = [&]() -> int64_t {  // next tile of this block's range (ABL & 2048) / of the launch (ABL & 4096)
+        uint32_t t = 0;
+        if constexpr ((ABL & 4096) != 0) {
+            if (lane == 0) t = __hip_atomic_fetch_add(epi.wq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) t = atomicAdd(&wq_next, 1u);
+        }
+        return gbase + (int64_t)__builtin_amdgcn_readfirstlane(t);
+    };
+    // ABL & 4096: one queue for the whole launch (tiles balance across CUs and XCDs too). Every wave draws until its
+    // draw fails, then counts itself finished; the last wave to finish (all draws of the launch are done by then)
+    // zeroes both counters, so the next launch on the stream starts from an empty queue.
+    auto finish = [&]() {
+        if constexpr ((ABL & 4096) != 0) {
+            if (lane == 0) {
+                const uint32_t total = gridDim.x * (THREADS / 64);
+                if (__hip_atomic_fetch_add(epi.wq + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+                    __hip_atomic_store(epi.wq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(epi.wq + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    };
+    if constexpr ((ABL & 2048) != 0 && (ABL & 4096) == 0) {
+        gbase = (int64_t)blockIdx.x * ngroups_all / gridDim.x;
+        ngroups = (int64_t)(blockIdx.x + 1) * ngroups_all / gridDim.x;  // end of this block's range
+        g = draw();
+    }
+    if constexpr ((ABL & 4096) != 0) g = draw();
+    if (g >= ngroups) {
+        finish();
+        return;
+    }
     const int64_t last = n - 1;
 
     QLane Q[TILES];
+    // ABL & 8192 (ENC 0, TILES 1): queries through raw buffer loads (load_q_tile)
+    constexpr bool kBufQ = (ABL & 8192) != 0 && ENC == 0 && TILES == 1;
+    const QOffsets vo{r * 60, r * 60 + 12 + 12 * h, r * 60 + 36 + 12 * h};
+    if constexpr (kBufQ) {
+        Q[0] = load_q_tile(q, n, g, vo);
+    } else {
 #pragma unroll
-    for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((g * TILES + t) * 32 + r, last), h);
+        for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((g * TILES + t) * 32 + r, last), h);
+    }
     if constexpr ((ABL & 32) != 0) {
         // stores that the hardware drops (empty descriptors): the loop is then entered with the same "prefetch
         // loads, then the epilogue's stores" vmcnt pattern as the back-edge, so the waits inside stay exact
@@ -802,8 +951,26 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     uint64_t ph[kInferPhases] = {};
     uint64_t tprev = 0;
     if constexpr ((ABL & 256) != 0) tprev = stamp_now();
+    uint64_t clk0 = 0, rclk0 = 0;
+    if constexpr ((ABL & 512) != 0) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rclk0 = __builtin_amdgcn_s_memrealtime();
+    }
     bool first_iter = true;
-    for (; g < ngroups; g += wstride) {
+    // queue variants draw one tile ahead: the draw for the tile after next is issued before this iteration's
+    // prefetch loads, so its (atomic) latency hides under a whole tile and the prefetch never waits for it
+    int64_t ng = 0;
+    uint32_t nn_raw = 0;  // the pending draw: lane 0's atomic result, read (readfirstlane) one iteration later
+    if constexpr ((ABL & (2048 | 4096)) != 0) ng = draw();
+    for (int64_t nn = 0; g < ngroups; g = ng, ng = nn) {
+        if constexpr ((ABL & (2048 | 4096)) != 0) {
+            if (!first_iter) {
+                // an asm readfirstlane stays here; the builtin is hoisted to the atomic and the wave then waits for it
+                uint32_t t;
+                asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(t) : "v"(nn_raw));
+                ng = gbase + (int64_t)t;
+            }
+        }
         if constexpr ((ABL & 256) != 0) {  // the previous iteration's epilogue (stores, loop overhead)
             const uint64_t tn = stamp_now();
             if (!first_iter) ph[7] += tn - tprev;
@@ -822,12 +989,28 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
                 const f4 a = {Q[t].p0, Q[t].p1, Q[t].b0, Q[t].b1}, b = {Q[t].b2, Q[t].i0, Q[t].i1, Q[t].i2};
 #pragma unroll
                 for (int kk = 0; kk < 5; ++kk) x[t][kk] = __builtin_bit_cast(h8, (kk & 1) ? a : b);
+            } else if constexpr ((ABL & 1024) != 0) {
+                encode_v3(Q[t], h, x[t]);
             } else {
                 encode_fast<(ABL & 16) != 0>(Q[t], h, x[t]);
             }
         }
-        const int64_t ng = g + wstride;
-        if constexpr ((ABL & 32) != 0) {
+        if constexpr ((ABL & (2048 | 4096)) != 0) {
+            if constexpr ((ABL & 4096) != 0) {
+                // every lane issues the buffer atomic; the descriptor covers lane 0's counter only, the other lanes'
+                // adds are dropped by the hardware (no branch around the atomic)
+                nn_raw = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, buffer_rsrc(epi.wq, 4), lane ? kBufferOff : 0, 0, 0);
+            } else {
+                if (lane == 0) nn_raw = atomicAdd(&wq_next, 1u);
+            }
+            first_iter = false;
+        } else {
+            ng = g + wstride;
+            nn = ng;
+        }
+        if constexpr (kBufQ) {
+            Q[0] = load_q_tile(q, n, ng, vo);
+        } else if constexpr ((ABL & 32) != 0) {
             // unconditional (clamped) prefetch: no branch around the loads, so the compiler's vmcnt bookkeeping
             // stays exact across the loop back-edge
 #pragma unroll
@@ -912,9 +1095,20 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
 #pragma unroll
             for (int t = 0; t < TILES; ++t) {
                 const int64_t s0 = (g * TILES + t) * 32, sq = s0 + r;
-                const float L0 = (float)(_Float16)fmaxf(o[t][0], 0.0f);
-                const float L1 = (float)(_Float16)fmaxf(o[t][1], 0.0f);
-                const float L2 = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                float L0, L1, L2;
+                if constexpr ((ABL & 8192) != 0) {
+                    // f16(max(x, 0)) == max(f16(x), 0): two packed converts + two packed maxes + three widenings
+                    const h2 z = {};
+                    const h2 a = __builtin_elementwise_max(__builtin_bit_cast(h2, pk2(o[t][0], o[t][1])), z);
+                    const h2 b = __builtin_elementwise_max(__builtin_bit_cast(h2, pk2(o[t][2], 0.0f)), z);
+                    L0 = (float)a[0];
+                    L1 = (float)a[1];
+                    L2 = (float)b[0];
+                } else {
+                    L0 = (float)(_Float16)fmaxf(o[t][0], 0.0f);
+                    L1 = (float)(_Float16)fmaxf(o[t][1], 0.0f);
+                    L2 = (float)(_Float16)fmaxf(o[t][2], 0.0f);
+                }
                 bool to_out = h == 0;
                 if constexpr (EPI >= 0) {
                     float4 v;
@@ -973,6 +1167,19 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             }
         }
     }
+    finish();
+    if constexpr ((ABL & 512) != 0) {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const int64_t wid = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+        if (lane == 0 && wid < kInferClockWavesMax) {
+            g_infer_clock[6 * wid] = c1 - clk0;
+            g_infer_clock[6 * wid + 1] = rclk0;
+            g_infer_clock[6 * wid + 2] = r1;
+            g_infer_clock[6 * wid + 3] = rstart;
+            g_infer_clock[6 * wid + 4] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // hwreg(HW_REG_HW_ID)
+            g_infer_clock[6 * wid + 5] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // hwreg(HW_REG_XCC_ID)
+        }
+    }
     if constexpr ((ABL & 256) != 0) {
         const uint64_t tn = stamp_now();
         ph[7] += tn - tprev;
@@ -990,6 +1197,16 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
     infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, InferEpilogue{});
 }
 
+// the same with the launch-wide work queue (ABL & 4096): wq = the handle's two zeroed counters
+template <int TILES, int WAVES_PER_EU, int THREADS, bool PREFETCH, int ABL>
+__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_q(const float* __restrict__ q,
+                                                                        float* __restrict__ out, int64_t n,
+                                                                        const h8* __restrict__ wf, uint32_t* wq) {
+    InferEpilogue e{};
+    e.wq = wq;
+    infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, e);
+}
+
 // Diagnostic build of the default inference kernel (variant 23) with per-wave phase stamps (ABL & 256).
 __global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                              int64_t n, const h8* __restrict__ wf,
@@ -1004,7 +1221,7 @@ template <int EPI>
 __global__ __launch_bounds__(512, 4) void infer_accumulate_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                                   int64_t n, const h8* __restrict__ wf,
                                                                   InferEpilogue epi) {
-    infer_v2_body<1, 512, false, kDefaultAbl, EPI>(q, out, n, wf, epi);
+    infer_v2_body<1, 512, false, kDefaultAbl | 1024 | 8192, EPI>(q, out, n, wf, epi);  // encoder v3, buffer-load prefetch
 }
 
 // InputEncoding::Hash inference (EPI -1: plain infer; 0 / 2: fused accumulation as above)
@@ -1672,27 +1889,30 @@ __global__ void encode_kernel(const float* __restrict__ q, float* __restrict__ e
 
 // The production encoder (encode_fast: f16 B fragments) unpacked to canonical order as f32 — lets the
 // parity tests check the exact code path the MLP kernels run.
-template <bool CHAIN>
+template <int VARIANT>  // 0: encode_fast, 1: encode_fast<CHAIN>, 2: encode_v3
 __global__ void encode_fast_kernel(const float* __restrict__ q, float* __restrict__ enc, int64_t n) {
-    if (CHAIN) fp32_flush_output_denorms();
+    if (VARIANT >= 1) fp32_flush_output_denorms();
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t s = gid >> 1;
     const int h = (int)(gid & 1);
     if (s >= n) return;
     const QLane Q = load_q(q, s, h);
     h8 x[5];
-    encode_fast<CHAIN>(Q, h, x);
+    if constexpr (VARIANT == 2) encode_v3(Q, h, x);
+    else encode_fast<VARIANT == 1>(Q, h, x);
 #pragma unroll
     for (int k = 0; k < 40; ++k) enc[s * NRC_ENC_WIDTH + slot_feature(k, h)] = (float)x[k >> 3][k & 7];
 }
 
-hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, bool chain) {
+hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, int variant) {
     if (n <= 0) return hipSuccess;
     const int grid = (int)((2 * n + 255) / 256);
-    if (chain)
-        hipLaunchKernelGGL(encode_fast_kernel<true>, dim3(grid), dim3(256), 0, s, queries, enc, n);
+    if (variant == 2)
+        hipLaunchKernelGGL(encode_fast_kernel<2>, dim3(grid), dim3(256), 0, s, queries, enc, n);
+    else if (variant == 1)
+        hipLaunchKernelGGL(encode_fast_kernel<1>, dim3(grid), dim3(256), 0, s, queries, enc, n);
     else
-        hipLaunchKernelGGL(encode_fast_kernel<false>, dim3(grid), dim3(256), 0, s, queries, enc, n);
+        hipLaunchKernelGGL(encode_fast_kernel<0>, dim3(grid), dim3(256), 0, s, queries, enc, n);
     return hipGetLastError();
 }
 
@@ -2900,6 +3120,24 @@ static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc,
     return hipGetLastError();
 }
 
+static int64_t g_last_clock_waves = 0;
+template <class K, class... Extra>
+static hipError_t launch_clocked(K kernel, int threads, int& cache_bpc, int64_t groups, const float* queries, float* out,
+                                 int64_t n, const _Float16* wf, hipStream_t s, Extra... extra) {
+    if (!cache_bpc) cache_bpc = blocks_per_cu(kernel, threads);
+    const int64_t want = (groups + threads / 64 - 1) / (threads / 64);
+    const int64_t grid = std::min<int64_t>(want, (int64_t)num_cus() * cache_bpc);
+    g_last_clock_waves = std::min<int64_t>(grid * (threads / 64), kInferClockWavesMax);
+    return launch_persistent_infer(kernel, threads, cache_bpc, groups, queries, out, n, wf, s, extra...);
+}
+
+hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves) {
+    const int64_t w = std::min(cap_waves, g_last_clock_waves);
+    *waves = w;
+    if (w <= 0) return hipSuccess;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_infer_clock), sizeof(uint64_t) * 6 * w, 0, hipMemcpyDeviceToHost);
+}
+
 // Inference kernel variants (A/B-able in one process through nrc_debug_infer_variant):
 //   0: v1 (weights hoisted into registers, one wave per SIMD)
 //   1: v2, 1 tile (32 queries) per wave iteration, up to 3 waves per SIMD
@@ -2911,10 +3149,12 @@ static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc,
 //   7-9, 14-16: ablations (timing only); 10-13: v3 register-resident weights; 17-20: v4 asm prefetch
 //   21: variant 3 + LDS-staged 16-B result stores;  22: variant 3 + omod doubling-chain encoder
 //   23: variant 22 + branch-free prefetch and buffer-store epilogue (default)
-static int g_default_infer_variant = 23;  // variant 22 + exact vmcnt waits (A/B: 90.4 vs 94.3 us)
+// round 2: variant 39 (encoder v3, per-CU LDS work queue on 1024-thread blocks, buffer-load prefetch, packed epilogue);
+// in-process A/B at 2^21 queries: 75.1 vs 86.5 us for variant 23 (profiles/r02_infer/)
+static int g_default_infer_variant = 39;
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
-                                hipStream_t s) {
+                                hipStream_t s, uint32_t* wq) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
     static int bpc[kNumInferVariants] = {};
@@ -2947,6 +3187,24 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 26: return launch_persistent_infer(infer_pp_kernel<512, 0>, 512, bpc[26], pairs, queries, out, n, wf, s);
         case 27: return launch_persistent_infer(infer_pp_kernel<512, 1>, 512, bpc[27], pairs, queries, out, n, wf, s);
         case 28: return launch_persistent_infer(infer_pp_kernel<256, 1>, 256, bpc[28], pairs, queries, out, n, wf, s);
+        // round 2: encoder v3 (tent-map triangle wave, clamped OneBlob wrap); 31/32: 23/30 with the clock stamps
+        case 30: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 1024>, 512, bpc[30], ntiles, queries, out, n, wf, s);
+        case 31: return launch_clocked(infer_kernel_v2<1, 4, 512, false, 48 | 512>, 512, bpc[31], ntiles, queries, out, n, wf, s);
+        case 32: return launch_clocked(infer_kernel_v2<1, 4, 512, false, 48 | 1024 | 512>, 512, bpc[32], ntiles, queries, out, n, wf, s);
+        // 33/34: variant 30 with 1024-thread blocks (one per CU) drawing tiles from an LDS work queue; 34 clocked
+        case 33: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048>, 1024, bpc[33], ntiles, queries, out, n, wf, s);
+        case 34: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 512>, 1024, bpc[34], ntiles, queries, out, n, wf, s);
+        // 35/36: as 33/34 with 512-thread blocks (two per CU, each with its own queue)
+        case 35: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 1024 | 2048>, 512, bpc[35], ntiles, queries, out, n, wf, s);
+        case 36: return launch_clocked(infer_kernel_v2<1, 4, 512, false, 48 | 1024 | 2048 | 512>, 512, bpc[36], ntiles, queries, out, n, wf, s);
+        // 39/40: variant 33 + buffer-load query prefetch and packed output epilogue (ABL 8192); 40 clocked
+        case 39: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192>, 1024, bpc[39], ntiles, queries, out, n, wf, s);
+        case 40: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 512>, 1024, bpc[40], ntiles, queries, out, n, wf, s);
+        // 37/38: variant 30 drawing tiles from the launch-wide work queue (the handle's counters); 38 clocked
+        case 37: if (!wq) return hipErrorInvalidValue;
+                 return launch_persistent_infer(infer_kernel_q<1, 4, 512, false, 48 | 1024 | 4096>, 512, bpc[37], ntiles, queries, out, n, wf, s, wq);
+        case 38: if (!wq) return hipErrorInvalidValue;
+                 return launch_clocked(infer_kernel_q<1, 4, 512, false, 48 | 1024 | 4096 | 512>, 512, bpc[38], ntiles, queries, out, n, wf, s, wq);
         // v4: explicit layer-ahead weight prefetch
         case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
         case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
@@ -2975,7 +3233,7 @@ hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, con
 }
 
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
-    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s);
+    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, nullptr);
 }
 
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,

@@ -83,8 +83,36 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
 
 
+def host_cores() -> tuple[int, str]:
+    """Host cores this process may use: the CPUs of its affinity mask, bounded by a cgroup-v2 CPU quota when one is
+    set (a quota of Q us per P us runs at most ceil(Q / P) threads at a time). Returns (cores, how it was found)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = f"{aff} CPUs in the affinity mask"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+            if quota < aff:
+                how += f", cgroup cpu.max quota {quota}"
+                aff = quota
+    except (OSError, ValueError):
+        pass
+    return max(1, min(256, aff)), how  # nrc_oracle.c runs at most 256 pthreads
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
 def default_threads() -> int:
-    return max(1, min(16, os.cpu_count() or 1))
+    return host_cores()[0]
 
 
 def encode(queries: np.ndarray) -> np.ndarray:

@@ -67,10 +67,10 @@ def test_encode_parity(nrc, orc, torch, dev, golden):
         np.testing.assert_allclose(enc.cpu().numpy(), orc.encode(q_np), rtol=0, atol=4e-6)
 
 
-@pytest.mark.parametrize("encoder", [0, 1])
+@pytest.mark.parametrize("encoder", [0, 1, 2])
 def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
     """The encoder inside the MLP kernels (closed-form OneBlob, direct (0) or omod doubling-chain (1) triangle
-    wave, f16 packing) against the oracle's tcnn-literal encoding rounded to f16: every feature of every query
+    wave; 2: encoder v3, tent-map triangle wave and clamped OneBlob wrap; f16 packing) against the oracle's tcnn-literal encoding rounded to f16: every feature of every query
     within one f16 ulp (plus 2e-6 absolute for the f32 evaluation-order differences)."""
     L = nrc._lib.lib()
     for q_np in [golden["queries"], golden["queries_edge"], nrc.synthetic.cornell_queries(20000, seed=22)]:
@@ -86,7 +86,7 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28])
+@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28] + list(range(30, 41)))
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every production-eligible kernel variant at sizes
     that exercise partial tiles / single blocks."""
@@ -285,7 +285,7 @@ def test_set_hyper_params_changes_the_step(nrc, orc, torch, dev, net, golden):
         if it == 2:
             net.setHyperParams(nrc.HyperParams(learningRate=5e-4))
             st.lr = 5e-4
-            assert abs(net.getLearningRate() - 5e-4) < 1e-12
+            assert net.getLearningRate() == np.float32(5e-4)
         q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=900 + it)
         net.train(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np))
         g, _ = orc.grad(st.params, q_np, t_np, mode=orc.MIXED)
@@ -299,9 +299,9 @@ def test_set_hyper_params_changes_the_step(nrc, orc, torch, dev, net, golden):
         q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=900 + it)
         g, _ = orc.grad(st_const.params, q_np, t_np, mode=orc.MIXED)
         st_const.apply(g)
-    d_sched = np.abs(p_gpu - st.params).max()
-    d_const = np.abs(p_gpu - st_const.params).max()
-    assert d_const > 20 * d_sched, (d_sched, d_const)
+    d_sched = rel(p_gpu, st.params)
+    d_const = rel(p_gpu, st_const.params)
+    assert d_const > 5 * d_sched, (d_sched, d_const)
 
 
 def test_set_config_on_a_live_handle_keeps_the_model(nrc, orc, torch, dev, net, golden):
@@ -314,7 +314,7 @@ def test_set_config_on_a_live_handle_keeps_the_model(nrc, orc, torch, dev, net, 
     net.set_state(nrc.StateSlot.INFER, params)
     net.setHyperParams(nrc.HyperParams(learningRate=7e-4))
     net.setConfig(nrc.InputEncoding.Hash)
-    assert abs(net.getLearningRate() - 7e-4) < 1e-12
+    assert net.getLearningRate() == np.float32(7e-4)
     assert json.loads(net.config_json())["encoding"]["nested"][0]["otype"] == "HashGrid"
     q_np = nrc.synthetic.cornell_queries(3000, seed=31)
     y = run_infer(nrc, torch, dev, net, q_np)

@@ -17,6 +17,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import nrc_loader  # noqa: E402
 
+CLOCKED = {31, 32, 34, 36, 38, 40}  # variants that record the in-kernel clock (nrc_debug_read_infer_clock)
+
 
 def main() -> None:
     ap = argparse.ArgumentParser()
@@ -66,6 +68,38 @@ def main() -> None:
         med = float(np.median(t))
         res[v] = {"median_us": med, "min_us": float(t.min()), "Gq_per_s": args.n / med / 1e3,
                   "tflops_alg": 41600 * args.n / (med * 1e-6) / 1e12, "rel_l2_vs_oracle": check[v]}
+        if v in CLOCKED:
+            # in-kernel clock of the variant's last launch (per wave: s_memtime cycles, 100 MHz s_memrealtime ticks)
+            for _ in range(args.iters):
+                L.nrc_debug_infer_variant(net._h, v, q.data_ptr(), outs[v].data_ptr(), args.n, sp)
+            torch.cuda.synchronize()
+            buf = np.zeros(6 * 8192, np.uint64)
+            w = ctypes.c_uint32()
+            nrc._lib.check(L.nrc_debug_read_infer_clock(buf.ctypes.data, 8192, ctypes.byref(w)))
+            c = buf[: 6 * w.value].reshape(-1, 6).astype(np.float64)
+            ghz = c[:, 0] / ((c[:, 2] - c[:, 1]) * 10.0)
+            tiles_per_wave = (args.n / 32) / w.value
+            t0 = c[:, 3].min()
+            start, lstart, end = (c[:, 3] - t0) / 100.0, (c[:, 1] - t0) / 100.0, (c[:, 2] - t0) / 100.0  # us
+            pct = lambda a: [float(np.percentile(a, p)) for p in (0, 10, 50, 90, 100)]  # noqa: E731
+            res[v].update({"clock_ghz_median": float(np.median(ghz)), "waves": int(w.value),
+                           "cycles_per_tile_median": float(np.median(c[:, 0]) / tiles_per_wave),
+                           "loop_us_median": float(np.median(end - lstart)),
+                           "wave_start_us_p0_10_50_90_100": pct(start), "loop_start_us_p": pct(lstart),
+                           "loop_end_us_p": pct(end)})
+            # per XCD and per CU: when their waves finish (the kernel ends with the slowest CU)
+            xcc = c[:, 5].astype(int) & 15
+            cu = (c[:, 4].astype(np.int64) >> 8) & 15
+            se = (c[:, 4].astype(np.int64) >> 13) & 7
+            res[v]["end_us_by_xcd_mean_max"] = {int(x): [float(end[xcc == x].mean()), float(end[xcc == x].max())]
+                                                for x in sorted(set(xcc.tolist()))}
+            cu_end = {}
+            for x, e_, c_ in zip(xcc, se, cu):
+                pass
+            keys = xcc * 256 + se * 16 + cu
+            per_cu = np.array([end[keys == k].max() for k in sorted(set(keys.tolist()))])
+            res[v]["cu_last_end_us_p0_10_50_90_100"] = pct(per_cu)
+            res[v]["cus_seen"] = int(len(per_cu))
     net.destroy()
     print(json.dumps({"n": args.n, "variants": res}, indent=1))
 
