@@ -139,6 +139,14 @@ typedef struct nrc_frame_params {
  * block once at the end (the reference blocks after every minibatch); 0 if the frame did not train. */
 nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* buffers, const nrc_frame_params* params,
                              float* loss_h);
+/* Data-parallel form: this replica renders the pixels [pixel_begin, pixel_end) — it infers and
+ * accumulates only those render queries, writing only that range of results / output_rgba — and infers ALL the
+ * train-suffix ends, so propagation and the shuffle are identical on every replica. With a communicator attached
+ * (nrc_set_comm) each of the NUM_BATCHES minibatches is trained as nrc_train_dp over the global 16,384 samples, this
+ * rank taking its contiguous 1/world slice (BASELINE configs[3]: 2,048 per rank at 8 GPUs). Without one it equals
+ * nrc_process_frame restricted to the pixel range. */
+nrc_status nrc_process_frame_shard(nrc_net* net, const nrc_frame_buffers* buffers, const nrc_frame_params* params,
+                                   uint32_t pixel_begin, uint32_t pixel_end, float* loss_h);
 
 #ifdef __cplusplus
 }

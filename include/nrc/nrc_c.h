@@ -138,6 +138,28 @@ nrc_status nrc_train_grad(nrc_net* net, const float* inputs_d, const float* targ
                           uint32_t global_b, float* grad_d);
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h);
 
+/* ---- data parallelism inside the library: RCCL over xGMI (new capability) ----
+ * The reference's callers are C++ (Device::nrcTrainRadiance, Device.cpp:1503-1509): one process (or thread) per GPU
+ * creates an RCCL communicator, attaches it to its handle, and calls nrc_train_dp where it called train(); the
+ * gradient exchange then happens inside the library on the handle's stream:
+ *     local fwd/bwd of b_local samples, normalised by 3 * global_b (nrc_train_grad)
+ *  -> ncclAllReduce(sum) of the NRC_GRAD_FLOATS (Hash: NRC_HASH_GRAD_FLOATS) buffer incl. the loss
+ *  -> the identical Adam + EMA step on every rank (nrc_train_apply), so the replicas stay bit-identical.
+ * With world = 1 the step is bitwise the fused nrc_train step. C callers without rccl.h can create the
+ * communicator through the nrc_comm_* helpers (one unique id made on rank 0 and shared by any means). */
+#define NRC_COMM_UNIQUE_ID_BYTES 128 /* NCCL_UNIQUE_ID_BYTES */
+nrc_status nrc_comm_get_unique_id(void* id_out /* NRC_COMM_UNIQUE_ID_BYTES */);
+/* ncclCommInitRank on the calling thread's current HIP device; *comm_out receives the ncclComm_t. */
+nrc_status nrc_comm_init_rank(void** comm_out, const void* unique_id, int world, int rank);
+nrc_status nrc_comm_destroy(void* comm);
+/* Attach an ncclComm_t (owned by the caller; NULL detaches). Rank and world size are read from it. */
+nrc_status nrc_set_comm(nrc_net* net, void* nccl_comm);
+nrc_status nrc_get_comm_rank(const nrc_net* net, int* rank, int* world);
+/* One data-parallel optimizer step over a global minibatch of global_b samples of which this rank holds b_local
+ * (b_local may be 0). loss_h: the global minibatch loss (blocking, as nrc_train). Requires an attached comm. */
+nrc_status nrc_train_dp(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b_local,
+                        uint32_t global_b, float* loss_h);
+
 /* ---- state access (host buffers of nrc_get_num_params() f32; synchronous) ----
  * Frequency: NRC_NUM_PARAMS (layout.h canonical blob). Hash: NRC_HASH_NUM_PARAMS = MLP blob then the grid table
  * [entry][2] (the grid's per-entry Adam step counters are internal). */

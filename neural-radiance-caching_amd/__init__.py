@@ -8,5 +8,5 @@ module ``nrc_amd`` by ``load()`` in __graft_entry__.py / tests/conftest.py / ben
 from . import _lib, dp, frame, stream, synthetic  # noqa: F401
 from ._lib import BATCH_SIZE, GRAD_FLOATS, HASH_GRAD_FLOATS, HASH_NUM_PARAMS, NUM_PARAMS, NrcError  # noqa: F401
 from ._lib import PRECISION_F16, PRECISION_FP8, WIDE_NUM_PARAMS  # noqa: F401
-from .network import (HyperParams, InputEncoding, Network, StateSlot, current_stream, default_config, encode,  # noqa: F401
+from .network import (Communicator, HyperParams, InputEncoding, Network, StateSlot, current_stream, default_config, encode,  # noqa: F401
                       fp8_convert)

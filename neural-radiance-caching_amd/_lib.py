@@ -37,11 +37,12 @@ EXPORTS = [
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
+    "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
     "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
-    "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame",
+    "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
     # include/nrc/stream.h (bound in stream.py)
     "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_open", "nrc_stream_close",
     "nrc_stream_write_frame", "nrc_stream_next_frame", "nrc_stream_read_section",
@@ -111,6 +112,12 @@ def lib() -> ctypes.CDLL:
         "nrc_get_grad_floats": (st, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "nrc_debug_encode_net": (st, [vp, fp, fp, u32, vp]),
         "nrc_set_step": (st, [vp, u32]),
+        "nrc_comm_get_unique_id": (st, [vp]),
+        "nrc_comm_init_rank": (st, [ctypes.POINTER(vp), vp, ctypes.c_int, ctypes.c_int]),
+        "nrc_comm_destroy": (st, [vp]),
+        "nrc_set_comm": (st, [vp, vp]),
+        "nrc_get_comm_rank": (st, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+        "nrc_train_dp": (st, [vp, fp, fp, u32, u32, ctypes.POINTER(ctypes.c_float)]),
         "nrc_encode": (st, [fp, fp, u32, vp]),
         "nrc_debug_infer_variant": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_read_infer_clock": (st, [vp, u32, ctypes.POINTER(u32)]),

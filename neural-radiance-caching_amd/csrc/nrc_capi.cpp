@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "nrc/frame.h"
 #include "nrc/nrc_c.h"
 #include "nrc_guard.h"
@@ -235,6 +237,9 @@ struct nrc_net {
     // minibatch-loss slots: host-mapped fine-grained (coherent) pinned memory written directly by the reduce/Adam
     // kernels, so reading a loss back costs one stream sync and no D2H copy launch (the copy was ~4.5 us)
     uint32_t* work_queue = nullptr;  // inference work-queue counters {next tile, finished waves}; zero between launches
+    ncclComm_t comm = nullptr;       // attached RCCL communicator (not owned), nrc_set_comm
+    int comm_rank = 0, comm_world = 1;
+    float* dp_grad = nullptr;        // [grad_floats] gradient exchange buffer of nrc_train_dp
     float* loss_dev = nullptr;   // device view of loss_host
     float* loss_host = nullptr;
     void alloc_loss_slots() {
@@ -282,6 +287,8 @@ struct nrc_net {
         f(slabs); f(loss_partials);  // loss_dev aliases loss_host (freed below)
         f(work_queue);
         work_queue = nullptr;
+        f(dp_grad);
+        dp_grad = nullptr;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer);
         f(scatter.pos); f(scatter.dy);
         scatter = HashScatter{};
@@ -478,6 +485,23 @@ float* slot_ptr(nrc_net* net, int slot) {
 }
 
 }  // namespace
+
+namespace {
+void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b, float* loss_h,
+                 float* loss_d);
+}  // namespace
+
+void nrc_amd::net_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
+                                 float* loss_d) {
+    do_train_dp(net, in, tgt, b_local, global_b, nullptr, loss_d);
+}
+
+bool nrc_amd::net_comm(nrc_net* net, int* rank, int* world) {
+    check_live(net);
+    *rank = net->comm_rank;
+    *world = net->comm_world;
+    return net->comm != nullptr;
+}
 
 nrc_loss_slots nrc_amd::net_loss_slots(nrc_net* net) {
     check_live(net);
@@ -780,9 +804,40 @@ nrc_status nrc_get_config_json(const nrc_net* net, char* buf, size_t cap, size_t
     });
 }
 
+namespace {
+void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b, float* grad_d);
+void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* loss_d);
+}  // namespace
+
 nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b,
                           float* grad_d) {
-    return guarded([&] {
+    return guarded([&] { do_train_grad(net, in, tgt, b, global_b, grad_d); });
+}
+
+nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
+    return guarded([&] { do_train_apply(net, grad_d, loss_h, nullptr); });
+}
+
+namespace {
+void nccl_check(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess)
+        throw ApiError(NRC_ERR_HIP, std::string(what) + " failed: " + ncclGetErrorString(r));
+}
+
+void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b, float* loss_h,
+                 float* loss_d) {
+    check_live(net);
+    if (!net->comm) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm)");
+    if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
+    do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad);
+    // one all-reduce of the gradient and the loss partial, on the handle's stream (stream-ordered with the kernels)
+    nccl_check(ncclAllReduce(net->dp_grad, net->dp_grad, net->grad_floats(), ncclFloat32, ncclSum, net->comm,
+                             net->stream), "ncclAllReduce");
+    do_train_apply(net, net->dp_grad, loss_h, loss_d);
+}
+
+void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b, float* grad_d) {
+    {
         check_live(net);
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
@@ -813,34 +868,91 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
         }
         HIP_CHECK(launch_reduce_adam(kReduceOnly, net->slabs, blocks, net->loss_partials, grad_d, nullptr,
                                      net->buffers(), net->optim(net->step + 1), net->stream));
-    });
+    }
 }
 
-nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
-    return guarded([&] {
-        check_live(net);
-        if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
-        net->step += 1;
-        if (net->wide()) {
-            HIP_CHECK(launch_wide_adam(kApplyOnly, nullptr, 0, nullptr, 0, const_cast<float*>(grad_d), net->loss_dev,
-                                       net->buffers(), net->optim(net->step), net->stream));
-            repack(net, net->stream);
-            if (loss_h) {
-                *loss_h = net->read_loss();
-            }
-            return;
-        }
-        HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), net->loss_dev,
-                                     net->buffers(), net->optim(net->step), net->stream));
+void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* loss_d) {
+    check_live(net);
+    if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
+    net->step += 1;
+    float* ld = loss_d ? loss_d : net->loss_dev;
+    if (net->wide()) {
+        HIP_CHECK(launch_wide_adam(kApplyOnly, nullptr, 0, nullptr, 0, const_cast<float*>(grad_d), ld, net->buffers(),
+                                   net->optim(net->step), net->stream));
+        repack(net, net->stream);
+    } else {
+        HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), ld, net->buffers(),
+                                     net->optim(net->step), net->stream));
         if (net->hash()) {
             GridBuffers gb = net->grid_buffers();
             gb.grad32 = grad_d + net->n_mlp;  // read-only in kApplyOnly
             HIP_CHECK(launch_grid_adam(kApplyOnly, gb, net->optim(net->step), net->stream));
         }
-        if (loss_h) {
+    }
+    if (loss_h) {
+        if (loss_d) {
+            HIP_CHECK(hipStreamSynchronize(net->stream));
+            HIP_CHECK(hipMemcpy(loss_h, loss_d, sizeof(float), hipMemcpyDeviceToHost));
+        } else {
             *loss_h = net->read_loss();
         }
+    }
+}
+}  // namespace
+
+nrc_status nrc_comm_get_unique_id(void* id_out) {
+    return guarded([&] {
+        if (!id_out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output");
+        static_assert(sizeof(ncclUniqueId) == NRC_COMM_UNIQUE_ID_BYTES, "unique id size");
+        ncclUniqueId id;
+        nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+        std::memcpy(id_out, &id, sizeof(id));
     });
+}
+
+nrc_status nrc_comm_init_rank(void** comm_out, const void* unique_id, int world, int rank) {
+    return guarded([&] {
+        if (!comm_out || !unique_id) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null argument");
+        if (world < 1 || rank < 0 || rank >= world) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad rank / world");
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        ncclComm_t c = nullptr;
+        nccl_check(ncclCommInitRank(&c, world, id, rank), "ncclCommInitRank");
+        *comm_out = c;
+    });
+}
+
+nrc_status nrc_comm_destroy(void* comm) {
+    return guarded([&] {
+        if (comm) nccl_check(ncclCommDestroy(static_cast<ncclComm_t>(comm)), "ncclCommDestroy");
+    });
+}
+
+nrc_status nrc_set_comm(nrc_net* net, void* comm) {
+    return guarded([&] {
+        check_live(net);
+        net->comm = static_cast<ncclComm_t>(comm);
+        net->comm_rank = 0;
+        net->comm_world = 1;
+        if (net->comm) {
+            nccl_check(ncclCommUserRank(net->comm, &net->comm_rank), "ncclCommUserRank");
+            nccl_check(ncclCommCount(net->comm, &net->comm_world), "ncclCommCount");
+        }
+    });
+}
+
+nrc_status nrc_get_comm_rank(const nrc_net* net, int* rank, int* world) {
+    return guarded([&] {
+        check_live(net);
+        if (!rank || !world) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null output");
+        *rank = net->comm_rank;
+        *world = net->comm_world;
+    });
+}
+
+nrc_status nrc_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
+                        float* loss_h) {
+    return guarded([&] { do_train_dp(net, in, tgt, b_local, global_b, loss_h, nullptr); });
 }
 
 nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst) {

@@ -92,78 +92,108 @@ nrc_status nrc_permute_train_data(const float* qs, const nrc_float3* ts, const i
     });
 }
 
+namespace {
+// Device::render's post-trace sequence for the pixels [p0, p1) of the frame (all of it: [0, screen)). A data-parallel
+// replica (communicator attached, nrc_set_comm) renders a pixel shard and trains on its 1/world slice of every
+// minibatch; the train-suffix ends (tiles) are inferred in full on every rank, so propagation and the shuffle are
+// identical everywhere and the sliced minibatches together are exactly the single-GPU minibatches.
+void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_params* p, uint32_t p0, uint32_t p1,
+                   float* loss_h) {
+    require(net && fb && p, "NULL argument");
+    require(valid_mode(p->render_mode), "unknown render mode");
+    require(p0 <= p1 && p1 <= p->screen_size, "bad pixel range");
+    hipStream_t s = nullptr;
+    check(nrc_get_stream(net, &s));
+    if (loss_h) *loss_h = 0.0f;
+    const uint32_t screen = p->screen_size, tiles = p->num_tiles;
+    const int mode = p->render_mode;
+    const bool whole = p0 == 0 && p1 == screen;
+    const uint32_t npix = p1 - p0;
+
+    // Device::nrcInferRadiance (Device.cpp:1272-1301): render queries are skipped for NoCache / CacheFirstVertex
+    const bool skip_render = mode == NRC_RENDER_NO_CACHE || mode == NRC_RENDER_CACHE_FIRST_VERTEX;
+    require((uint64_t)screen + tiles <= UINT32_MAX, "screen_size + num_tiles overflows");
+    const float* qi = fb->queries_inference_d;
+    nrc_float3* ri = fb->results_inference_d;
+    // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion)
+    const bool fuse = !skip_render && !p->keep_render_results &&
+                      (mode == NRC_RENDER_FULL || mode == NRC_RENDER_CACHE_ONLY);
+    if ((uint64_t)screen + tiles > 0) require(qi && ri, "inference buffers are NULL");
+    auto infer_range = [&](uint32_t first, uint32_t count, uint32_t acc_pixels) {
+        // queries [first, first + count); the first acc_pixels of them are render queries of pixels first..
+        if (count == 0) return;
+        const float* q = qi + (size_t)first * NRC_INPUT_DIMS;
+        float* r = reinterpret_cast<float*>(ri + first);
+        if (fuse && acc_pixels > 0)
+            check(nrc_infer_accumulate(net, q, r, count, fb->last_render_throughput_d + first,
+                                       fb->output_rgba_d + (size_t)first * 4, acc_pixels, mode, p->iteration_index));
+        else
+            check(nrc_infer_stream(net, q, r, count, s));
+    };
+    if (whole && !skip_render) {
+        infer_range(0, screen + tiles, screen);  // one launch over the contiguous render + tile queries
+    } else {
+        if (!skip_render) infer_range(p0, npix, npix);
+        infer_range(screen, tiles, 0);
+    }
+    // Device::nrcAccumulateRadiance (Device.cpp:1310-1337)
+    if (!skip_render && !fuse && npix > 0)
+        check(nrc_accumulate_render_radiance(fb->results_inference_d + p0, fb->last_render_throughput_d + p0,
+                                             fb->output_rgba_d + (size_t)p0 * 4, npix, mode, p->iteration_index, s));
+    // Device::nrcVisualizeFirstRadiance (Device.cpp:1339-1370)
+    if (mode == NRC_RENDER_CACHE_FIRST_VERTEX && npix > 0) {
+        require(fb->queries_cache_vis_d && fb->results_cache_vis_d, "cache-vis buffers are NULL");
+        check(nrc_infer_stream(net, fb->queries_cache_vis_d + (size_t)p0 * NRC_INPUT_DIMS,
+                               reinterpret_cast<float*>(fb->results_cache_vis_d + p0), npix, s));
+        check(nrc_copy_radiance_to_output(fb->results_cache_vis_d + p0, fb->output_rgba_d + (size_t)p0 * 4, npix, s));
+    }
+
+    // Training (Device.cpp:2505-2512): only when the trace produced records
+    const int32_t nrec = std::min(p->num_training_records, (int32_t)NRC_NUM_TRAINING_RECORDS_PER_FRAME);
+    if (!p->train || nrec <= 0) return;
+    require(fb->train_queries_d[0] && fb->train_queries_d[1] && fb->train_targets_d[0] && fb->train_targets_d[1],
+            "training double buffers are NULL");
+    // Device::nrcPropagateRadiance (Device.cpp:1382-1419): end radiance = results after the render part
+    check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
+                                       fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
+    // Device::nrcShuffleTrainingData (Device.cpp:1427-1469)
+    check(nrc_permute_train_data(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d,
+                                 p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],
+                                 fb->train_targets_d[1], NRC_NUM_TRAINING_RECORDS_PER_FRAME, s));
+    // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss. The minibatch losses
+    // land in host-mapped slots and are read after one sync at the end (the reference syncs after
+    // every minibatch, Device.cpp:1504); summed in the same order, so the mean is the same float.
+    const nrc_loss_slots slots = net_loss_slots(net);
+    int rank = 0, world = 1;
+    const bool dp = net_comm(net, &rank, &world);
+    // this rank's slice of every minibatch (dp::shard_range): sizes differ by at most one sample
+    const uint32_t base = NRC_BATCH_SIZE / world, rem = NRC_BATCH_SIZE % world;
+    const uint32_t s0 = rank * base + std::min<uint32_t>(rank, rem), sn = base + (rank < (int)rem ? 1 : 0);
+    for (int b = 0; b < NRC_NUM_BATCHES; ++b) {
+        const size_t first = (size_t)b * NRC_BATCH_SIZE + (dp ? s0 : 0);
+        const float* bq = fb->train_queries_d[1] + first * NRC_INPUT_DIMS;
+        const float* bt = reinterpret_cast<const float*>(fb->train_targets_d[1] + first);
+        if (dp)
+            net_train_dp_async(net, bq, bt, sn, NRC_BATCH_SIZE, slots.dev + b);
+        else
+            check(nrc_train_async(net, bq, bt, NRC_BATCH_SIZE, slots.dev + b));
+    }
+    if (loss_h) {
+        HIP_CHECK(hipStreamSynchronize(s));  // the slots are host-mapped: the kernels wrote them directly
+        float total = 0.0f;
+        for (int b = 0; b < NRC_NUM_BATCHES; ++b) total += slots.host[b];
+        *loss_h = total * (1.0f / NRC_NUM_BATCHES);
+    }
+}
+}  // namespace
+
 nrc_status nrc_process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_params* p, float* loss_h) {
-    return guarded([&] {
-        require(net && fb && p, "NULL argument");
-        require(valid_mode(p->render_mode), "unknown render mode");
-        hipStream_t s = nullptr;
-        check(nrc_get_stream(net, &s));
-        if (loss_h) *loss_h = 0.0f;
-        const uint32_t screen = p->screen_size, tiles = p->num_tiles;
-        const int mode = p->render_mode;
+    return guarded([&] { process_frame(net, fb, p, 0, p ? p->screen_size : 0, loss_h); });
+}
 
-        // Device::nrcInferRadiance (Device.cpp:1272-1301): render queries are skipped for NoCache / CacheFirstVertex
-        const bool skip_render = mode == NRC_RENDER_NO_CACHE || mode == NRC_RENDER_CACHE_FIRST_VERTEX;
-        const float* q = fb->queries_inference_d;
-        nrc_float3* r = fb->results_inference_d;
-        uint64_t nq = (uint64_t)screen + tiles;
-        if (skip_render) {
-            q += (size_t)screen * NRC_INPUT_DIMS;
-            r += screen;
-            nq = tiles;
-        }
-        require(nq <= UINT32_MAX, "screen_size + num_tiles overflows");
-        // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion)
-        const bool fuse = !skip_render && !p->keep_render_results &&
-                          (mode == NRC_RENDER_FULL || mode == NRC_RENDER_CACHE_ONLY);
-        if (nq > 0) {
-            require(fb->queries_inference_d && fb->results_inference_d, "inference buffers are NULL");
-            if (fuse)
-                check(nrc_infer_accumulate(net, q, reinterpret_cast<float*>(r), (uint32_t)nq,
-                                           fb->last_render_throughput_d, fb->output_rgba_d, screen, mode,
-                                           p->iteration_index));
-            else
-                check(nrc_infer_stream(net, q, reinterpret_cast<float*>(r), (uint32_t)nq, s));
-        }
-        // Device::nrcAccumulateRadiance (Device.cpp:1310-1337)
-        if (!skip_render && !fuse)
-            check(nrc_accumulate_render_radiance(fb->results_inference_d, fb->last_render_throughput_d,
-                                                 fb->output_rgba_d, screen, mode, p->iteration_index, s));
-        // Device::nrcVisualizeFirstRadiance (Device.cpp:1339-1370)
-        if (mode == NRC_RENDER_CACHE_FIRST_VERTEX && screen > 0) {
-            require(fb->queries_cache_vis_d && fb->results_cache_vis_d, "cache-vis buffers are NULL");
-            check(nrc_infer_stream(net, fb->queries_cache_vis_d, reinterpret_cast<float*>(fb->results_cache_vis_d),
-                                   screen, s));
-            check(nrc_copy_radiance_to_output(fb->results_cache_vis_d, fb->output_rgba_d, screen, s));
-        }
-
-        // Training (Device.cpp:2505-2512): only when the trace produced records
-        const int32_t nrec = std::min(p->num_training_records, (int32_t)NRC_NUM_TRAINING_RECORDS_PER_FRAME);
-        if (!p->train || nrec <= 0) return;
-        require(fb->train_queries_d[0] && fb->train_queries_d[1] && fb->train_targets_d[0] && fb->train_targets_d[1],
-                "training double buffers are NULL");
-        // Device::nrcPropagateRadiance (Device.cpp:1382-1419): end radiance = results after the render part
-        check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
-                                           fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
-        // Device::nrcShuffleTrainingData (Device.cpp:1427-1469)
-        check(nrc_permute_train_data(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d,
-                                     p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],
-                                     fb->train_targets_d[1], NRC_NUM_TRAINING_RECORDS_PER_FRAME, s));
-        // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss. The minibatch losses
-        // land in host-mapped slots and are read after one sync at the end (the reference syncs after
-        // every minibatch, Device.cpp:1504); summed in the same order, so the mean is the same float.
-        const nrc_loss_slots slots = net_loss_slots(net);
-        for (int b = 0; b < NRC_NUM_BATCHES; ++b)
-            check(nrc_train_async(net, fb->train_queries_d[1] + (size_t)b * NRC_BATCH_SIZE * NRC_INPUT_DIMS,
-                                  reinterpret_cast<const float*>(fb->train_targets_d[1] + (size_t)b * NRC_BATCH_SIZE),
-                                  NRC_BATCH_SIZE, slots.dev + b));
-        if (loss_h) {
-            HIP_CHECK(hipStreamSynchronize(s));  // the slots are host-mapped: the kernels wrote them directly
-            float total = 0.0f;
-            for (int b = 0; b < NRC_NUM_BATCHES; ++b) total += slots.host[b];
-            *loss_h = total * (1.0f / NRC_NUM_BATCHES);
-        }
-    });
+nrc_status nrc_process_frame_shard(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_params* p,
+                                   uint32_t pixel_begin, uint32_t pixel_end, float* loss_h) {
+    return guarded([&] { process_frame(net, fb, p, pixel_begin, pixel_end, loss_h); });
 }
 
 }  // extern "C"

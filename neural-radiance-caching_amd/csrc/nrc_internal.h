@@ -231,6 +231,11 @@ struct nrc_loss_slots {  // four minibatch-loss slots in host-mapped coherent pi
 struct nrc_net;
 namespace nrc_amd {
 nrc_loss_slots net_loss_slots(nrc_net* net);
+// the attached communicator (nrc_set_comm): false if none; rank / world of it
+bool net_comm(nrc_net* net, int* rank, int* world);
+// nrc_train_dp with the loss left in a device slot (frame driver)
+void net_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
+                        float* loss_d);
 
 // ---- per-frame kernels around the network (nrc_frame.hip, include/nrc/frame.h)
 hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,

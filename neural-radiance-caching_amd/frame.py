@@ -88,6 +88,8 @@ def _sigs():
         "nrc_permute_train_data": [vp, vp, vp, u64, u32, i32, vp, vp, u32, vp],
         "nrc_process_frame": [vp, ctypes.POINTER(NrcFrameBuffers), ctypes.POINTER(NrcFrameParams),
                               ctypes.POINTER(ctypes.c_float)],
+        "nrc_process_frame_shard": [vp, ctypes.POINTER(NrcFrameBuffers), ctypes.POINTER(NrcFrameParams), u32, u32,
+                                    ctypes.POINTER(ctypes.c_float)],
     }.items():
         fn = getattr(L, name)
         fn.restype = st
@@ -224,4 +226,16 @@ def process_frame(net, buffers: FrameBuffers, params: FrameParams, loss: bool = 
     fb, fp = buffers.as_struct(), params.as_struct()
     lh = ctypes.c_float(float("nan"))
     check(_sigs().nrc_process_frame(net._h, ctypes.byref(fb), ctypes.byref(fp), ctypes.byref(lh) if loss else None))
+    return lh.value if loss else None
+
+
+def process_frame_shard(net, buffers: FrameBuffers, params: FrameParams, pixel_begin: int, pixel_end: int,
+                        loss: bool = True):
+    """Data-parallel replica of process_frame (frame.h nrc_process_frame_shard): renders pixels [pixel_begin,
+    pixel_end), infers every train-suffix end, and with a communicator attached trains on this rank's slice of
+    every minibatch through nrc_train_dp."""
+    fb, fp = buffers.as_struct(), params.as_struct()
+    lh = ctypes.c_float(float("nan"))
+    check(_sigs().nrc_process_frame_shard(net._h, ctypes.byref(fb), ctypes.byref(fp), int(pixel_begin), int(pixel_end),
+                                          ctypes.byref(lh) if loss else None))
     return lh.value if loss else None

@@ -209,6 +209,27 @@ class Network:
                                         ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
+    # ---- data parallelism inside the library (nrc_c.h: RCCL communicator + nrc_train_dp) ------------------
+    def set_comm(self, comm) -> None:
+        """Attach an RCCL communicator (a Communicator, an ncclComm_t address, or None to detach)."""
+        c = comm.handle if isinstance(comm, Communicator) else comm
+        check(self._lib.nrc_set_comm(self._h, c))
+
+    def comm_rank(self) -> tuple[int, int]:
+        r, w = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.nrc_get_comm_rank(self._h, ctypes.byref(r), ctypes.byref(w)))
+        return r.value, w.value
+
+    def train_dp(self, inputs, targets, b_local: int, global_b: int, loss: bool = False):
+        """One data-parallel step: this rank's b_local samples of a global minibatch of global_b, the gradient
+        all-reduced over the attached communicator inside the library, then the identical Adam + EMA step."""
+        lh = ctypes.c_float(float("nan"))
+        b = int(b_local)
+        pi = _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None) if b else None
+        pt = _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None
+        check(self._lib.nrc_train_dp(self._h, pi, pt, b, int(global_b), ctypes.byref(lh) if loss else None))
+        return lh.value if loss else None
+
     @property
     def num_params(self) -> int:
         """Parameter count of the configured model (Frequency 22,528; Hash 21,504 MLP + 991,232 grid)."""
@@ -252,6 +273,34 @@ class Network:
         check(self._lib.nrc_set_step(self._h, int(value)))
 
 
+class Communicator:
+    """An RCCL communicator made through the C-ABI helpers (nrc_comm_*): rank 0 calls unique_id(), shares the
+    128 bytes with the other ranks (e.g. a torch.distributed broadcast), and every rank constructs one on its
+    current HIP device."""
+
+    UNIQUE_ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(Communicator.UNIQUE_ID_BYTES)
+        check(lib().nrc_comm_get_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, unique_id: bytes, world: int, rank: int):
+        if len(unique_id) != self.UNIQUE_ID_BYTES:
+            raise ValueError("unique id must be 128 bytes")
+        h = ctypes.c_void_p()
+        check(lib().nrc_comm_init_rank(ctypes.byref(h), ctypes.create_string_buffer(unique_id, len(unique_id)),
+                                       int(world), int(rank)))
+        self.handle = h
+        self.world, self.rank = int(world), int(rank)
+
+    def destroy(self) -> None:
+        if self.handle is not None and self.handle.value:
+            check(lib().nrc_comm_destroy(self.handle))
+            self.handle = ctypes.c_void_p()
+
+
 def encode(inputs, encoded, n: int, stream=None) -> None:
     """The Composite encoding alone (test entry): f32 [n][80] canonical feature order."""
     check(lib().nrc_encode(_dev_ptr(inputs, "inputs"), _dev_ptr(encoded, "encoded"), int(n), _stream_ptr(stream)))
@@ -275,5 +324,5 @@ def fp8_convert(x, y, n: int, relu: bool = True, stream=None) -> None:
     check(lib().nrc_debug_fp8_convert(_dev_ptr(x, "x", n), py, int(n), int(bool(relu)), _stream_ptr(stream)))
 
 
-__all__ = ["Network", "InputEncoding", "HyperParams", "StateSlot", "NrcError", "encode", "default_config", "fp8_convert",
+__all__ = ["Network", "Communicator", "InputEncoding", "HyperParams", "StateSlot", "NrcError", "encode", "default_config", "fp8_convert",
            "BATCH_SIZE", "NUM_PARAMS", "GRAD_FLOATS", "current_stream"]

@@ -1,0 +1,132 @@
+"""Data parallelism on the GPU path.
+
+* In-library RCCL (nrc_set_comm + nrc_train_dp): with a world-1 communicator the step is bitwise the fused
+  nrc_train step (the all-reduce of one rank is the identity); the frame driver's shard entry with a world-1
+  communicator reproduces nrc_process_frame bitwise.
+* Two ranks on one GPU over gloo (torch.distributed) with the real HIP nrc_train_grad / nrc_train_apply: the
+  replicas stay bit-identical, and after the steps they match the single-process nrc_train on the concatenated
+  16,384-sample minibatches to the gradient's summation-order tolerance. (RCCL itself cannot put two ranks on one
+  device; the multi-GPU RCCL path is the driver's 8-GPU bench, rehearsed here with the same code over gloo.)
+"""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+
+    return _t
+
+
+def to_dev(torch, dev, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def test_world1_rccl_step_is_bitwise_nrc_train(nrc, torch, dev, golden):
+    comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
+    nets = []
+    for _ in range(2):
+        n = nrc.Network()
+        n.init(stream=torch.cuda.current_stream())
+        n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+        nets.append(n)
+    nets[1].set_comm(comm)
+    assert nets[1].comm_rank() == (0, 1)
+    losses = [[], []]
+    for it in range(3):
+        q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=60 + it)
+        q, t = to_dev(torch, dev, q_np), to_dev(torch, dev, t_np)
+        losses[0].append(nets[0].train(q, t, loss=True))
+        losses[1].append(nets[1].train_dp(q, t, nrc.BATCH_SIZE, nrc.BATCH_SIZE, loss=True))
+    assert losses[0] == losses[1]
+    for slot in nrc.StateSlot:
+        np.testing.assert_array_equal(nets[0].get_state(slot), nets[1].get_state(slot))
+    assert nets[0].step == nets[1].step == 3
+    with pytest.raises(nrc.NrcError):
+        nets[0].train_dp(q, t, nrc.BATCH_SIZE, nrc.BATCH_SIZE)  # no communicator attached
+    for n in nets:
+        n.destroy()
+    comm.destroy()
+
+
+def test_world1_rccl_frame_shard_is_bitwise_process_frame(nrc, torch, dev):
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(160, 96, (8, 8), seed=3)
+    cap = F.NUM_TRAINING_RECORDS_PER_FRAME
+    nrec = min(f.num_training_records, cap)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pad = lambda a, w: np.concatenate([a[:nrec], np.zeros((cap - nrec, w), np.float32)])  # noqa: E731
+    rec = np.zeros(cap, F.TRAINING_RECORD_DTYPE)
+    rec[:nrec] = f.train_records[:nrec]
+    S, T = f.screen_size, f.num_tiles
+
+    def buffers():
+        return F.FrameBuffers(t(f.queries_inference), torch.zeros((S + T, 3), device=dev), t(f.last_render_throughput),
+                              torch.zeros((S, 4), device=dev), F.records_to_device(f.end_vertices, dev),
+                              F.records_to_device(rec, dev), [t(pad(f.train_queries, 15)), torch.zeros((cap, 15), device=dev)],
+                              [t(pad(f.train_targets, 3)), torch.zeros((cap, 3), device=dev)])
+
+    comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
+    outs = []
+    for use_dp in (False, True):
+        net = nrc.Network()
+        net.init(stream=torch.cuda.current_stream())
+        fb = buffers()
+        if use_dp:
+            net.set_comm(comm)
+        losses = []
+        for it in range(2):
+            fp = F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1)
+            losses.append(F.process_frame_shard(net, fb, fp, 0, S) if use_dp else F.process_frame(net, fb, fp))
+        torch.cuda.synchronize()
+        outs.append((losses, fb.output_rgba.cpu().numpy(), net.get_state(nrc.StateSlot.PARAMS)))
+        net.destroy()
+    comm.destroy()
+    assert outs[0][0] == outs[1][0]
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_array_equal(outs[0][2], outs[1][2])
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_ranks_on_one_gpu_gloo(tmp_path, nrc, torch, dev, golden):
+    """tools/dp_rank_worker.py x 2 (gloo, both on cuda:0): bit-identical replicas, equal to nrc_train on the full
+    minibatches within the summation-order tolerance."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    np.save(tmp_path / "params.npy", golden["params_b"])
+    procs = [subprocess.Popen([sys.executable, str(ROOT / "tools" / "dp_rank_worker.py"), str(tmp_path)],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), logs
+    steps = 3
+    ref = nrc.Network()
+    ref.init(stream=torch.cuda.current_stream())
+    ref.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+    ref_losses = []
+    for it in range(steps):
+        q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=80 + it)
+        ref_losses.append(ref.train(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np), loss=True))
+    for slot in ("params", "infer"):
+        a, b = np.load(tmp_path / f"{slot}_0.npy"), np.load(tmp_path / f"{slot}_1.npy")
+        np.testing.assert_array_equal(a, b)
+    p = np.load(tmp_path / "params_0.npy")
+    r = ref.get_state(nrc.StateSlot.PARAMS)
+    assert np.linalg.norm(p - r) <= 1e-4 * np.linalg.norm(r)
+    np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
+    ref.destroy()

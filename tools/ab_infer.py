@@ -26,6 +26,9 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--weights", default="scaled", choices=["scaled", "bench"],
+                    help="scaled: 1.6 x the init weights; bench: bench.py's state (xavier init + 4 frames of "
+                         "self-training on its synthetic batches) and its query stream")
     args = ap.parse_args()
     import torch
 
@@ -37,12 +40,23 @@ def main() -> None:
     sp = int(stream.cuda_stream)
     variants = [int(v) for v in args.variants.split(",")]
 
-    q_np = nrc.synthetic.cornell_queries(args.n, seed=2)
-    q = torch.from_numpy(q_np).to(dev)
     net = nrc.Network()
     net.init(stream=stream)
-    params = orc.init_params(1337) * np.float32(1.6)
-    net.set_state(nrc.StateSlot.INFER, params)
+    if args.weights == "bench":
+        seed = nrc.synthetic.SEED
+        q_np = nrc.synthetic.cornell_queries(args.n, seed=seed)
+        for f in range(4):
+            tq, tt = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE * 4, seed=seed * 31 + f)
+            tq, tt = torch.from_numpy(tq).to(dev), torch.from_numpy(tt).to(dev)
+            for b in range(4):
+                net.train(tq[b * nrc.BATCH_SIZE:], tt[b * nrc.BATCH_SIZE:])
+        torch.cuda.synchronize()
+        params = net.get_state(nrc.StateSlot.INFER)
+    else:
+        q_np = nrc.synthetic.cornell_queries(args.n, seed=2)
+        params = orc.init_params(1337) * np.float32(1.6)
+        net.set_state(nrc.StateSlot.INFER, params)
+    q = torch.from_numpy(q_np).to(dev)
     outs = {v: torch.empty((args.n, 3), device=dev) for v in variants}
     idx = np.arange(0, args.n, 4099)
     y_ref = orc.forward(params, q_np[idx], orc.MIXED)

@@ -1,0 +1,50 @@
+"""One rank of tests/test_gpu_dp.py::test_two_ranks_on_one_gpu_gloo: torch.distributed over gloo, the real HIP
+nrc_train_grad / nrc_train_apply through nrc_amd.dp.DataParallelTrainer, every rank on cuda:0.
+
+    RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tools/dp_rank_worker.py <out_dir>
+"""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import nrc_loader  # noqa: E402
+
+
+def main() -> None:
+    import torch
+    import torch.distributed as dist
+
+    out = Path(sys.argv[1])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    nrc = nrc_loader.load()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    net.set_state(nrc.StateSlot.PARAMS, np.load(out / "params.npy"))
+    grad = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
+    trainer = nrc.dp.DataParallelTrainer(net, grad)
+    trainer.broadcast_state(net, dev)
+    losses = []
+    for it in range(3):
+        q, t = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=80 + it)
+        s, c = nrc.dp.shard_range(nrc.BATCH_SIZE, rank, world)
+        qd = torch.from_numpy(np.ascontiguousarray(q[s:s + c])).to(dev)
+        td = torch.from_numpy(np.ascontiguousarray(t[s:s + c])).to(dev)
+        losses.append(trainer.step(qd, td, c, nrc.BATCH_SIZE, loss=True))
+    torch.cuda.synchronize()
+    np.save(out / f"params_{rank}.npy", net.get_state(nrc.StateSlot.PARAMS))
+    np.save(out / f"infer_{rank}.npy", net.get_state(nrc.StateSlot.INFER))
+    np.save(out / f"loss_{rank}.npy", np.array(losses))
+    net.destroy()
+    dist.destroy_process_group()
+    print(f"rank {rank} ok")
+
+
+if __name__ == "__main__":
+    main()
