@@ -1,10 +1,13 @@
-"""Benchmark of the NRC hot path on MI355X (BASELINE.json metric, configs[1] at N=1).
+"""Benchmark of the NRC hot path on MI355X (BASELINE.json metric).
 
-A step = one ``infer`` over the frame's queries resident in HBM (2^21 synthetic Cornell queries per
-GPU, the 1080p 1spp batch of configs[1]); ``value`` = total queries over all ranks / max-over-ranks
-time (weak scaling: every rank processes its own 2^21). The same run also times the per-frame
-self-training (configs[2]: 4 x 16,384-sample steps; for N > 1 each rank trains on its own 16,384
-per minibatch with an RCCL all-reduce of the gradient) and reports it as ``train_step_ms``.
+N = 1 — configs[1]: a step = one ``infer`` over 2^21 synthetic Cornell queries resident in HBM (the 1080p 1spp
+batch); configs[2]: the per-frame self-training (4 x 16,384-sample steps) reported as ``train_step_ms``.
+
+N > 1 — configs[3] (C4): the 2K frame's 2^22 queries sharded contiguously over the ranks
+(2^19 per GPU at 8; strong scaling, no collective on the inference path), and every 16,384-sample minibatch split
+into 16,384 / N per rank with the gradient all-reduced over RCCL INSIDE the library (nrc_set_comm + nrc_train_dp:
+global batch 16,384, the reference's per-step semantics). The weak-scaling figures (2^21 queries per GPU) are kept
+as the extra key ``weak``.
 
 Launch: ``python bench.py [--gpus N --steps K --warmup W]``; N > 1 under torch.distributed.run.
 """
@@ -31,6 +34,7 @@ PEAK_FP8_TFLOPS = 5000.0  # MI355X dense fp8 (MX-scaled) MFMA
 FLOP_PER_QUERY_WIDE = 2 * (66 * 128 + 4 * 128 * 128 + 128 * 3)  # 148,736
 PEAK_HBM_GBS = 8000.0
 QUERIES_PER_GPU = 1 << 21
+QUERIES_C4 = 1 << 22  # configs[3]: the 2K frame, sharded over the ranks
 ROUND = "r01"
 
 
@@ -46,6 +50,9 @@ def parse():
     ap.add_argument("--no-wide", action="store_true", help="skip the configs[4] width-128 f16/FP8 inference lines")
     ap.add_argument("--no-hash", action="store_true", help="skip the InputEncoding::Hash line")
     ap.add_argument("--frame-iters", type=int, default=20, help="timed 1080p post-trace frames (0: skip)")
+    ap.add_argument("--rehearse-comm", action="store_true",
+                    help="N = 1 only: train through a world-1 RCCL communicator (nrc_train_dp), to rehearse the N > 1 "
+                         "training path on one GPU")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one "
                          "GPU, which is not a measurement)")
@@ -267,30 +274,52 @@ def main() -> None:
             dist.init_process_group(args.dist_backend)
 
     seed = nrc.synthetic.SEED + rank
-    nq = args.queries
-    q_np = nrc.synthetic.cornell_queries(nq, seed=seed)
-    q = torch.from_numpy(q_np).to(dev)
+    c4 = world > 1
+    stream = torch.cuda.current_stream()
+    # configs[3] for N > 1: this rank's contiguous shard of the 2^22-query frame; configs[1] (2^21) for N = 1
+    nq_total = QUERIES_C4 if c4 else args.queries
+    q0, nq = nrc.dp.shard_range(nq_total, rank, world) if c4 else (0, nq_total)
+    q_np = nrc.synthetic.cornell_queries(nq_total, seed=nrc.synthetic.SEED)[q0:q0 + nq] if c4 else \
+        nrc.synthetic.cornell_queries(nq, seed=seed)
+    q = torch.from_numpy(np.ascontiguousarray(q_np)).to(dev)
     out = torch.empty((nq, 3), dtype=torch.float32, device=dev)
     frames_q, frames_t = [], []
     for f in range(4):
-        tq, tt = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE * 4, seed=seed * 31 + f)
+        # the same global minibatches on every rank (each trains on its slice of them)
+        tq, tt = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE * 4, seed=nrc.synthetic.SEED * 31 + f)
         frames_q.append(torch.from_numpy(tq).to(dev))
         frames_t.append(torch.from_numpy(tt).to(dev))
-    stream = torch.cuda.current_stream()
 
     net = nrc.Network()
     net.init(stream=stream, encoding=nrc.InputEncoding.Frequency)
-    grad = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
-    trainer = nrc.dp.DataParallelTrainer(net, grad) if distributed else None
+    comm = None
+    trainer = None
+    b0, bn = nrc.dp.shard_range(nrc.BATCH_SIZE, rank, world)
     if distributed:
-        trainer.broadcast_state(net, dev)
+        if args.dist_backend == "nccl":
+            # RCCL communicator inside the library: rank 0 makes the unique id, torch.distributed carries it
+            uid = torch.zeros(nrc.Communicator.UNIQUE_ID_BYTES, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(nrc.Communicator.unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, src=0)
+            comm = nrc.Communicator(bytes(uid.cpu().numpy().tobytes()), world, rank)
+            net.set_comm(comm)
+        else:
+            # rehearsal of several ranks on one GPU (gloo): the Python all-reduce (RCCL cannot share a device)
+            trainer = nrc.dp.DataParallelTrainer(net, torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev))
+        nrc.dp.DataParallelTrainer(net, None).broadcast_state(net, dev)
+    elif args.rehearse_comm:
+        comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
+        net.set_comm(comm)
 
     def train_frame(fi: int) -> None:
         tq, tt = frames_q[fi % 4], frames_t[fi % 4]
         for b in range(4):
             s = b * nrc.BATCH_SIZE
-            if distributed:
-                trainer.step(tq[s:], tt[s:], nrc.BATCH_SIZE, nrc.BATCH_SIZE * world)
+            if comm is not None:
+                net.train_dp(tq[s + b0:], tt[s + b0:], bn, nrc.BATCH_SIZE)
+            elif trainer is not None:
+                trainer.step(tq[s + b0:], tt[s + b0:], bn, nrc.BATCH_SIZE)
             else:
                 net.train(tq[s:], tt[s:])
 
@@ -299,6 +328,12 @@ def main() -> None:
         if distributed:
             dist.barrier()
         torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        if distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     # a few frames of self-training first so inference runs on non-trivial (EMA) weights
     for f in range(4):
@@ -317,16 +352,32 @@ def main() -> None:
     barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step, same stream
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+    wall_max = max_over_ranks(wall)
     ms_per_step = wall_max / args.steps * 1e3
-    value = world * nq * args.steps / wall_max / 1e6
+    value = nq_total * args.steps / wall_max / 1e6
     # the weights the timed inference used (training below moves them), for the CPU leg's parity check
     infer_params = net.get_state(nrc.StateSlot.INFER) if rank == 0 and world == 1 and not args.no_cpu else None
+    out_np = out.cpu().numpy() if infer_params is not None else None
 
-    # ---- training: frames of 4 x 16384
+    weak = None
+    if c4:
+        # weak scaling (the r01 line): 2^21 queries per GPU
+        nw = QUERIES_PER_GPU
+        qw = torch.from_numpy(nrc.synthetic.cornell_queries(nw, seed=seed)).to(dev)
+        ow = torch.empty((nw, 3), dtype=torch.float32, device=dev)
+        for _ in range(args.warmup):
+            net.infer(qw, ow, nw)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            net.infer(qw, ow, nw)
+        barrier()
+        ww = max_over_ranks(time.perf_counter() - t0)
+        weak = {"queries_per_gpu": nw, "value": world * nw * args.steps / ww / 1e6, "unit": "M queries/s",
+                "ms_per_step": ww / args.steps * 1e3, "scaling": "weak"}
+        del qw, ow
+
+    # ---- training: frames of 4 x 16384 (N > 1: each minibatch split over the ranks, RCCL all-reduce per step)
     for f in range(2):
         train_frame(f)
     barrier()
@@ -334,10 +385,7 @@ def main() -> None:
     for f in range(args.train_frames):
         train_frame(f)
     barrier()
-    tw = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
-    train_frame_ms = float(tw.item()) / args.train_frames * 1e3
+    train_frame_ms = max_over_ranks(time.perf_counter() - t0) / args.train_frames * 1e3
     train_step_ms = train_frame_ms / 4
 
     # ---- one whole post-trace frame: fused infer+accumulate over the 1080p frame's
@@ -350,6 +398,14 @@ def main() -> None:
     hashgrid = hash_bench(nrc, dev, max(10, args.steps // 10)) if world == 1 and not args.no_hash else None
 
     achieved = FLOP_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e12
+    if c4:
+        workload = (f"configs[3]: 2K frame of 2^22 queries sharded over {world} GPUs ({nq_total // world} per GPU), "
+                    f"fused encode+64x5 MLP inference (fp16 MFMA, f32 accumulate); train: every 16384-sample minibatch "
+                    f"split into {world} x {nrc.BATCH_SIZE // world}, RCCL all-reduce of the gradient inside the library "
+                    f"(nrc_train_dp)")
+    else:
+        workload = ("configs[1]: Cornell 1080p 1spp, 2^21-query fused encode+64x5 MLP inference per GPU "
+                    "(fp16 MFMA, f32 accumulate); train: configs[2] 4 x 16384 per frame per GPU")
     result = {
         "metric": "M radiance queries/sec + train-step ms, 64x5 MLP @ 2M samples/frame",
         "value": value,
@@ -359,18 +415,18 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c4 else "weak",
         "vs_baseline": None,
         "dtype": "f16",
         "data": "synthetic (seeded Cornell-box RadianceQuery stream, SURVEY §8(d)); random-init weights "
                 "after 4 frames of self-training",
-        "config": {"workload": "configs[1]: Cornell 1080p 1spp, 2^21-query fused encode+64x5 MLP inference per GPU "
-                               "(fp16 MFMA, f32 accumulate); train: configs[2] 4 x 16384 per frame per GPU",
-                   "queries_per_gpu": nq, "train_batch_per_gpu": nrc.BATCH_SIZE,
+        "config": {"workload": workload, "queries_total": nq_total, "queries_per_gpu": nq,
+                   "train_batch_global": nrc.BATCH_SIZE, "train_batch_per_gpu": bn if distributed else nrc.BATCH_SIZE,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "train_step_ms": train_step_ms,
         "train_frame_ms": train_frame_ms,
         "infer_kernel_ms": kernel_ms,
+        "weak": weak,
         "frame": frame,
         "wide_c5": wide,
         "hash": hashgrid,
@@ -381,12 +437,14 @@ def main() -> None:
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        params = infer_params
-        out_np = out.cpu().numpy()  # the last timed inference step's output, computed with infer_params
-        result["cpu_baseline"] = cpu_baseline(q_np, params, args.cpu_seconds,
+        result["cpu_baseline"] = cpu_baseline(q_np, infer_params, args.cpu_seconds,
                                               nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=seed * 31),
                                               gpu_out=out_np)
+    if comm is not None:
+        net.set_comm(None)
     net.destroy()
+    if comm is not None:
+        comm.destroy()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:

@@ -4,8 +4,16 @@
 // It is the C++ stand-in for the renderer: plain C-ABI calls on hipMalloc'ed buffers, no torch.
 //
 //   nrc_replay <stream.nrcs> [--frames N] [--no-train] [--dump-output out.f32] [--dump-results out.f32]
+//              [--ranks N | --rank r --world N --id-file F]
 //
 // Prints one JSON line per frame (loss, GPU ms of the frame's NRC work) and a summary line.
+//
+// Data parallel: with --ranks N the process forks N ranks (before any HIP call; rank r uses HIP
+// device r % device_count), or an external launcher starts each rank with --rank/--world/--id-file. Rank 0 writes
+// the RCCL unique id to the id file, every rank attaches a communicator to its handle (nrc_set_comm) and replays
+// its shard of every frame through nrc_process_frame_shard: the pixels shard_range(screen, r, N), every
+// train-suffix end, and its 1/N slice of each 16,384-sample minibatch, the gradient all-reduced inside the
+// library. Dumps get a ".rank<r>" suffix for N > 1 (only the rank's pixel range of the output is written).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -14,6 +22,11 @@
 #include <vector>
 
 #include <hip/hip_runtime.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <thread>
 
 #include "nrc/stream.h"
 
@@ -56,6 +69,39 @@ void dump(const char* path, const void* dev, size_t bytes) {
     std::fclose(f);
 }
 
+void shard_range(uint32_t n, int rank, int world, uint32_t* begin, uint32_t* end) {
+    const uint32_t base = n / world, rem = n % world;
+    *begin = rank * base + std::min<uint32_t>(rank, rem);
+    *end = *begin + base + (rank < (int)rem ? 1 : 0);
+}
+
+// rank 0 publishes the RCCL unique id (write + rename, so readers never see a partial file); the others wait for it
+void exchange_id(const std::string& file, int rank, unsigned char* id) {
+    if (rank == 0) {
+        NRC(nrc_comm_get_unique_id(id));
+        const std::string tmp = file + ".tmp";
+        FILE* f = std::fopen(tmp.c_str(), "wb");
+        if (!f || std::fwrite(id, 1, NRC_COMM_UNIQUE_ID_BYTES, f) != NRC_COMM_UNIQUE_ID_BYTES) {
+            std::fprintf(stderr, "nrc_replay: cannot write %s\n", tmp.c_str());
+            std::exit(2);
+        }
+        std::fclose(f);
+        if (std::rename(tmp.c_str(), file.c_str()) != 0) std::exit(2);
+        return;
+    }
+    for (int i = 0; i < 6000; ++i) {  // 60 s
+        FILE* f = std::fopen(file.c_str(), "rb");
+        if (f) {
+            const size_t got = std::fread(id, 1, NRC_COMM_UNIQUE_ID_BYTES, f);
+            std::fclose(f);
+            if (got == NRC_COMM_UNIQUE_ID_BYTES) return;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    std::fprintf(stderr, "nrc_replay: rank %d timed out waiting for %s\n", rank, file.c_str());
+    std::exit(2);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -68,16 +114,59 @@ int main(int argc, char** argv) {
     long max_frames = -1;
     bool train = true;
     const char *dump_out = nullptr, *dump_res = nullptr;
+    int ranks = 0, rank = 0, world = 1;
+    std::string id_file;
     for (int i = 2; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--frames") && i + 1 < argc) max_frames = std::atol(argv[++i]);
         else if (!std::strcmp(argv[i], "--no-train")) train = false;
         else if (!std::strcmp(argv[i], "--dump-output") && i + 1 < argc) dump_out = argv[++i];
         else if (!std::strcmp(argv[i], "--dump-results") && i + 1 < argc) dump_res = argv[++i];
+        else if (!std::strcmp(argv[i], "--ranks") && i + 1 < argc) ranks = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) world = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--id-file") && i + 1 < argc) id_file = argv[++i];
         else {
             std::fprintf(stderr, "nrc_replay: unknown argument %s\n", argv[i]);
             return 2;
         }
     }
+    if (ranks > 0) {
+        // fork the ranks before anything touches HIP; the parent only waits
+        world = ranks;
+        char tmpl[] = "/tmp/nrc_replay_id_XXXXXX";
+        const int fd = mkstemp(tmpl);
+        if (fd < 0) return 2;
+        close(fd);
+        std::remove(tmpl);
+        id_file = tmpl;
+        std::vector<pid_t> kids;
+        for (int r = 0; r < ranks; ++r) {
+            const pid_t pid = fork();
+            if (pid < 0) return 2;
+            if (pid == 0) {
+                rank = r;
+                kids.clear();
+                break;
+            }
+            kids.push_back(pid);
+        }
+        if (!kids.empty()) {
+            int rc = 0;
+            for (pid_t k : kids) {
+                int st = 0;
+                waitpid(k, &st, 0);
+                if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) rc = 1;
+            }
+            std::remove(id_file.c_str());
+            return rc;
+        }
+    }
+    const bool dp = world > 1 || ranks > 0 || !id_file.empty();
+    if (dp && (world < 1 || rank < 0 || rank >= world || id_file.empty())) {
+        std::fprintf(stderr, "nrc_replay: --rank/--world/--id-file (or --ranks) required for data parallelism\n");
+        return 2;
+    }
+    std::string rank_suffix = world > 1 ? ".rank" + std::to_string(rank) : "";
 
     // pass 1: headers only, to size the buffers (the reference sizes them from the resolution, Device.cpp:1246-1257)
     nrc_stream* s = nullptr;
@@ -95,6 +184,11 @@ int main(int argc, char** argv) {
     }
     NRC(nrc_stream_close(s));
 
+    if (dp) {
+        int ndev = 0;
+        HIP(hipGetDeviceCount(&ndev));
+        HIP(hipSetDevice(rank % std::max(ndev, 1)));
+    }
     hipStream_t stream;
     HIP(hipStreamCreate(&stream));
     const size_t cap = NRC_NUM_TRAINING_RECORDS_PER_FRAME;
@@ -129,6 +223,13 @@ int main(int argc, char** argv) {
     nrc_net* net = nullptr;
     NRC(nrc_create(&net));
     NRC(nrc_init(net, stream, NRC_ENCODING_FREQUENCY, nullptr, 0));
+    void* comm = nullptr;
+    if (dp) {
+        unsigned char id[NRC_COMM_UNIQUE_ID_BYTES];
+        exchange_id(id_file, rank, id);
+        NRC(nrc_comm_init_rank(&comm, id, world, rank));
+        NRC(nrc_set_comm(net, comm));
+    }
 
     hipEvent_t e0, e1;
     HIP(hipEventCreate(&e0));
@@ -154,7 +255,13 @@ int main(int argc, char** argv) {
         p.train = train ? 1 : 0;
         float loss = 0.0f;
         HIP(hipEventRecord(e0, stream));
-        NRC(nrc_process_frame(net, &fb, &p, &loss));
+        if (dp) {
+            uint32_t p0 = 0, p1 = 0;
+            shard_range(h.screen_size, rank, world, &p0, &p1);
+            NRC(nrc_process_frame_shard(net, &fb, &p, p0, p1, &loss));
+        } else {
+            NRC(nrc_process_frame(net, &fb, &p, &loss));
+        }
         HIP(hipEventRecord(e1, stream));
         HIP(hipEventSynchronize(e1));
         float ms = 0.0f;
@@ -168,13 +275,16 @@ int main(int argc, char** argv) {
     }
     NRC(nrc_stream_close(s));
     HIP(hipStreamSynchronize(stream));
-    if (dump_out) dump(dump_out, output, (size_t)last_screen * 4 * sizeof(float));
-    if (dump_res) dump(dump_res, results_inference, ((size_t)last_screen + last_tiles) * sizeof(nrc_float3));
+    if (dump_out) dump((dump_out + rank_suffix).c_str(), output, (size_t)last_screen * 4 * sizeof(float));
+    if (dump_res)
+        dump((dump_res + rank_suffix).c_str(), results_inference, ((size_t)last_screen + last_tiles) * sizeof(nrc_float3));
     uint32_t step = 0;
     NRC(nrc_get_step(net, &step));
-    std::printf("{\"frames\": %ld, \"mean_loss\": %.9g, \"mean_gpu_ms\": %.4f, \"train_steps\": %u}\n", frames,
-                frames ? total_loss / frames : 0.0, frames ? total_ms / frames : 0.0, step);
+    std::printf("{\"frames\": %ld, \"mean_loss\": %.9g, \"mean_gpu_ms\": %.4f, \"train_steps\": %u, \"rank\": %d, "
+                "\"world\": %d}\n", frames, frames ? total_loss / frames : 0.0, frames ? total_ms / frames : 0.0, step, rank,
+                world);
     NRC(nrc_destroy(net));
     NRC(nrc_free(net));
+    if (comm) NRC(nrc_comm_destroy(comm));
     return 0;
 }

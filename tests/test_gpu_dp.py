@@ -97,6 +97,41 @@ def test_world1_rccl_frame_shard_is_bitwise_process_frame(nrc, torch, dev):
     np.testing.assert_array_equal(outs[0][2], outs[1][2])
 
 
+def test_frame_pixel_shards_cover_the_frame(nrc, torch, dev):
+    """nrc_process_frame_shard without a communicator: two replicas rendering [0, S/2) and [S/2, S) write exactly
+    their halves of the frame buffer, and together equal the whole-frame nrc_process_frame; every replica infers all
+    train-suffix ends, so their training (full minibatches here) is identical."""
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(160, 96, (8, 8), seed=6)
+    cap = F.NUM_TRAINING_RECORDS_PER_FRAME
+    nrec = min(f.num_training_records, cap)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pad = lambda a, w: np.concatenate([a[:nrec], np.zeros((cap - nrec, w), np.float32)])  # noqa: E731
+    rec = np.zeros(cap, F.TRAINING_RECORD_DTYPE)
+    rec[:nrec] = f.train_records[:nrec]
+    S, T = f.screen_size, f.num_tiles
+    res = []
+    for rng in [(0, S), (0, S // 2 + 7), (S // 2 + 7, S)]:
+        net = nrc.Network()
+        net.init(stream=torch.cuda.current_stream())
+        fb = F.FrameBuffers(t(f.queries_inference), torch.zeros((S + T, 3), device=dev), t(f.last_render_throughput),
+                            torch.full((S, 4), -1.0, device=dev), F.records_to_device(f.end_vertices, dev),
+                            F.records_to_device(rec, dev), [t(pad(f.train_queries, 15)), torch.zeros((cap, 15), device=dev)],
+                            [t(pad(f.train_targets, 3)), torch.zeros((cap, 3), device=dev)])
+        fp = F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, 0, 0, 1)
+        loss = F.process_frame(net, fb, fp) if rng == (0, S) else F.process_frame_shard(net, fb, fp, *rng)
+        torch.cuda.synchronize()
+        res.append((rng, loss, fb.output_rgba.cpu().numpy(), net.get_state(nrc.StateSlot.PARAMS)))
+        net.destroy()
+    full = res[0][2]
+    for rng, loss, out, params in res[1:]:
+        a, b = rng
+        np.testing.assert_array_equal(out[a:b], full[a:b])
+        assert (np.delete(out, np.arange(a, b), axis=0) == -1.0).all()
+        assert loss == res[0][1]
+        np.testing.assert_array_equal(params, res[0][3])
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

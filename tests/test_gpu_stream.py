@@ -126,3 +126,22 @@ def test_replay_with_recorded_permutation_and_modes(nrc, dev, tmp_path):
     np.testing.assert_array_equal(fb.train_queries[1].cpu().numpy(), pad(f.train_queries, 15)[perm % nrec])
     net.destroy()
     net2.destroy()
+
+
+def test_replay_ranks1_rccl_matches_plain_replay(nrc, dev, tmp_path):
+    """nrc_replay --ranks 1 (a forked rank with a world-1 RCCL communicator, nrc_process_frame_shard + nrc_train_dp)
+    reproduces the plain replay bit for bit: losses, frame buffer and radiance."""
+    S = nrc.stream
+    p = tmp_path / "k.nrcs"
+    S.record_synthetic(p, 3, 160, 120, seed=5)
+    outs = {}
+    for mode, extra in (("plain", []), ("ranks1", ["--ranks", "1"])):
+        out_f, res_f = tmp_path / f"out_{mode}.f32", tmp_path / f"res_{mode}.f32"
+        r = subprocess.run([str(REPLAY_BIN), str(p), "--dump-output", str(out_f), "--dump-results", str(res_f)] + extra,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]  # RCCL may log to stdout
+        assert lines[-1]["train_steps"] == 12 and lines[-1]["world"] == 1
+        outs[mode] = ([x["loss"] for x in lines if "frame" in x], out_f.read_bytes(), res_f.read_bytes())
+    assert outs["plain"][0] == outs["ranks1"][0]
+    assert outs["plain"][1] == outs["ranks1"][1] and outs["plain"][2] == outs["ranks1"][2]
