@@ -6,8 +6,9 @@ Tolerances (north_star: "outputs within 1e-3 relative-L2" of the network; fp16 a
 * encoding vs oracle (f32, before the f16 cast): |diff| <= 4e-6;
 * weight gradient vs ORC_MIXED: relative L2 <= 2e-3 (f16 deltas, different summation order);
 * Adam + EMA from an identical gradient: relative <= 1e-6 (f32, same operation order);
-* tcnn-emulation (ORC_TCNN, f16 accumulation) and exact f32 (ORC_FP32) distances are asserted
-  loosely (<= 1e-2) and reported — parity with tcnn itself is unpinned.
+* tcnn-emulation (ORC_TCNN, f16 accumulation) and exact f32 (ORC_FP32) distances are asserted at the measured
+  bound (<= 2.5e-3; measured 1.7e-3 - 2.1e-3) and reported — parity with tcnn itself is unpinned (DESIGN.md §4-5,
+  sensitivity table profiles/r02_sensitivity/).
 """
 import numpy as np
 import pytest
@@ -132,7 +133,12 @@ def test_infer_golden_and_modes(nrc, orc, torch, dev, net, golden):
         r_fp32 = rel(y, golden[f"{yk}_fp32"])
         print(f"{qk}: rel-L2 vs mixed {r_mixed:.2e}, vs tcnn-emulation {r_tcnn:.2e}, vs fp32 {r_fp32:.2e}")
         assert r_mixed <= 1e-3
-        assert r_tcnn <= 1e-2 and r_fp32 <= 1e-2
+        # Measured bounds: the f16-accumulation emulation ORC_TCNN [M] sits 1.74e-3 / 2.08e-3 (these
+        # two query sets, golden weights) from ORC_MIXED, i.e. from this kernel's numerics, and exact f32 math
+        # 1.86e-3 / 1.76e-3: the default path does NOT meet north_star's 1e-3 against the f16-accumulate reading of
+        # tcnn, only against ORC_MIXED. With trained weights the ORC_TCNN distance is 5e-4 - 7e-4
+        # (profiles/r02_sensitivity/sensitivity.json).
+        assert r_tcnn <= 2.5e-3 and r_fp32 <= 2.5e-3
 
 
 def test_infer_unaligned_and_offset_buffers(nrc, orc, torch, dev, net, golden):
