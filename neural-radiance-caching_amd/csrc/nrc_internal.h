@@ -19,6 +19,48 @@ constexpr int kBwdFrags = 2 + 4 * 2 * 4;
 constexpr int kFwdHalves = kFwdFrags * kFragHalves;  // 23552 halves = 46 KiB
 constexpr int kBwdHalves = kBwdFrags * kFragHalves;  // 17408 halves = 34 KiB
 
+// ---- Training layout "t16" (round 2, Frequency encoding): v_mfma_f32_16x16x32_f16 with 16 samples per wave, 8
+// waves = 128 samples per block (nrc_train16.hip). Lane l = (g = l >> 4, c = l & 15). A fragment (1 KiB) is the A
+// operand of one 16x16x32 MFMA for a wave: lane (g, m) holds A[row m][k = 8g + j], j = 0..7.
+// Forward image: L0 4 M-blocks x 3 k-steps (the 96-slot encoder layout below), L1..L4 4 x 2, L5 1 x 2 = 46 frags.
+// Backward image (W_l^T): L5^T 4 M-blocks of a 16x16x16 operand (K = the 16 output rows; 512 B used of each 1-KiB
+// slot, lane (g, m) holds 4 halves k = 4g + j), L4^T..L1^T 4 x 2 = 36 frags.
+__host__ __device__ constexpr int t16_fwd_frag(int layer, int mb, int s) {
+    return layer == 0 ? mb * 3 + s : layer <= 4 ? 12 + (layer - 1) * 8 + mb * 2 + s : 44 + s;
+}
+__host__ __device__ constexpr int t16_bwd_frag(int layer, int mb, int s) {
+    return layer == 5 ? mb : 4 + (layer - 1) * 8 + mb * 2 + s;
+}
+constexpr int kT16FwdFrags = 46, kT16BwdFrags = 36;
+// Row of a 64-row activation / delta held in B-operand k-step s, lane group g, element j: accumulator-as-operand of
+// the 16x16 C layout (M-blocks 2s and 2s + 1, rows 4g .. 4g + 3 of each).
+__host__ __device__ constexpr int t16_row(int s, int g, int j) { return 32 * s + 16 * (j >> 2) + 4 * g + (j & 3); }
+// Layer-0 input: 96 K slots, 24 per lane group g (its 16 samples' features), slot n = 0..23 of group g is
+// K = 32 (n / 8) + 8 g + n % 8. Every lane computes the same kinds in the same slots: n 0..8 TriangleWave (dims
+// n / 3, octaves 3g + n % 3), 9, 10 Identity (dims 2g, 2g + 1), 12..15 / 16..19 OneBlob (dims 2g / 2g + 1),
+// 11 and 20..23 padding 1.0 (pad id 5g + 0..4). Group 3's Identity / OneBlob slots and the pad ids >= 14 are dummies
+// with zero weights. Returns the canonical feature (0..79) of slot K, or -1.
+__host__ __device__ constexpr int t16_slot_feature(int K) {
+    return [](int g, int n) {
+        if (n <= 8) return 12 * (n / 3) + 3 * g + n % 3;
+        if (n == 9 || n == 10) return g < 3 ? 60 + 2 * g + (n - 9) : -1;
+        if (n >= 12 && n <= 19) return g < 3 ? 36 + 4 * (2 * g + (n >= 16)) + (n & 3) : -1;
+        const int pid = 5 * g + (n == 11 ? 0 : n - 19);
+        return pid < 14 ? 66 + pid : -1;
+    }((K % 32) / 8, 8 * (K / 32) + K % 8);
+}
+// Weight-gradient slab of one block in the t16 layout: per layer, 16x16 dW tiles (tm, tn) row-major, each tile
+// [lane 0..63][4 floats] = accumulator register i of lane l: dW[16 tm + 4 (l >> 4) + i][16 tn + (l & 15)] (layer 0:
+// column = K slot). L0 4 x 6 tiles, L1..L4 4 x 4, L5 1 x 4: 23,552 floats, as the 32x32 slab.
+__host__ __device__ constexpr int t16_ntn(int L) { return L == 0 ? 6 : 4; }
+__host__ __device__ constexpr int t16_slab_base(int L, int tm, int tn) {
+    return (L == 0 ? 0 : L <= 4 ? 6144 + (L - 1) * 4096 : 22528) + (tm * t16_ntn(L) + tn) * 256;
+}
+static_assert(t16_slab_base(5, 0, 4) == 23552, "t16 slab size");
+hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                          const _Float16* wf, const _Float16* wb, float* slabs, float* loss_partials, uint64_t* stamps,
+                          hipStream_t s);
+
 // Gradient exchange buffer: loss-scaled dL/dW (NRC_NUM_PARAMS f32) followed by the minibatch loss.
 
 constexpr int kTrainSamplesPerBlock = 128;  // 4 waves x 32 samples
@@ -182,6 +224,7 @@ struct ModelBuffers {
     float *params, *m, *v, *ema, *infer;  // f32 master / Adam / EMA / debiased EMA (inference)
     _Float16 *wf_train, *wb_train, *wf_infer;
     const int *fwd_pos, *bwd_pos;
+    const int* fwdt_pos;  // position in wf_train (the t16 layout for Frequency; fwd_pos otherwise)
     int n_mlp;  // MLP (matrix) parameter count = slab stride: 22528 Frequency, 21504 Hash
     int n_total;  // all parameters (MLP + grid): index of the loss in a data-parallel gradient buffer
     const int* slab_param;  // [n_slab] parameter of each slab position, -1 = padding
