@@ -178,8 +178,9 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* input
  * of its persistent loop, s_memrealtime (100 MHz) at loop start, at loop end and at wave start, HW_ID, XCC_ID:
  * 6 * *waves values into host_dst (at most cap_waves waves). */
 nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, uint32_t* waves);
-/* Diagnostic: the training fwd/bwd kernel with s_memtime phase stamps (16 uint64 per 128-sample block
- * written to stamps_d); performs no optimizer step. */
+/* Diagnostic: the training fwd/bwd kernel with s_memtime phase stamps written to stamps_d: 16 uint64 per wave,
+ * [block][wave 0..3][16] for the Frequency kernel (nrc_train16.hip; size 64 * ceil(b / 128)), [block][16] under
+ * NRC_TRAIN_KERNEL=32; performs no optimizer step. */
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
                                   uint64_t* stamps_d);
 /* Diagnostic: the default inference kernel with s_memtime phase stamps; per wave of its persistent grid, 8 uint64

@@ -2,6 +2,7 @@
 // MFMA weight images and workspaces (the reference's tcnn::TrainableModel, NRCNetwork.cu:15-20).
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -170,6 +171,72 @@ void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd, int encodi
         }
 }
 
+// The same two maps for the t16 training layout (Frequency, nrc_train16.hip): position in the 16x16x32 forward
+// training image (fwdt) and in its backward image (bwd). The inference image keeps build_scatter_maps' fwd.
+void build_t16_maps(std::vector<int>& fwdt, std::vector<int>& bwd) {
+    fwdt.assign(NRC_NUM_PARAMS, -1);
+    bwd.assign(NRC_NUM_PARAMS, -1);
+    auto pos = [](int frag, int lane, int j) { return frag * kFragHalves + lane * 8 + j; };
+    // row o of a 64-row operand <-> (k-step s, lane group g, element j) of t16_row
+    auto sgj = [](int o, int& s, int& g, int& j) {
+        s = o >> 5;
+        g = (o >> 2) & 3;
+        j = 4 * ((o >> 4) & 1) + (o & 3);
+    };
+    for (int K = 0; K < 96; ++K) {
+        const int f = t16_slot_feature(K);
+        if (f < 0) continue;
+        for (int o = 0; o < 64; ++o)
+            fwdt[kLayerOff[0] + o * NRC_ENC_WIDTH + f] = pos(t16_fwd_frag(0, o >> 4, K >> 5), 16 * ((K >> 3) & 3) + (o & 15), K & 7);
+    }
+    for (int l = 1; l <= 4; ++l)
+        for (int o = 0; o < 64; ++o)
+            for (int i = 0; i < 64; ++i) {
+                const int p = kLayerOff[l] + o * 64 + i;
+                int s, g, j;
+                sgj(i, s, g, j);
+                fwdt[p] = pos(t16_fwd_frag(l, o >> 4, s), 16 * g + (o & 15), j);
+                sgj(o, s, g, j);
+                bwd[p] = pos(t16_bwd_frag(l, i >> 4, s), 16 * g + (i & 15), j);
+            }
+    for (int o = 0; o < NRC_OUT_PADDED; ++o)
+        for (int i = 0; i < 64; ++i) {
+            const int p = kLayerOff[5] + o * 64 + i;
+            int s, g, j;
+            sgj(i, s, g, j);
+            fwdt[p] = pos(t16_fwd_frag(5, 0, s), 16 * g + o, j);
+            // W5^T as 16x16x16 A operands: lane (g, m) halves k = 4g + j = output row o, 4 halves per lane
+            bwd[p] = t16_bwd_frag(5, i >> 4, 0) * kFragHalves + (16 * (o >> 2) + (i & 15)) * 4 + (o & 3);
+        }
+}
+
+// Slab map of the t16 layout (t16_slab_pos): register i of lane l of tile (tm, tn) holds dW[16 tm + 4 (l >> 4) + i]
+// [16 tn + (l & 15)] (layer 0: column = K slot -> feature, -1 for the dummy slots).
+std::vector<int> build_t16_slab_map() {
+    std::vector<int> m(slab_floats(0), -1);
+    for (int L = 0; L < NRC_NUM_LAYERS; ++L) {
+        const int ntm = L == 5 ? 1 : 4, in_dim = L == 0 ? NRC_ENC_WIDTH : 64;
+        for (int tm = 0; tm < ntm; ++tm)
+            for (int tn = 0; tn < t16_ntn(L); ++tn)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = 16 * tm + 4 * (lane >> 4) + i, col = 16 * tn + (lane & 15);
+                        const int f = L == 0 ? t16_slot_feature(col) : col;
+                        if (f < 0) continue;
+                        m[t16_slab_pos(L, tm, tn, lane, i)] = kLayerOff[L] + row * in_dim + f;
+                    }
+    }
+    return m;
+}
+
+// Training kernel of a 64-wide Frequency network: the t16 kernel unless NRC_TRAIN_KERNEL=32 selects the round-1
+// 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
+bool want_t16(int encoding) {
+    if (encoding != NRC_ENCODING_FREQUENCY) return false;
+    const char* e = std::getenv("NRC_TRAIN_KERNEL");
+    return !(e && std::string(e) == "32");
+}
+
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
     if (encoding == NRC_ENCODING_FREQUENCY) {
@@ -229,6 +296,8 @@ struct nrc_net {
     float *params = nullptr, *m = nullptr, *v = nullptr, *ema = nullptr, *infer = nullptr;
     _Float16 *wf_train = nullptr, *wb_train = nullptr, *wf_infer = nullptr;
     int *fwd_pos = nullptr, *bwd_pos = nullptr;
+    int* fwdt_pos = nullptr;  // t16 training layout only (else the training image is laid out as fwd_pos)
+    bool t16 = false;         // Frequency training on nrc_train16.hip
     int* slab_param = nullptr;  // [n_slab] parameter of each weight-gradient slab position
     int n_slab = 0;
     float* slabs = nullptr;
@@ -283,7 +352,7 @@ struct nrc_net {
         };
         f(params); f(m); f(v); f(ema); f(infer);
         f(wf_train); f(wb_train); f(wf_infer);
-        f(fwd_pos); f(bwd_pos); f(slab_param);
+        f(fwd_pos); f(bwd_pos); f(fwdt_pos); f(slab_param);
         f(slabs); f(loss_partials);  // loss_dev aliases loss_host (freed below)
         f(work_queue);
         work_queue = nullptr;
@@ -307,7 +376,8 @@ struct nrc_net {
         if (loss_host) (void)hipHostFree(loss_host);
         params = m = v = ema = infer = nullptr;
         wf_train = wb_train = wf_infer = nullptr;
-        fwd_pos = bwd_pos = nullptr;
+        fwd_pos = bwd_pos = fwdt_pos = nullptr;
+        t16 = false;
         slab_param = nullptr;
         slabs = loss_partials = loss_dev = loss_host = nullptr;
         slab_blocks = 0;
@@ -319,6 +389,8 @@ struct nrc_net {
         b.params = params; b.m = m; b.v = v; b.ema = ema; b.infer = infer;
         b.wf_train = wf_train; b.wb_train = wb_train; b.wf_infer = wf_infer;
         b.fwd_pos = fwd_pos; b.bwd_pos = bwd_pos;
+        b.fwdt_pos = fwdt_pos ? fwdt_pos : fwd_pos;
+        b.slab_f16 = t16;
         b.n_mlp = n_mlp;
         b.n_total = (int)n_total();
         b.slab_param = slab_param;
@@ -416,6 +488,20 @@ void wide_grad_partials(nrc_net* net, const float* in, const float* tgt, uint32_
                                         net->wide_ws_d, net->wide_slabs, net->wide_loss_partials, net->stream));
 }
 
+// 64-wide Frequency / FrequencySH fwd + loss + bwd + per-block dW slabs (n_total = 3 x global batch)
+void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total,
+                    uint64_t* stamps = nullptr) {
+    if (net->t16)
+        HIP_CHECK(launch_train16(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                 reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream));
+    else if (stamps)
+        HIP_CHECK(launch_train_stamped(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                       net->slabs, net->loss_partials, stamps, net->stream));
+    else
+        HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                       net->slabs, net->loss_partials, net->stream, net->encoding));
+}
+
 void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h, float* loss_d = nullptr) {
     check_live(net);
     if (b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "batch size must be >= 1");
@@ -439,8 +525,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
                                     net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
                                     net->ensure_scatter(blocks)));
     else
-        HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                       net->slabs, net->loss_partials, net->stream, net->encoding));
+        train_partials(net, in, tgt, b, 3.0f * (float)b);
     net->step += 1;
     HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
                                  loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
@@ -635,10 +720,17 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemset(net->wf_infer, 0, sizeof(_Float16) * kFwdHalves));
         std::vector<int> fwd, bwd;
         build_scatter_maps(fwd, bwd, net->encoding);
+        net->t16 = want_t16(net->encoding);
+        if (net->t16) {
+            std::vector<int> fwdt;
+            build_t16_maps(fwdt, bwd);
+            HIP_CHECK(hipMalloc(&net->fwdt_pos, sizeof(int) * net->n_mlp));
+            HIP_CHECK(hipMemcpy(net->fwdt_pos, fwdt.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
+        }
         HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         {
-            const std::vector<int> sm = build_slab_map(net->encoding);
+            const std::vector<int> sm = net->t16 ? build_t16_slab_map() : build_slab_map(net->encoding);
             net->n_slab = (int)sm.size();
             HIP_CHECK(hipMalloc(&net->slab_param, sizeof(int) * sm.size()));
             HIP_CHECK(hipMemcpy(net->slab_param, sm.data(), sizeof(int) * sm.size(), hipMemcpyHostToDevice));
@@ -863,8 +955,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
                                         net->stream, net->ensure_scatter(blocks)));
             HIP_CHECK(launch_grid_grad_export(net->grid_grad, grad_d + net->n_mlp, net->n_grid, net->stream));
         } else {
-            HIP_CHECK(launch_train_fwd_bwd(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
-                                           net->wb_train, net->slabs, net->loss_partials, net->stream, net->encoding));
+            train_partials(net, in, tgt, b, 3.0f * (float)global_b);
         }
         HIP_CHECK(launch_reduce_adam(kReduceOnly, net->slabs, blocks, net->loss_partials, grad_d, nullptr,
                                      net->buffers(), net->optim(net->step + 1), net->stream));
@@ -1066,8 +1157,7 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tg
         if (!in || !tgt || !stamps_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
-        HIP_CHECK(launch_train_stamped(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                       net->slabs, net->loss_partials, stamps_d, net->stream));
+        train_partials(net, in, tgt, b, 3.0f * (float)b, stamps_d);
     });
 }
 

@@ -164,4 +164,37 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// ---- tcnn Adam + EMA (optimizers/adam.h, exponential_moving_average.h) of one parameter with its f16
+// image packs, shared by reduce_adam_kernel (nrc_kernels.hip) and the fused optimizer phase of nrc_train16.hip.
+// adam_pack_one (mode kReduceFused) split into its loads and the rest, same float operations
+struct AdamIn {
+    float w, m, v, ema;
+    int fp, ft, bp;
+};
+__device__ __forceinline__ AdamIn adam_load(int p, const ModelBuffers& mb) {
+    return AdamIn{mb.params[p], mb.m[p], mb.v[p], mb.ema[p], mb.fwd_pos[p], mb.fwdt_pos[p], mb.bwd_pos[p]};
+}
+__device__ __forceinline__ void adam_pack_pre(int p, float gsum, const AdamIn& in, const ModelBuffers& mb,
+                                              const OptimArgs& oa, float lr_t, float ema_debias) {
+#pragma clang fp contract(off)
+    float gradient = gsum / oa.loss_scale;
+    float w = in.w;
+    gradient += oa.l2_reg * w;
+    const float gsq = gradient * gradient;
+    const float m1 = oa.beta1 * in.m + (1.0f - oa.beta1) * gradient;
+    const float v1 = oa.beta2 * in.v + (1.0f - oa.beta2) * gsq;
+    mb.m[p] = m1;
+    mb.v[p] = v1;
+    const float eff = lr_t / (sqrtf(v1) + oa.eps);
+    w = w - eff * m1;
+    mb.params[p] = w;
+    const float e = in.ema * oa.ema_decay + w * (1.0f - oa.ema_decay);
+    mb.ema[p] = e;
+    const float inf = e / ema_debias;
+    mb.infer[p] = inf;
+    mb.wf_train[in.ft] = (_Float16)w;
+    mb.wf_infer[in.fp] = (_Float16)inf;
+    if (in.bp >= 0) mb.wb_train[in.bp] = (_Float16)w;
+}
+
 }  // namespace nrc_amd

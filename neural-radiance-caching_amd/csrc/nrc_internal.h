@@ -49,17 +49,19 @@ __host__ __device__ constexpr int t16_slot_feature(int K) {
         return pid < 14 ? 66 + pid : -1;
     }((K % 32) / 8, 8 * (K / 32) + K % 8);
 }
-// Weight-gradient slab of one block in the t16 layout: per layer, 16x16 dW tiles (tm, tn) row-major, each tile
-// [lane 0..63][4 floats] = accumulator register i of lane l: dW[16 tm + 4 (l >> 4) + i][16 tn + (l & 15)] (layer 0:
-// column = K slot). L0 4 x 6 tiles, L1..L4 4 x 4, L5 1 x 4: 23,552 floats, as the 32x32 slab.
+// Weight-gradient slab of one block in the t16 layout (f16 elements): per layer, 16x16 dW tiles (tm, tn) row-major
+// (L0 4 x 6 tiles, L1..L4 4 x 4, L5 1 x 4: 23,552 elements, as the 32x32 slab), stored as column pairs: tiles
+// (tm, 2p) and (tm, 2p + 1) are one 1-KiB record [lane 0..63][8], elements 0..3 = accumulator registers 0..3 of the
+// even tile, 4..7 of the odd one, so a wave holding both writes them with one 16-byte store per lane. Register i of
+// lane l holds dW[16 tm + 4 (l >> 4) + i][16 tn + (l & 15)] (layer 0: column = K slot).
 __host__ __device__ constexpr int t16_ntn(int L) { return L == 0 ? 6 : 4; }
 __host__ __device__ constexpr int t16_slab_base(int L, int tm, int tn) {
     return (L == 0 ? 0 : L <= 4 ? 6144 + (L - 1) * 4096 : 22528) + (tm * t16_ntn(L) + tn) * 256;
 }
+__host__ __device__ constexpr int t16_slab_pos(int L, int tm, int tn, int lane, int i) {
+    return t16_slab_base(L, tm, tn & ~1) + lane * 8 + 4 * (tn & 1) + i;
+}
 static_assert(t16_slab_base(5, 0, 4) == 23552, "t16 slab size");
-hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
-                          const _Float16* wf, const _Float16* wb, float* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s);
 
 // Gradient exchange buffer: loss-scaled dL/dW (NRC_NUM_PARAMS f32) followed by the minibatch loss.
 
@@ -225,11 +227,19 @@ struct ModelBuffers {
     _Float16 *wf_train, *wb_train, *wf_infer;
     const int *fwd_pos, *bwd_pos;
     const int* fwdt_pos;  // position in wf_train (the t16 layout for Frequency; fwd_pos otherwise)
+    bool slab_f16;        // slabs hold f16 partials (t16)
     int n_mlp;  // MLP (matrix) parameter count = slab stride: 22528 Frequency, 21504 Hash
     int n_total;  // all parameters (MLP + grid): index of the loss in a data-parallel gradient buffer
     const int* slab_param;  // [n_slab] parameter of each slab position, -1 = padding
     int n_slab;             // slab stride (floats per training block)
 };
+
+// slabs: f16 (nrc_train16.hip slab_pair), reduced by launch_reduce_adam (ModelBuffers::slab_f16)
+hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                          const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
+                          hipStream_t s);
+// host-f32 Adam step-size and EMA debias of optimizer step oa.step (tcnn adam.h; identical to the oracle's)
+void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias);
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;

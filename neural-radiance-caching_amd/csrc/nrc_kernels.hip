@@ -13,6 +13,8 @@
 // as pre-swizzled A-operand "fragment images" (one ds_read_b128 per MFMA), packed by
 // reduce_adam_kernel after every optimizer step. Weight gradients (a contraction over samples) go
 // through a per-block LDS transpose read with ds_read_b64_tr_b16.
+#include <cstdlib>
+
 #include "nrc_device.h"
 
 namespace nrc_amd {
@@ -2290,46 +2292,16 @@ __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const
         inf = e / ema_debias;
         mb.infer[p] = inf;
     }
-    const int fp = mb.fwd_pos[p];
-    mb.wf_train[fp] = (_Float16)w;
-    mb.wf_infer[fp] = (_Float16)inf;
+    mb.wf_train[mb.fwdt_pos[p]] = (_Float16)w;
+    mb.wf_infer[mb.fwd_pos[p]] = (_Float16)inf;
     const int bp = mb.bwd_pos[p];
     if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
 }
 
-// adam_pack_one (mode kReduceFused) split into its loads and the rest, same float operations
-struct AdamIn {
-    float w, m, v, ema;
-    int fp, bp;
-};
-__device__ __forceinline__ AdamIn adam_load(int p, const ModelBuffers& mb) {
-    return AdamIn{mb.params[p], mb.m[p], mb.v[p], mb.ema[p], mb.fwd_pos[p], mb.bwd_pos[p]};
-}
-__device__ __forceinline__ void adam_pack_pre(int p, float gsum, const AdamIn& in, const ModelBuffers& mb,
-                                              const OptimArgs& oa, float lr_t, float ema_debias) {
-#pragma clang fp contract(off)
-    float gradient = gsum / oa.loss_scale;
-    float w = in.w;
-    gradient += oa.l2_reg * w;
-    const float gsq = gradient * gradient;
-    const float m1 = oa.beta1 * in.m + (1.0f - oa.beta1) * gradient;
-    const float v1 = oa.beta2 * in.v + (1.0f - oa.beta2) * gsq;
-    mb.m[p] = m1;
-    mb.v[p] = v1;
-    const float eff = lr_t / (sqrtf(v1) + oa.eps);
-    w = w - eff * m1;
-    mb.params[p] = w;
-    const float e = in.ema * oa.ema_decay + w * (1.0f - oa.ema_decay);
-    mb.ema[p] = e;
-    const float inf = e / ema_debias;
-    mb.infer[p] = inf;
-    mb.wf_train[in.fp] = (_Float16)w;
-    mb.wf_infer[in.fp] = (_Float16)inf;
-    if (in.bp >= 0) mb.wb_train[in.bp] = (_Float16)w;
-}
-
 // The per-slab loss partials are summed by wave 0 of block 0: a strided per-lane sum and a fixed xor
 // butterfly (one load latency instead of a serial chain of nslabs loads).
+// H: f16 slabs (the t16 training kernel's), converted to f32 before the same fixed-order f32 sums
+template <bool H>
 __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
                                                           const float* __restrict__ loss_partials,
                                                           float* __restrict__ grad_io, float* __restrict__ loss_out,
@@ -2363,12 +2335,20 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             if (mode == kReduceFused && pp >= 0) ain = adam_load(pp, mb);
         }
         f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        auto ld = [&](int slab) -> f4 {
+            if constexpr (H) {
+                const h4 v = *(const h4*)((const _Float16*)slabs + (int64_t)slab * mb.n_slab + p0);
+                return f4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+            } else {
+                return *(const f4*)&slabs[(int64_t)slab * mb.n_slab + p0];
+            }
+        };
         int i = grp;
         for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
             f4 v[8];
             // plain loads (0.4 us per step faster than nontemporal ones here)
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = *(const f4*)&slabs[(int64_t)(i + u * kRedGroups) * mb.n_slab + p0];
+            for (int u = 0; u < 8; ++u) v[u] = ld(i + u * kRedGroups);
 #pragma unroll
             for (int u = 0; u < 8; u += 2) {
                 a0 += v[u];
@@ -2376,7 +2356,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             }
         }
         for (int u = 0; i < nslabs; i += kRedGroups, ++u) {
-            const f4 v = *(const f4*)&slabs[(int64_t)i * mb.n_slab + p0];
+            const f4 v = ld(i);
             if (u & 1) a1 += v;
             else a0 += v;
         }
@@ -3440,16 +3420,25 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials, float* grad_io,
-                              float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias) {
     // Bias corrections in host f32 (glibc powf/sqrtf), identical to the oracle's.
     const float step = (float)(oa.step ? oa.step : 1);
-    const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
-    const float ema_debias = 1.0f - powf(oa.ema_decay, step);
+    lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
+    ema_debias = 1.0f - powf(oa.ema_decay, step);
+}
+
+hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials, float* grad_io,
+                              float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+    float lr_t, ema_debias;
+    adam_host_factors(oa, lr_t, ema_debias);
     // reduce modes walk the slab positions, apply / pack modes the parameters
     const int grid = (mode == kReduceFused || mode == kReduceOnly ? mb.n_slab : mb.n_mlp) / (kRedParams * kRedVec);
-    hipLaunchKernelGGL(reduce_adam_kernel, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials, grad_io,
-                       loss_out, mb, oa, lr_t, ema_debias);
+    if (mb.slab_f16)
+        hipLaunchKernelGGL(reduce_adam_kernel<true>, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials,
+                           grad_io, loss_out, mb, oa, lr_t, ema_debias);
+    else
+        hipLaunchKernelGGL(reduce_adam_kernel<false>, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs,
+                           loss_partials, grad_io, loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();
 }
 

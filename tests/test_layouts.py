@@ -81,3 +81,51 @@ def test_slab_positions_cover_every_weight_once():
                             seen[key] = pos
         assert len(seen) == n
         assert max(seen.values()) < slab_block_base(enc, 5, 0, 2)
+
+
+# ---- t16 training layout (neural-radiance-caching_amd/csrc/nrc_train16.hip swz64 / off64 / swz32 / off32)
+def swz64(r):
+    return (r & 1) | (((r >> 2) & 1) << 1) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3)
+
+
+def off64(r, Q):
+    return r * 128 + 8 * (Q ^ swz64(r))
+
+
+def swz32(r):
+    return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | (((r >> 3) & 1) << 2)
+
+
+def off32(r, Q):
+    return r * 64 + 8 * (Q ^ swz32(r))
+
+
+def test_t16_images_are_bijections():
+    assert sorted(off64(r, Q) for r in range(128) for Q in range(16)) == list(range(0, 128 * 128, 8))
+    assert sorted(off32(r, Q) for r in range(128) for Q in range(8)) == list(range(0, 128 * 64, 8))
+
+
+def test_t16_row_writes_are_conflict_free():
+    # ds_write_b64: 16 contiguous lanes per LDS cycle, banks (a / 4) mod 32; a 16-lane group is 16 consecutive
+    # samples (rows 16k .. 16k + 15) writing the same quad
+    for off, nq in ((off64, 16), (off32, 8)):
+        for k in range(8):
+            for Q in range(nq):
+                banks = [(off(16 * k + c, Q) // 4 + i) % 32 for c in range(16) for i in range(2)]
+                assert len(set(banks)) == 32, (off.__name__, k, Q)
+
+
+def test_t16_transposed_reads_are_conflict_free():
+    # ds_read_b64_tr_b16: 32-lane halves, banks (a / 4) mod 64; lane (G, q, p) reads row 32 kk + 8 G + q (+ 4) of the
+    # tile's quad 4 t + p
+    for off, ntile in ((off64, 4), (off32, 2)):
+        for t in range(ntile):
+            for kk in range(4):
+                for second in range(2):
+                    for half in range(2):
+                        banks = []
+                        for lane in range(32 * half, 32 * half + 32):
+                            G, q, p = lane >> 4, (lane >> 2) & 3, lane & 3
+                            a = off(32 * kk + 8 * G + 4 * second + q, 4 * t + p)
+                            banks += [(a // 4) % 64, (a // 4 + 1) % 64]
+                        assert len(set(banks)) == 64, (off.__name__, t, kk, second, half)
