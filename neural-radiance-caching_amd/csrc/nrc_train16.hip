@@ -522,9 +522,9 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
     stamp();
 
     // ---- steps 4..1: dW_L from buffer L & 1, delta_{L-1} into the other buffer with a_{L-2} (step 1: the input
-    // slots 0..63, quads 8s + 2g, 8s + 2g + 1). Phases fenced by sched_barrier: operand reads; the chain's MFMAs of
-    // group 0, then group 1; the dW tiles of row 0 with group 0's gate, then row 1 with group 1's; the image writes
-    // and the next layer's W^T reads. One deferred slab store in each of the four MFMA phases.
+    // slots 0..63, quads 8s + 2g, 8s + 2g + 1). Phases fenced by sched_barrier: the dW operand reads and the a_{L-2}
+    // writes; the chain's MFMAs of group 0, then group 1 (each with one deferred slab store); the next layer's W^T
+    // reads; the dW tiles of row 0 with group 0's gate and delta writes, then row 1 with group 1's.
 #define NRC_T16_STEP(L, IMGD, IMGA, NIMGD, NIMGA)                                                                  \
     {                                                                                                              \
         TrTile ta[2], tb[2];                                                                                       \
@@ -533,6 +533,18 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
         _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int kk = 0; kk < 4; ++kk) {           \
             A[i][kk] = tr_op(ta[i], kk);                                                                           \
             B[i][kk] = tr_op(tb[i], kk);                                                                           \
+        }                                                                                                          \
+        /* a_{L-2} (step 1: the input slots 0..63) does not depend on this step: written first */                  \
+        _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
+            if constexpr (L > 1) {                                                                                 \
+                put_rows64(NIMGA, wo[u], a[L > 1 ? L - 2 : 0][u]);                                                 \
+            } else {                                                                                               \
+                _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                 \
+                    const u4 w = __builtin_bit_cast(u4, x[u][ks]);                                                 \
+                    *(u2*)(NIMGA + off64(r[u], 8 * ks + 2 * g)) = u2{w.x, w.y};                                    \
+                    *(u2*)(NIMGA + off64(r[u], 8 * ks + 2 * g + 1)) = u2{w.z, w.w};                                \
+                }                                                                                                  \
+            }                                                                                                      \
         }                                                                                                          \
         __builtin_amdgcn_sched_barrier(0);                                                                         \
         f4 cc[2][4];                                                                                               \
@@ -544,6 +556,8 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
             flush(u);                                                                                              \
             __builtin_amdgcn_sched_barrier(0);                                                                     \
         }                                                                                                          \
+        /* W is dead after the chain: the next layer's W^T reads go out with the first dW half */                  \
+        if constexpr (L > 1) load_wt<(L > 1 ? L - 1 : 1)>(lwb, lane, W);                                            \
         f4 acc[2][2];                                                                                              \
         _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                            \
             _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                        \
@@ -552,21 +566,9 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
             }                                                                                                      \
             _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2)                                                       \
                 dn[i][s2] = gate_b(cc[i][2 * s2], cc[i][2 * s2 + 1], a[L - 1][i][s2]);                             \
+            put_rows64(NIMGD, wo[i], dn[i]);                                                                       \
             __builtin_amdgcn_sched_barrier(0);                                                                     \
         }                                                                                                          \
-        _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
-            put_rows64(NIMGD, wo[u], dn[u]);                                                                       \
-            if constexpr (L > 1) {                                                                                 \
-                put_rows64(NIMGA, wo[u], a[L > 1 ? L - 2 : 0][u]);                                                 \
-            } else {                                                                                               \
-                _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                 \
-                    const u4 w = __builtin_bit_cast(u4, x[u][ks]);                                                 \
-                    *(u2*)(NIMGA + off64(r[u], 8 * ks + 2 * g)) = u2{w.x, w.y};                                    \
-                    *(u2*)(NIMGA + off64(r[u], 8 * ks + 2 * g + 1)) = u2{w.z, w.w};                                \
-                }                                                                                                  \
-            }                                                                                                      \
-        }                                                                                                          \
-        if constexpr (L > 1) load_wt<(L > 1 ? L - 1 : 1)>(lwb, lane, W);                                            \
         _Pragma("unroll") for (int i = 0; i < 2; ++i) pend[i] = pack_pair(acc[i][0], acc[i][1]);                    \
         pend_L = L;                                                                                                \
         _Pragma("unroll") for (int u = 0; u < 2; ++u)                                                              \
