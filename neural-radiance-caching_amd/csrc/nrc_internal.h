@@ -174,7 +174,8 @@ hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, h
 
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
-// wq: the handle's work-queue counters (2 x u32, zero between launches), needed by the queue variants (37, 38)
+// variants kept for A/B: 0, 23, 30, 39 (default), 40 (39 + in-kernel clock); wq is unused since the launch-wide
+// queue variants were removed
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s, uint32_t* wq = nullptr);
 constexpr int kNumInferVariants = 41;

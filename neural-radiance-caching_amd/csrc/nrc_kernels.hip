@@ -1050,16 +1050,6 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
     infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, InferEpilogue{});
 }
 
-// the same with the launch-wide work queue (ABL & 4096): wq = the handle's two zeroed counters
-template <int TILES, int WAVES_PER_EU, int THREADS, bool PREFETCH, int ABL>
-__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_q(const float* __restrict__ q,
-                                                                        float* __restrict__ out, int64_t n,
-                                                                        const h8* __restrict__ wf, uint32_t* wq) {
-    InferEpilogue e{};
-    e.wq = wq;
-    infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, e);
-}
-
 // Diagnostic build of the default inference kernel (variant 23) with per-wave phase stamps (ABL & 256).
 __global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                              int64_t n, const h8* __restrict__ wf,
@@ -1474,256 +1464,6 @@ __global__ void fp8_convert_kernel(const float* __restrict__ x, uint8_t* __restr
     if (i >= n) return;
     const float a = __builtin_amdgcn_fmed3f(x[i], relu ? 0.0f : -448.0f, 448.0f);
     y[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.0f, 0, false) & 0xffu);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Inference v3: weight fragments resident in registers (loaded once per wave from LDS), so the MFMA
-// stream never waits on LDS. RESIDENT = 46: every layer in registers (1 wave per SIMD, TILES
-// independent tiles interleaved for ILP); RESIDENT = 32: hidden layers 1..4 in registers, input and
-// output layers re-read from LDS (fits 2 waves per SIMD).
-// ------------------------------------------------------------------------------------------------
-template <int TILES, int KK>
-__device__ __forceinline__ void layer_regs(const h8* a0, const h8* a1, const h8 (&in)[TILES][KK],
-                                           h8 (&y)[TILES][4]) {
-    f16v c[TILES][2];
-#pragma unroll
-    for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) {
-            c[t][0] = mfma(a0[kk], in[t][kk], c[t][0]);
-            c[t][1] = mfma(a1[kk], in[t][kk], c[t][1]);
-        }
-#pragma unroll
-    for (int t = 0; t < TILES; ++t) {
-        y[t][0] = relu_h8(c[t][0], 0);
-        y[t][1] = relu_h8(c[t][0], 8);
-        y[t][2] = relu_h8(c[t][1], 0);
-        y[t][3] = relu_h8(c[t][1], 8);
-    }
-}
-
-template <int TILES, int RESIDENT, int WAVES_PER_EU>
-__global__ __launch_bounds__(256, WAVES_PER_EU) void infer_kernel_v3(const float* __restrict__ q,
-                                                                     float* __restrict__ out, int64_t n,
-                                                                     const h8* __restrict__ wf) {
-    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
-    copy_to_lds<256, kFwdFrags * 64>(lw, wf);
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, r = lane & 31;
-    constexpr int F0 = RESIDENT == 46 ? 0 : 10;  // first register-resident fragment
-    h8 wr[RESIDENT];
-#pragma unroll
-    for (int f = 0; f < RESIDENT; ++f) wr[f] = lw[(F0 + f) * 64 + lane];
-
-    const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
-    const int64_t wstride = (int64_t)gridDim.x * 4;
-    int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= ngroups) return;
-    const int64_t last = n - 1;
-
-    QLane Q[TILES];
-#pragma unroll
-    for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
-    for (; g < ngroups; g += wstride) {
-        h8 x[TILES][5];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) encode_fast(Q[t], h, x[t]);
-        const int64_t ng = g + wstride;
-        if (ng < ngroups) {
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
-        }
-        h8 y[TILES][4], z[TILES][4];
-        if (RESIDENT == 46) {
-            layer_regs<TILES, 5>(&wr[fwd_frag(0, 0, 0)], &wr[fwd_frag(0, 1, 0)], x, y);
-        } else {
-            lds_h8* wl = launder((lds_h8*)(lw + lane));
-            h8 a0[5], a1[5];
-#pragma unroll
-            for (int kk = 0; kk < 5; ++kk) {
-                a0[kk] = wl[fwd_frag(0, 0, kk) * 64];
-                a1[kk] = wl[fwd_frag(0, 1, kk) * 64];
-            }
-            layer_regs<TILES, 5>(a0, a1, x, y);
-        }
-        layer_regs<TILES, 4>(&wr[fwd_frag(1, 0, 0) - F0], &wr[fwd_frag(1, 1, 0) - F0], y, z);
-        layer_regs<TILES, 4>(&wr[fwd_frag(2, 0, 0) - F0], &wr[fwd_frag(2, 1, 0) - F0], z, y);
-        layer_regs<TILES, 4>(&wr[fwd_frag(3, 0, 0) - F0], &wr[fwd_frag(3, 1, 0) - F0], y, z);
-        layer_regs<TILES, 4>(&wr[fwd_frag(4, 0, 0) - F0], &wr[fwd_frag(4, 1, 0) - F0], z, y);
-        f16v o[TILES];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) o[t] = zero16();
-        h8 a5[4];
-        if (RESIDENT == 46) {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) a5[kk] = wr[fwd_frag(5, 0, kk)];
-        } else {
-            lds_h8* wl = launder((lds_h8*)(lw + lane));
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) a5[kk] = wl[fwd_frag(5, 0, kk) * 64];
-        }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) o[t] = mfma(a5[kk], y[t][kk], o[t]);
-        if (h == 0) {
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) {
-                const int64_t s = (g * TILES + t) * 32 + r;
-                if (s < n) {
-                    float* dst = out + s * NRC_OUTPUT_DIMS;
-                    dst[0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
-                    dst[1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
-                    dst[2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
-                }
-            }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Inference v4: explicit weight-fragment prefetch. Layer l+1's fragments are issued (inline-asm
-// ds_read_b128, which the scheduler cannot sink next to its consumer) before layer l's MFMAs and
-// retired by a counted s_waitcnt lgkmcnt right before layer l+1 — LDS latency hides under a whole
-// layer of MFMAs. The next tile's layer-0 fragments are issued before the output layer. The loop holds
-// no other LDS or scalar-memory traffic, so lgkmcnt counts exactly these reads (in issue order).
-// ------------------------------------------------------------------------------------------------
-template <int OFF>
-__device__ __forceinline__ void ldsrd(h8& d, uint32_t base) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(OFF * 1024));
-}
-#define NRC_RD_LAYER4(A, L)                                      \
-    ldsrd<fwd_frag(L, 0, 0)>(A[0][0], base);                      \
-    ldsrd<fwd_frag(L, 0, 1)>(A[0][1], base);                      \
-    ldsrd<fwd_frag(L, 0, 2)>(A[0][2], base);                      \
-    ldsrd<fwd_frag(L, 0, 3)>(A[0][3], base);                      \
-    ldsrd<fwd_frag(L, 1, 0)>(A[1][0], base);                      \
-    ldsrd<fwd_frag(L, 1, 1)>(A[1][1], base);                      \
-    ldsrd<fwd_frag(L, 1, 2)>(A[1][2], base);                      \
-    ldsrd<fwd_frag(L, 1, 3)>(A[1][3], base);
-#define NRC_RD_LAYER0(A)                                         \
-    ldsrd<fwd_frag(0, 0, 0)>(A[0][0], base);                      \
-    ldsrd<fwd_frag(0, 0, 1)>(A[0][1], base);                      \
-    ldsrd<fwd_frag(0, 0, 2)>(A[0][2], base);                      \
-    ldsrd<fwd_frag(0, 0, 3)>(A[0][3], base);                      \
-    ldsrd<fwd_frag(0, 0, 4)>(A[0][4], base);                      \
-    ldsrd<fwd_frag(0, 1, 0)>(A[1][0], base);                      \
-    ldsrd<fwd_frag(0, 1, 1)>(A[1][1], base);                      \
-    ldsrd<fwd_frag(0, 1, 2)>(A[1][2], base);                      \
-    ldsrd<fwd_frag(0, 1, 3)>(A[1][3], base);                      \
-    ldsrd<fwd_frag(0, 1, 4)>(A[1][4], base);
-#define NRC_RD_LAYER5(A)                                         \
-    ldsrd<fwd_frag(5, 0, 0)>(A[0], base);                         \
-    ldsrd<fwd_frag(5, 0, 1)>(A[1], base);                         \
-    ldsrd<fwd_frag(5, 0, 2)>(A[2], base);                         \
-    ldsrd<fwd_frag(5, 0, 3)>(A[3], base);
-
-// Wait until at most N LDS reads are outstanding; the "+v" ties stop the compiler from using the
-// fragments before this point, sched_barrier stops it from hoisting MFMAs above it (guide §5.4 rule 18).
-template <int N, int KK>
-__device__ __forceinline__ void lds_wait(h8 (&a)[2][KK]) {
-    if constexpr (KK == 5)
-        asm volatile("s_waitcnt lgkmcnt(%10)"
-                     : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[0][4]), "+v"(a[1][0]),
-                       "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]), "+v"(a[1][4])
-                     : "i"(N));
-    else
-        asm volatile("s_waitcnt lgkmcnt(%8)"
-                     : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]), "+v"(a[1][1]),
-                       "+v"(a[1][2]), "+v"(a[1][3])
-                     : "i"(N));
-    __builtin_amdgcn_sched_barrier(0);
-}
-template <int N>
-__device__ __forceinline__ void lds_wait5(h8 (&a)[4]) {
-    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "i"(N));
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int TILES, int THREADS, int WAVES_PER_EU>
-__global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v4(const float* __restrict__ q,
-                                                                         float* __restrict__ out, int64_t n,
-                                                                         const h8* __restrict__ wf) {
-    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
-    copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, r = lane & 31;
-    const int64_t ngroups = (((n + 31) >> 5) + TILES - 1) / TILES;
-    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
-    // wave-uniform tile index (readfirstlane: scalar address arithmetic, scalar buffer descriptors)
-    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (g >= ngroups) return;
-    const int64_t last = n - 1;
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_h8*)(lw + lane);
-
-    QLane Q[TILES];
-#pragma unroll
-    for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((g * TILES + t) * 32 + r, last), h);
-    h8 w0[2][5];
-    NRC_RD_LAYER0(w0);
-    __builtin_amdgcn_sched_barrier(0);
-    for (; g < ngroups; g += wstride) {
-        h8 x[TILES][5];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) encode_fast(Q[t], h, x[t]);
-        const int64_t ng = g + wstride;
-        if (ng < ngroups) {
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) Q[t] = load_q(q, min((ng * TILES + t) * 32 + r, last), h);
-        }
-        h8 wa[2][4], wb[2][4], w5[4];
-        h8 y[TILES][4], z[TILES][4];
-        __builtin_amdgcn_sched_barrier(0);
-        NRC_RD_LAYER4(wa, 1);
-        lds_wait<8>(w0);
-        layer_mfma<TILES, 5>(w0, x, y);
-        __builtin_amdgcn_sched_barrier(0);
-        NRC_RD_LAYER4(wb, 2);
-        lds_wait<8>(wa);
-        layer_mfma<TILES, 4>(wa, y, z);
-        __builtin_amdgcn_sched_barrier(0);
-        NRC_RD_LAYER4(wa, 3);
-        lds_wait<8>(wb);
-        layer_mfma<TILES, 4>(wb, z, y);
-        __builtin_amdgcn_sched_barrier(0);
-        NRC_RD_LAYER4(wb, 4);
-        lds_wait<8>(wa);
-        layer_mfma<TILES, 4>(wa, y, z);
-        __builtin_amdgcn_sched_barrier(0);
-        NRC_RD_LAYER5(w5);
-        lds_wait<4>(wb);
-        layer_mfma<TILES, 4>(wb, z, y);
-        __builtin_amdgcn_sched_barrier(0);
-        NRC_RD_LAYER0(w0);  // next tile's layer 0
-        lds_wait5<10>(w5);
-        f16v o[TILES];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) o[t] = zero16();
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) o[t] = mfma(w5[kk], y[t][kk], o[t]);
-        if (h == 0) {
-#pragma unroll
-            for (int t = 0; t < TILES; ++t) {
-                const int64_t s = (g * TILES + t) * 32 + r;
-                if (s < n) {
-                    float* dst = out + s * NRC_OUTPUT_DIMS;
-                    dst[0] = (float)(_Float16)fmaxf(o[t][0], 0.0f);
-                    dst[1] = (float)(_Float16)fmaxf(o[t][1], 0.0f);
-                    dst[2] = (float)(_Float16)fmaxf(o[t][2], 0.0f);
-                }
-            }
-        }
-    }
-    // drain the speculative layer-0 reads before the wave exits
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // Standalone encoding kernel (HBM-bound; used by the parity tests of the encoding): writes the f32
@@ -2696,219 +2436,6 @@ __global__ __launch_bounds__(256) void wide_adam_kernel(int mode, const float* _
 
 
 // ------------------------------------------------------------------------------------------------
-// Ping-pong inference (variant 26). One wave owns two 32-query tiles A and B per iteration and runs them
-// through the network half a layer apart: while tile A's MFMAs of layer l issue, the VALU converts tile B's
-// layer l-1 accumulators (ReLU + f16 pack) into its next B operand, and vice versa. The next iteration's two tiles
-// are encoded in slices spread over the same phases, so every phase carries MFMAs and VALU of independent chains
-// and a wave can fill its own MFMA gaps (cdna_hip_programming.md T19); both tiles share each weight-fragment read,
-// which halves the LDS traffic per MFMA. Same arithmetic as infer_v2_body (bit-identical outputs).
-// ------------------------------------------------------------------------------------------------
-// encode_fast<CHAIN = true> split into slices: 0-2 triangle wave of position dim d, 3-5 OneBlob input i, 6 identity
-// and pads. FAST: the wave's OneBlob inputs satisfy -3 <= 4x < 7 (blob_many's in-range branch).
-template <int K, bool FAST>
-__device__ __forceinline__ void enc_slice(const QLane& Q, int h, uint32_t (&w)[20]) {
-    if constexpr (K < 3) {
-        const float hs = h ? 64.0f : 1.0f;
-        const float p = (K == 0 ? Q.p0 : K == 1 ? Q.p1 : Q.p2) * hs;
-        float g[6];
-        g[0] = fract2_abs(p);
-#pragma unroll
-        for (int k = 1; k < 6; ++k) g[k] = fract2(g[k - 1]);
-#pragma unroll
-        for (int k = 0; k < 6; k += 2) w[(K * 6 + k) >> 1] = pk2_abs(g[k] - 1.0f, g[k + 1] - 1.0f);
-    } else if constexpr (K < 6) {
-        const float x = K == 3 ? Q.b0 : K == 4 ? Q.b1 : Q.b2;
-        blob_fast<FAST>(x, w[9 + 2 * (K - 3)], w[10 + 2 * (K - 3)]);
-    } else {
-        w[15] = pk2(Q.i0, Q.i1);
-        w[16] = pk2(Q.i2, 1.0f);
-        w[17] = w[18] = w[19] = 0x3C003C00u;
-    }
-}
-
-__device__ __forceinline__ void enc_words_to_frags(const uint32_t (&w)[20], h8 (&x)[5]) {
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-        u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
-        x[kk] = __builtin_bit_cast(h8, t4);
-    }
-}
-
-__device__ __forceinline__ bool blob_in_range(const QLane& Q) {
-    const float t0 = Q.b0 * 4.0f, t1 = Q.b1 * 4.0f, t2 = Q.b2 * 4.0f;
-    return t0 >= -3.0f && t0 < 7.0f && t1 >= -3.0f && t1 < 7.0f && t2 >= -3.0f && t2 < 7.0f;
-}
-
-// one layer's MFMAs for one tile: M-block 0's K chain, then M-block 1's
-template <int KK>
-__device__ __forceinline__ void pp_mfma(const h8 (&a)[2][KK], const h8 (&in)[KK], f16v (&c)[2]) {
-    c[0] = zero16();
-    c[1] = zero16();
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) c[0] = mfma(a[0][kk], in[kk], c[0]);
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) c[1] = mfma(a[1][kk], in[kk], c[1]);
-}
-__device__ __forceinline__ void pp_relu(const f16v (&c)[2], h8 (&y)[4]) {
-    y[0] = relu_h8(c[0], 0);
-    y[1] = relu_h8(c[0], 8);
-    y[2] = relu_h8(c[1], 0);
-    y[3] = relu_h8(c[1], 8);
-}
-// interleave: per MFMA one group of NV VALU (LLVM SchedGroupMask: MFMA 0x8, VALU 0x2)
-template <int NM, int NV>
-__device__ __forceinline__ void pp_pattern() {
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x2, NV, 0);
-    }
-}
-#define PP_FENCE() __builtin_amdgcn_sched_barrier(0)
-
-// One iteration: tiles (xA, xB) through the network into oA/oB; (QA, QB) encoded into (nA, nB) meanwhile.
-template <bool FAST, int SCHED>
-__device__ __forceinline__ void pp_iteration(lds_h8* lw_lane, const h8 (&xA)[5], const h8 (&xB)[5], const QLane& QA,
-                                             const QLane& QB, int h, h8 (&nA)[5], h8 (&nB)[5], f16v& oA, f16v& oB) {
-    uint32_t wA[20], wB[20];
-    f16v cA[2], cB[2];
-    h8 yA[4], yB[4];
-    lds_h8* wl = launder(lw_lane);
-    h8 a0[2][5];
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-        a0[0][kk] = wl[fwd_frag(0, 0, kk) * 64];
-        a0[1][kk] = wl[fwd_frag(0, 1, kk) * 64];
-    }
-    // P1: layer 0 (A) | encode: identity of both, OneBlob 2 and triangle dim 0 of A
-    PP_FENCE();
-    pp_mfma<5>(a0, xA, cA);
-    enc_slice<6, FAST>(QA, h, wA);
-    enc_slice<6, FAST>(QB, h, wB);
-    enc_slice<5, FAST>(QA, h, wA);
-    enc_slice<0, FAST>(QA, h, wA);
-    if constexpr (SCHED) pp_pattern<10, 5>();
-    PP_FENCE();
-    // P2: layer 0 (B) | ReLU(A), triangle dim 0 of B
-    pp_mfma<5>(a0, xB, cB);
-    pp_relu(cA, yA);
-    enc_slice<0, FAST>(QB, h, wB);
-    h8 a[2][4];
-    wl = launder(lw_lane);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-        a[0][kk] = wl[fwd_frag(1, 0, kk) * 64];
-        a[1][kk] = wl[fwd_frag(1, 1, kk) * 64];
-    }
-    if constexpr (SCHED) pp_pattern<10, 5>();
-    PP_FENCE();
-#pragma unroll
-    for (int l = 1; l <= 4; ++l) {
-        // layer l (A) | ReLU(B of layer l-1), an encoder slice of A
-        pp_mfma<4>(a, yA, cA);
-        pp_relu(cB, yB);
-        if (l == 1) enc_slice<1, FAST>(QA, h, wA);
-        if (l == 2) enc_slice<2, FAST>(QA, h, wA);
-        if (l == 3) enc_slice<3, FAST>(QA, h, wA);
-        if (l == 4) enc_slice<4, FAST>(QA, h, wA);
-        if constexpr (SCHED) pp_pattern<8, 6>();
-        PP_FENCE();
-        // layer l (B) | ReLU(A of layer l), an encoder slice of B; next layer's fragments
-        pp_mfma<4>(a, yB, cB);
-        pp_relu(cA, yA);
-        if (l == 1) enc_slice<1, FAST>(QB, h, wB);
-        if (l == 2) enc_slice<2, FAST>(QB, h, wB);
-        if (l == 3) enc_slice<3, FAST>(QB, h, wB);
-        if (l == 4) enc_slice<4, FAST>(QB, h, wB);
-        wl = launder(lw_lane);
-        if (l < 4) {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                a[0][kk] = wl[fwd_frag(l + 1, 0, kk) * 64];
-                a[1][kk] = wl[fwd_frag(l + 1, 1, kk) * 64];
-            }
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) a[0][kk] = wl[fwd_frag(5, 0, kk) * 64];
-        }
-        if constexpr (SCHED) pp_pattern<8, 6>();
-        PP_FENCE();
-    }
-    // output layer (A) | ReLU(B of layer 4), OneBlob 2 of B
-    oA = zero16();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) oA = mfma(a[0][kk], yA[kk], oA);
-    pp_relu(cB, yB);
-    enc_slice<5, FAST>(QB, h, wB);
-    if constexpr (SCHED) pp_pattern<4, 10>();
-    PP_FENCE();
-    oB = zero16();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) oB = mfma(a[0][kk], yB[kk], oB);
-    enc_words_to_frags(wA, nA);
-    enc_words_to_frags(wB, nB);
-    PP_FENCE();
-}
-
-// radiance of tile t (32 rows from s0) leaves through a raw buffer store whose descriptor covers its valid rows
-__device__ __forceinline__ void pp_store(float* __restrict__ out, int64_t n, int64_t s0, int r, int h, const f16v& o) {
-    const float L0 = (float)(_Float16)fmaxf(o[0], 0.0f);
-    const float L1 = (float)(_Float16)fmaxf(o[1], 0.0f);
-    const float L2 = (float)(_Float16)fmaxf(o[2], 0.0f);
-    const u3 ov = {__builtin_bit_cast(uint32_t, L0), __builtin_bit_cast(uint32_t, L1), __builtin_bit_cast(uint32_t, L2)};
-    __builtin_amdgcn_raw_buffer_store_b96(ov, buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12),
-                                          h == 0 ? r * 12 : kBufferOff, 0, 0);
-}
-
-template <int THREADS, int SCHED>
-__global__ __launch_bounds__(THREADS, 2) void infer_pp_kernel(const float* __restrict__ q, float* __restrict__ out,
-                                                              int64_t n, const h8* __restrict__ wf) {
-    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
-    fp32_flush_output_denorms();
-    copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, r = lane & 31;
-    const int64_t npairs = (((n + 31) >> 5) + 1) >> 1;
-    const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
-    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (g >= npairs) return;
-    const int64_t last = n - 1;
-    auto qrow = [&](int64_t pair, int t) { return min((pair * 2 + t) * 32 + r, last); };
-    lds_h8* lw_lane = (lds_h8*)(lw + lane);
-
-    // prologue: encode the first pair, prefetch the second
-    h8 xA[5], xB[5];
-    {
-        const QLane QA = load_q(q, qrow(g, 0), h), QB = load_q(q, qrow(g, 1), h);
-        encode_fast<true>(QA, h, xA);
-        encode_fast<true>(QB, h, xB);
-    }
-    QLane QA = load_q(q, qrow(g + wstride, 0), h), QB = load_q(q, qrow(g + wstride, 1), h);
-    __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);  // see variant 23
-    for (; g < npairs; g += wstride) {
-        const QLane NA = load_q(q, qrow(g + 2 * wstride, 0), h), NB = load_q(q, qrow(g + 2 * wstride, 1), h);
-        h8 nA[5], nB[5];
-        f16v oA, oB;
-        if (__all(blob_in_range(QA) && blob_in_range(QB)))
-            pp_iteration<true, SCHED>(lw_lane, xA, xB, QA, QB, h, nA, nB, oA, oB);
-        else {
-            asm volatile("; OneBlob wrap path");
-            pp_iteration<false, SCHED>(lw_lane, xA, xB, QA, QB, h, nA, nB, oA, oB);
-        }
-        pp_store(out, n, g * 64, r, h, oA);
-        pp_store(out, n, g * 64 + 32, r, h, oB);
-#pragma unroll
-        for (int kk = 0; kk < 5; ++kk) {
-            xA[kk] = nA[kk];
-            xB[kk] = nB[kk];
-        }
-        QA = NA;
-        QB = NB;
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
 static int num_cus() {
@@ -2981,63 +2508,21 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
     static int bpc[kNumInferVariants] = {};
-    const int64_t pairs = (ntiles + 1) / 2;
+    (void)wq;
     switch (variant) {
+        // The kernels kept for in-process A/B (tools/ab_infer.py). The rejected ones of rounds 1-2 (register-resident
+        // weights, explicit layer-ahead prefetch, ping-pong tiles, 2-tile waves, SIMD-staggered starts, launch-wide
+        // work queue, ablations) were measured, recorded in DESIGN.md §13 / profiles/r02_infer, and removed.
+        // 0: round-1 reference kernel (32-query tiles, one tile per wave iteration)
         case 0: return launch_persistent_infer(infer_kernel, kInferThreads, bpc[0], ntiles, queries, out, n, wf, s);
-        case 1: return launch_persistent_infer(infer_kernel_v2<1, 3, 256, false>, 256, bpc[1], ntiles, queries, out, n, wf, s);
-        case 2: return launch_persistent_infer(infer_kernel_v2<2, 2, 256, false>, 256, bpc[2], pairs, queries, out, n, wf, s);
-        case 3: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false>, 512, bpc[3], ntiles, queries, out, n, wf, s);
-        case 4: return launch_persistent_infer(infer_kernel_v2<1, 3, 256, true>, 256, bpc[4], ntiles, queries, out, n, wf, s);
-        case 5: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, true>, 512, bpc[5], ntiles, queries, out, n, wf, s);
-        case 6: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, true>, 512, bpc[6], pairs, queries, out, n, wf, s);
-        // ablations (timing only; outputs are wrong): no encode / no ReLU max / neither
-        case 7: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 1>, 512, bpc[7], ntiles, queries, out, n, wf, s);
-        case 8: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 2>, 512, bpc[8], ntiles, queries, out, n, wf, s);
-        case 9: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 3>, 512, bpc[9], ntiles, queries, out, n, wf, s);
-        case 14: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 4>, 512, bpc[14], ntiles, queries, out, n, wf, s);
-        case 15: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 7>, 512, bpc[15], ntiles, queries, out, n, wf, s);
-        case 16: return launch_persistent_infer(infer_kernel_v2<2, 2, 256, false, 7>, 256, bpc[16], pairs, queries, out, n, wf, s);
-        // v2 variant 3 with LDS-staged coalesced 16-B result stores
-        case 21: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 8>, 512, bpc[21], ntiles, queries, out, n, wf, s);
-        // v2 variant 3 with the omod doubling-chain triangle wave (f32 output denormals flushed)
-        case 22: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 16>, 512, bpc[22], ntiles, queries, out, n, wf, s);
-        // variant 22 + branch-free prefetch and buffer-store epilogue (exact vmcnt waits)
+        // 23: round-1 production (1 tile / 4 waves per SIMD, omod triangle chain, branch-free prefetch, buffer stores)
         case 23: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48>, 512, bpc[23], ntiles, queries, out, n, wf, s);
-        // variant 23 + staggered start of the waves sharing a SIMD (quarter-tile steps / odd slots half a tile)
-        case 24: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 64>, 512, bpc[24], ntiles, queries, out, n, wf, s);
-        case 25: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 128>, 512, bpc[25], ntiles, queries, out, n, wf, s);
-        // ping-pong: two tiles per wave half a layer apart, encoder slices spread over the phases
-        case 26: return launch_persistent_infer(infer_pp_kernel<512, 0>, 512, bpc[26], pairs, queries, out, n, wf, s);
-        case 27: return launch_persistent_infer(infer_pp_kernel<512, 1>, 512, bpc[27], pairs, queries, out, n, wf, s);
-        case 28: return launch_persistent_infer(infer_pp_kernel<256, 1>, 256, bpc[28], pairs, queries, out, n, wf, s);
-        // round 2: encoder v3 (tent-map triangle wave, clamped OneBlob wrap); 31/32: 23/30 with the clock stamps
+        // 30: 23 with encoder v3 (tent-map triangle wave, clamped OneBlob wrap)
         case 30: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 1024>, 512, bpc[30], ntiles, queries, out, n, wf, s);
-        case 31: return launch_clocked(infer_kernel_v2<1, 4, 512, false, 48 | 512>, 512, bpc[31], ntiles, queries, out, n, wf, s);
-        case 32: return launch_clocked(infer_kernel_v2<1, 4, 512, false, 48 | 1024 | 512>, 512, bpc[32], ntiles, queries, out, n, wf, s);
-        // 33/34: variant 30 with 1024-thread blocks (one per CU) drawing tiles from an LDS work queue; 34 clocked
-        case 33: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048>, 1024, bpc[33], ntiles, queries, out, n, wf, s);
-        case 34: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 512>, 1024, bpc[34], ntiles, queries, out, n, wf, s);
-        // 35/36: as 33/34 with 512-thread blocks (two per CU, each with its own queue)
-        case 35: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 1024 | 2048>, 512, bpc[35], ntiles, queries, out, n, wf, s);
-        case 36: return launch_clocked(infer_kernel_v2<1, 4, 512, false, 48 | 1024 | 2048 | 512>, 512, bpc[36], ntiles, queries, out, n, wf, s);
-        // 39/40: variant 33 + buffer-load query prefetch and packed output epilogue (ABL 8192); 40 clocked
+        // 39 (default): 30 with 1024-thread blocks (one per CU) drawing tiles from an LDS work queue, buffer-load query
+        // prefetch and the packed output epilogue; 40: 39 with the in-kernel clock (nrc_debug_read_infer_clock)
         case 39: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192>, 1024, bpc[39], ntiles, queries, out, n, wf, s);
         case 40: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 512>, 1024, bpc[40], ntiles, queries, out, n, wf, s);
-        // 37/38: variant 30 drawing tiles from the launch-wide work queue (the handle's counters); 38 clocked
-        case 37: if (!wq) return hipErrorInvalidValue;
-                 return launch_persistent_infer(infer_kernel_q<1, 4, 512, false, 48 | 1024 | 4096>, 512, bpc[37], ntiles, queries, out, n, wf, s, wq);
-        case 38: if (!wq) return hipErrorInvalidValue;
-                 return launch_clocked(infer_kernel_q<1, 4, 512, false, 48 | 1024 | 4096 | 512>, 512, bpc[38], ntiles, queries, out, n, wf, s, wq);
-        // v4: explicit layer-ahead weight prefetch
-        case 17: return launch_persistent_infer(infer_kernel_v4<1, 256, 2>, 256, bpc[17], ntiles, queries, out, n, wf, s);
-        case 18: return launch_persistent_infer(infer_kernel_v4<1, 256, 3>, 256, bpc[18], ntiles, queries, out, n, wf, s);
-        case 19: return launch_persistent_infer(infer_kernel_v4<2, 256, 2>, 256, bpc[19], pairs, queries, out, n, wf, s);
-        case 20: return launch_persistent_infer(infer_kernel_v4<2, 512, 2>, 512, bpc[20], pairs, queries, out, n, wf, s);
-        // v3: register-resident weights
-        case 10: return launch_persistent_infer(infer_kernel_v3<1, 46, 1>, 256, bpc[10], ntiles, queries, out, n, wf, s);
-        case 11: return launch_persistent_infer(infer_kernel_v3<2, 46, 1>, 256, bpc[11], pairs, queries, out, n, wf, s);
-        case 12: return launch_persistent_infer(infer_kernel_v3<1, 32, 2>, 256, bpc[12], ntiles, queries, out, n, wf, s);
-        case 13: return launch_persistent_infer(infer_kernel_v3<3, 46, 1>, 256, bpc[13], (ntiles + 2) / 3, queries, out, n, wf, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -3069,7 +2554,6 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
     switch (mode) {
         case -1: return launch_persistent_infer(infer_hash_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi, g);
         case 0: return launch_persistent_infer(infer_hash_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi, g);
-        case 2: return launch_persistent_infer(infer_hash_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi, g);
         default: return hipErrorInvalidValue;
     }
 }
@@ -3083,7 +2567,6 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
     switch (mode) {
         case -1: return launch_persistent_infer(infer_sh_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
         case 0: return launch_persistent_infer(infer_sh_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
-        case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
@@ -3203,7 +2686,6 @@ hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, 
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     switch (mode) {
         case 0: return launch_persistent_infer(infer_accumulate_kernel<0>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
-        case 2: return launch_persistent_infer(infer_accumulate_kernel<2>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }

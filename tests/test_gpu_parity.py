@@ -87,9 +87,9 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", list(range(7)) + [10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 26, 27, 28] + list(range(30, 41)))
+@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
-    """Per-query max error (not an aggregate) for every production-eligible kernel variant at sizes
+    """Per-query max error (not an aggregate) for every kernel variant kept for A/B at sizes
     that exercise partial tiles / single blocks."""
     net.set_state(nrc.StateSlot.INFER, golden["params_b"])
     L = nrc._lib.lib()

@@ -17,7 +17,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import nrc_loader  # noqa: E402
 
-CLOCKED = {31, 32, 34, 36, 38, 40}  # variants that record the in-kernel clock (nrc_debug_read_infer_clock)
+CLOCKED = {40}  # variants that record the in-kernel clock (nrc_debug_read_infer_clock)
 
 
 def main() -> None:
@@ -25,7 +25,7 @@ def main() -> None:
     ap.add_argument("--n", type=int, default=1 << 21)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="23,30,39")
     ap.add_argument("--weights", default="scaled", choices=["scaled", "bench"],
                     help="scaled: 1.6 x the init weights; bench: bench.py's state (xavier init + 4 frames of "
                          "self-training on its synthetic batches) and its query stream")
