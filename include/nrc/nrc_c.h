@@ -183,6 +183,10 @@ nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, ui
  * NRC_TRAIN_KERNEL=32; performs no optimizer step. */
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
                                   uint64_t* stamps_d);
+/* Diagnostic (InputEncoding::Hash): the inputs of the last training call's grid-gradient scatter, copied on the
+ * handle's stream into device buffers: pos_d [b][4] floats (position, 0), dy_d [16 levels][b] packed f16 pairs
+ * (dL/d feature 0, 1 of that level, loss-scaled). b <= the last call's sample count. */
+nrc_status nrc_debug_hash_scatter_inputs(nrc_net* net, float* pos_d, uint32_t* dy_d, uint32_t b);
 /* Diagnostic: the default inference kernel with s_memtime phase stamps; per wave of its persistent grid, 8 uint64
  * cycle sums (encode + prefetch, layers 0..4, output layer, epilogue) go to stamps_d, which must hold
  * 8 * NRC_INFER_STAMP_WAVES_MAX entries; *waves_h receives the number of waves written. */

@@ -38,7 +38,7 @@ EXPORTS = [
     "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
     "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp",
-    "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
+    "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_hash_scatter_inputs", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
     "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
@@ -122,6 +122,7 @@ def lib() -> ctypes.CDLL:
         "nrc_debug_infer_variant": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_read_infer_clock": (st, [vp, u32, ctypes.POINTER(u32)]),
         "nrc_debug_train_stamps": (st, [vp, fp, fp, u32, vp]),
+        "nrc_debug_hash_scatter_inputs": (st, [vp, vp, vp, u32]),
         "nrc_debug_infer_stamps": (st, [vp, fp, fp, u32, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "nrc_debug_encode_fast": (st, [fp, fp, u32, vp]),
         "nrc_debug_encode_fast_variant": (st, [ctypes.c_int, fp, fp, u32, vp]),

@@ -325,7 +325,7 @@ struct nrc_net {
     }
     // InputEncoding::Hash: grid part of the model arrays starts at n_mlp
     int n_mlp = NRC_NUM_PARAMS, n_grid = 0;
-    _Float16* grid_grad = nullptr;  // f16 [n_grid]: half2 per entry, packed-half atomics (tcnn)
+    int64_t* grid_grad = nullptr;  // [n_grid] exact fixed-point sums (x 2^24) of the f16 grid-gradient contributions
     uint32_t* grid_steps = nullptr;
     float2* grid_bias = nullptr;  // Adam bias-correction table of the grid parameters (GridBuffers::bias)
     _Float16 *table_train = nullptr, *table_infer = nullptr;
@@ -400,7 +400,7 @@ struct nrc_net {
     GridBuffers grid_buffers() const {
         GridBuffers g;
         g.params = params + n_mlp; g.m = m + n_mlp; g.v = v + n_mlp; g.ema = ema + n_mlp; g.infer = infer + n_mlp;
-        g.grad16 = grid_grad; g.grad32 = nullptr; g.steps = grid_steps;
+        g.grad64 = grid_grad; g.grad32 = nullptr; g.steps = grid_steps;
         g.table_train = table_train; g.table_infer = table_infer;
         g.bias = grid_bias; g.bias_len = grid_bias ? kGridBiasLen : 0;
         g.n = n_grid;
@@ -699,11 +699,11 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMalloc(&net->bwd_pos, sizeof(int) * net->n_mlp));
         if (net->hash()) {
             const size_t ng = (size_t)net->n_grid;
-            HIP_CHECK(hipMalloc(&net->grid_grad, sizeof(_Float16) * ng));
+            HIP_CHECK(hipMalloc(&net->grid_grad, sizeof(int64_t) * ng));
             HIP_CHECK(hipMalloc(&net->grid_steps, sizeof(uint32_t) * ng));
             HIP_CHECK(hipMalloc(&net->table_train, sizeof(_Float16) * ng));
             HIP_CHECK(hipMalloc(&net->table_infer, sizeof(_Float16) * ng));
-            HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(_Float16) * ng));
+            HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(int64_t) * ng));
             HIP_CHECK(hipMemset(net->grid_steps, 0, sizeof(uint32_t) * ng));
             std::vector<float2> bias(kGridBiasLen + 1, float2{0.0f, 0.0f});
             for (uint32_t st = 1; st <= kGridBiasLen; ++st)
@@ -1158,6 +1158,20 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tg
         const int blocks = train_blocks(b);
         net->ensure_slabs(blocks);
         train_partials(net, in, tgt, b, 3.0f * (float)b, stamps_d);
+    });
+}
+
+nrc_status nrc_debug_hash_scatter_inputs(nrc_net* net, float* pos_d, uint32_t* dy_d, uint32_t b) {
+    return guarded([&] {
+        check_live(net);
+        if (!net->hash()) throw ApiError(NRC_ERR_UNSUPPORTED, "nrc_debug_hash_scatter_inputs: InputEncoding::Hash only");
+        if (!pos_d || !dy_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
+        if (!net->scatter.pos || (int64_t)b > net->scatter.bcap)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "b exceeds the last training call's scatter buffers");
+        HIP_CHECK(hipMemcpyAsync(pos_d, net->scatter.pos, sizeof(float4) * b, hipMemcpyDeviceToDevice, net->stream));
+        for (int l = 0; l < NRC_HASH_LEVELS; ++l)
+            HIP_CHECK(hipMemcpyAsync(dy_d + (size_t)l * b, net->scatter.dy + (size_t)l * net->scatter.bcap,
+                                     sizeof(uint32_t) * b, hipMemcpyDeviceToDevice, net->stream));
     });
 }
 

@@ -244,7 +244,8 @@ void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias);
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
-    _Float16* grad16;     // f16 [n] (half2 per entry), accumulated by the training kernel, zeroed by grid_adam_kernel
+    int64_t* grad64;      // [n] exact fixed-point sums (value x 2^24) of the f16 contributions, accumulated by
+                          // grid_scatter_kernel, rounded to f16 and zeroed by grid_adam_kernel
     const float* grad32;  // kApplyOnly: the all-reduced data-parallel gradient (f32 [n], read-only)
     uint32_t* steps;  // per-entry Adam step counters
     _Float16 *table_train, *table_infer;
@@ -265,11 +266,11 @@ struct HashScatter {
     uint32_t* dy;  // [NRC_HASH_LEVELS][bcap]
     int64_t bcap;
 };
-hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t s);
+hipError_t launch_grid_grad_export(int64_t* g64, float* g32, int n, hipStream_t s);
 hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
                                 int64_t* waves, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
-                             const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
+                             const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,

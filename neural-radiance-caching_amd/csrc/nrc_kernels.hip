@@ -2728,6 +2728,26 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
 // and step counter; bias correction uses the entry's own step. The fused mode reads the f16 gradient the training
 // kernel accumulated and zeroes it for the next step; kApplyOnly reads a caller's (all-reduced) f32 gradient
 // without writing it.
+// An exact fixed-point sum (value x 2^24, grid_scatter_kernel) rounded once to f16, nearest-even; overflow -> inf.
+__device__ __forceinline__ _Float16 fixed_to_f16(int64_t v) {
+    const uint32_t sign = v < 0 ? 0x8000u : 0u;
+    const uint64_t a = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+    if (a < 1024u) return __builtin_bit_cast(_Float16, (uint16_t)(sign | (uint32_t)a));  // subnormal / zero: exact
+    const int msb = 63 - __builtin_clzll(a), shift = msb - 10;  // keep 11 significant bits
+    uint64_t mant = shift > 0 ? a >> shift : a;
+    if (shift > 0) {
+        const uint64_t rem = a & ((1ull << shift) - 1), half = 1ull << (shift - 1);
+        if (rem > half || (rem == half && (mant & 1u))) ++mant;
+    }
+    int be = shift + 1;  // biased exponent: value = mant / 1024 * 2^(shift - 14)
+    if (mant == 2048u) {
+        mant = 1024u;
+        ++be;
+    }
+    if (be >= 31) return __builtin_bit_cast(_Float16, (uint16_t)(sign | 0x7C00u));
+    return __builtin_bit_cast(_Float16, (uint16_t)(sign | ((uint32_t)be << 10) | (uint32_t)(mant - 1024u)));
+}
+
 __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -2740,8 +2760,8 @@ __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb
         if (mode == kApplyOnly) {
             gradient = gb.grad32[i] / oa.loss_scale;
         } else {
-            gradient = (float)gb.grad16[i] / oa.loss_scale;
-            gb.grad16[i] = (_Float16)0.0f;
+            gradient = (float)fixed_to_f16(gb.grad64[i]) / oa.loss_scale;
+            gb.grad64[i] = 0;
         }
         if (gradient != 0.0f) {
             const uint32_t st = gb.steps[i] + 1u;
@@ -2783,50 +2803,65 @@ hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa
     return hipGetLastError();
 }
 
-// Data-parallel export of the f16 grid gradient: f32 copy into the exchange buffer, source zeroed for the next step.
-__global__ __launch_bounds__(256) void grid_grad_export_kernel(_Float16* __restrict__ g16, float* __restrict__ g32,
+// Data-parallel export of the grid gradient: the f16-rounded exact sum as f32 into the exchange buffer, the fixed-point
+// accumulator zeroed for the next step.
+__global__ __launch_bounds__(256) void grid_grad_export_kernel(int64_t* __restrict__ g64, float* __restrict__ g32,
                                                                int n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    g32[i] = (float)g16[i];
-    g16[i] = (_Float16)0.0f;
+    g32[i] = (float)fixed_to_f16(g64[i]);
+    g64[i] = 0;
 }
 
-hipError_t launch_grid_grad_export(_Float16* g16, float* g32, int n, hipStream_t s) {
-    hipLaunchKernelGGL(grid_grad_export_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g16, g32, n);
+hipError_t launch_grid_grad_export(int64_t* g64, float* g32, int n, hipStream_t s) {
+    hipLaunchKernelGGL(grid_grad_export_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g64, g32, n);
     return hipGetLastError();
 }
 
-// Trilinear grid-gradient scatter (tcnn kernel_grid_backward). Block = (level, half of the level's table, slice of
-// the step's samples): it recomputes each sample's 8 corners at its level and adds w_corner * dy (each product
-// rounded to f16) into an f16 LDS copy of its half table with packed-half LDS atomics (ds_pk_add_f16: f16
-// accumulation, as tcnn's half2 atomicAdd; 64 KiB, two blocks per CU), then flushes the touched entries of the half
-// table with one packed-half global atomic each, issued in entry order. On MI355X device-scope float atomics
-// execute at the memory side and 64 lanes adding to 64 random rows run ~17x below the contiguous rate
-// (MI355X_MICROARCH.md § Global float atomics): the in-kernel version of this scatter (2 M random half2 atomics per
-// 16,384-sample step) dominated the step; here the random adds stay in the CU and the global ones walk the table in
-// order. The slice length is per level: the coarse levels cover the scene
-// with a handful of cells (position * 0.005 spans ~1.6 * 2^l cells per axis), so their LDS adds collide on a few
-// addresses and serialise -- a block's time grows with (slice samples / touched entries) -- while a fine level's
-// block costs mostly its half-table flush. So the slice doubles per level from `min` to `max`.
-constexpr int kScatterThreads = 1024, kScatterHalf = NRC_HASH_T / 2, kScatterPer = 2;
+// Trilinear grid-gradient scatter (tcnn kernel_grid_backward), deterministic. Block = (level, quarter of the level's
+// table, slice of the step's samples): it recomputes each sample's 8 corners at its level and adds w_corner * dy (each
+// product rounded to f16, as tcnn's half2 atomicAdd sees it) to an LDS copy of its quarter table as an exact
+// fixed-point integer (f16 value x 2^24: every f16 is an integer multiple of 2^-24, |value| < 2^16, so a step's sum
+// fits 64 bits), then flushes the touched entries with one 64-bit global integer atomic each, in entry order.
+// Integer addition is associative: the sums are exact and the same in every run whatever the order of the adds
+// (round 1 accumulated in f16 with packed-half atomics, which made Hash training order-dependent). grid_adam_kernel
+// rounds each exact sum to f16 once (fixed_to_f16) -- the oracle's f64 sum rounded to f16
+// (oracle/nrc_hash_oracle.c) -- and zeroes it.
+// On MI355X device-scope atomics execute at the memory side and 64 lanes adding to 64 random rows run ~17x below the
+// contiguous rate (MI355X_MICROARCH.md § Global float atomics): the random adds stay in the CU and the global ones
+// walk the table in order. The slice length is per level: the coarse levels cover the scene with a handful of cells
+// (position * 0.005 spans ~1.6 * 2^l cells per axis), so their LDS adds collide on a few addresses and serialise --
+// a block's time grows with (slice samples / touched entries) -- while a fine level's block costs mostly its
+// table flush. So the slice doubles per level from `min` to `max`.
+constexpr int kScatterThreads = 1024, kScatterPart = 8192, kScatterPer = 2;
 struct ScatterPlan {
     int first_block[NRC_HASH_LEVELS + 1];  // level l owns blocks [first_block[l], first_block[l + 1])
     int slice[NRC_HASH_LEVELS];            // samples per block at level l
 };
+constexpr int scatter_parts(int level) { return level == 0 ? 1 : NRC_HASH_T / kScatterPart; }
+
+// f16 value (bits) x 2^24 as an exact integer
+__device__ __forceinline__ int64_t f16_to_fixed(uint32_t h) {
+    const uint32_t e = (h >> 10) & 31u, m = h & 1023u;
+    const int64_t mag = e == 0 ? (int64_t)m : (int64_t)(m | 1024u) << (e - 1);
+    return (h & 0x8000u) ? -mag : mag;
+}
+
 __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const float4* __restrict__ pos,
                                                                        const uint32_t* __restrict__ dy, int64_t bcap,
-                                                                       ScatterPlan plan, h2v* __restrict__ grad) {
-    __shared__ h2v acc[kScatterHalf];  // 64 KiB: two blocks per CU
+                                                                       ScatterPlan plan,
+                                                                       unsigned long long* __restrict__ grad) {
+    __shared__ unsigned long long acc[kScatterPart][2];  // 128 KiB: one block per CU
     int level = 0;
 #pragma unroll
     for (int l = 1; l < NRC_HASH_LEVELS; ++l) level += (int)blockIdx.x >= plan.first_block[l];
     const int local = (int)blockIdx.x - plan.first_block[level];
-    const int half = level == 0 ? 0 : local & 1;  // level 0 (4,096 entries) has one half
-    const int64_t slice = plan.slice[level], s0 = (int64_t)(level == 0 ? local : local >> 1) * slice;
+    const int nparts = level == 0 ? 1 : NRC_HASH_T / kScatterPart;
+    const int part = local % nparts;
+    const int64_t slice = plan.slice[level], s0 = (int64_t)(local / nparts) * slice;
     const uint32_t lbase = NRC_HASH_LEVEL_ENTRY_OFFSET(level), lsize = level == 0 ? 4096u : (uint32_t)NRC_HASH_T;
-    const uint32_t e0 = (uint32_t)half * kScatterHalf;
-    const uint32_t ne = min((uint32_t)kScatterHalf, lsize - e0);
+    const uint32_t e0 = (uint32_t)part * kScatterPart;
+    const uint32_t ne = min((uint32_t)kScatterPart, lsize - e0);
     const uint32_t* dyl = dy + (int64_t)level * bcap;
     const int64_t s1 = min(bcap, s0 + slice);
     // the first batch's loads are issued before the table is zeroed (their latency hides behind it)
@@ -2842,7 +2877,7 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
         }
     };
     load();
-    for (uint32_t i = threadIdx.x; i < ne / 4; i += kScatterThreads) ((float4*)acc)[i] = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads) acc[i][0] = acc[i][1] = 0ull;
     __syncthreads();
     for (;;) {
 #pragma unroll
@@ -2856,9 +2891,12 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
 #pragma unroll
             for (int cc = 0; cc < 8; ++cc) {
                 const uint32_t e = C.entry[cc] - lbase - e0;
-                if (e < ne)
-                    __builtin_amdgcn_ds_atomic_fadd_v2f16((__attribute__((address_space(3))) h2v*)&acc[e],
-                                                          h2v{(_Float16)(C.w[cc] * dy0), (_Float16)(C.w[cc] * dy1)});
+                if (e < ne) {
+                    const h2v c = {(_Float16)(C.w[cc] * dy0), (_Float16)(C.w[cc] * dy1)};
+                    const uint32_t cb = __builtin_bit_cast(uint32_t, c);
+                    if (cb & 0x7FFFu) atomicAdd(&acc[e][0], (unsigned long long)f16_to_fixed(cb & 0xFFFFu));
+                    if (cb & 0x7FFF0000u) atomicAdd(&acc[e][1], (unsigned long long)f16_to_fixed(cb >> 16));
+                }
             }
         }
         s += (int64_t)kScatterPer * kScatterThreads;
@@ -2866,15 +2904,14 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
         load();
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads) {
-        const h2v v = acc[i];
-        if (__builtin_bit_cast(uint32_t, v) & 0x7FFF7FFFu)
-            __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v*)(grad + lbase + e0 + i), v);
+    for (uint32_t i = threadIdx.x; i < 2 * ne; i += kScatterThreads) {
+        const unsigned long long v = acc[i >> 1][i & 1];
+        if (v) __hip_atomic_fetch_add(grad + 2 * (uint64_t)(lbase + e0) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
-                             const _Float16* wf, const _Float16* wb, const _Float16* grid, _Float16* grid_grad,
+                             const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc) {
     if (b <= 0) return hipSuccess;
     const int blocks = train_blocks(b);
@@ -2882,7 +2919,7 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
     if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap) return hipErrorInvalidValue;
     hipLaunchKernelGGL((train_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
-                       reinterpret_cast<const uint32_t*>(grid), reinterpret_cast<h2v*>(grid_grad), sc->pos, sc->dy,
+                       reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
                        bcap);
     static const int smin_env = getenv("NRC_SCATTER_MIN") ? atoi(getenv("NRC_SCATTER_MIN")) : 0;
     static const int smax_env = getenv("NRC_SCATTER_MAX") ? atoi(getenv("NRC_SCATTER_MAX")) : 0;
@@ -2894,11 +2931,11 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
         const int sl = (int)std::min<int64_t>((int64_t)smax, (int64_t)smin << l);
         plan.first_block[l] = nb;
         plan.slice[l] = sl;
-        nb += (l == 0 ? 1 : 2) * (int)((bcap + sl - 1) / sl);
+        nb += scatter_parts(l) * (int)((bcap + sl - 1) / sl);
     }
     plan.first_block[NRC_HASH_LEVELS] = nb;
     hipLaunchKernelGGL(grid_scatter_kernel, dim3(nb), dim3(kScatterThreads), 0, s, sc->pos, sc->dy, bcap, plan,
-                       reinterpret_cast<h2v*>(grid_grad));
+                       reinterpret_cast<unsigned long long*>(grid_grad));
     return hipGetLastError();
 }
 

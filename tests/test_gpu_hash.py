@@ -5,8 +5,11 @@ Tolerances (stated here): encoder features within 1 f16 ulp; inf
 most 0.1 % of queries beyond 16 f16 ulps; one training step: loss rel <= 1e-3, MLP weights rel-L2 <= 3e-3 with
 >= 99 % of update signs equal,
 grid entries: the same set of entries updated (>= 99.5 %) with the same update sign (>= 99 %) — the first Adam
-step moves every touched entry by +-lr, so the sign is the whole update; the grid gradient is summed with half2
-atomics in an arbitrary order (as tcnn's), so training is not bitwise reproducible in this mode."""
+step moves every touched entry by +-lr, so the sign is the whole update (the network's dL/d feature differs from the
+oracle's by f16 rounding of a different evaluation order). The grid-gradient scatter itself is exact: from the GPU's
+own dL/d feature values, every entry's gradient is the f16 rounding of the exact sum of its f16 contributions
+(test_hash_grid_gradient_is_the_exact_sum), and Hash training is bitwise reproducible
+(test_hash_training_is_deterministic)."""
 import numpy as np
 import pytest
 
@@ -207,6 +210,71 @@ def test_hash_data_parallel_split_matches_fused_step(nrc, orc, dev):
         # whole batch, and an entry whose near-zero gradient flips sign moves by 2 lr — a handful of the ~1e5
         assert rel(ps[M:], pf[M:]) <= 5e-4
         assert split.step == fused.step == 1
+    finally:
+        for n in nets:
+            n.destroy()
+
+
+def _exact_grid_gradient(orc, pos, dy, b):
+    """CPU restatement of grid_scatter_kernel + fixed_to_f16: per sample and level, the 8 corners
+    (orc.hash_corners), each contribution f16(w * dy_f) (f32 product, RNE), summed exactly (integers of 2^-24),
+    the sum rounded once to f16 (nearest-even)."""
+    acc = np.zeros(orc.HASH_GRID_PARAMS, dtype=object)
+    dyh = dy.view(np.float16).reshape(16, b, 2).astype(np.float32)
+    for s in range(b):
+        q = np.zeros(15, np.float32)
+        q[:3] = pos[s, :3]
+        for lvl in range(16):
+            d0, d1 = dyh[lvl, s]
+            if d0 == 0.0 and d1 == 0.0:
+                continue
+            e, w = orc.hash_corners(q, lvl)
+            for c in range(8):
+                for f, dv in ((0, d0), (1, d1)):
+                    v = np.float16(np.float32(w[c]) * np.float32(dv))
+                    if v != 0:
+                        acc[2 * int(e[c]) + f] += int(round(float(v) * 2.0 ** 24))
+    out = np.array([np.float16(float(a) / 2.0 ** 24) if a else np.float16(0.0) for a in acc], np.float16)
+    return out.astype(np.float32)
+
+
+def test_hash_grid_gradient_is_the_exact_sum(nrc, orc, dev, hnet):
+    """The grid gradient a training call produces equals, bit for bit, the f16 rounding of the exact sum of the
+    f16 contributions w_corner * dy computed from the scatter's own inputs (positions, dL/d feature)."""
+    import torch
+    params = _trained_like(orc, seed=21)
+    hnet.set_state(nrc.StateSlot.PARAMS, params)
+    b = 384
+    q, t = nrc.synthetic.cornell_batch(b, seed=77)
+    g = torch.zeros(hnet.grad_floats, device=dev)
+    hnet.train_grad(_t(q, dev), _t(t, dev), b, b, g)
+    pos = torch.zeros((b, 4), dtype=torch.float32, device=dev)
+    dy = torch.zeros((16, b), dtype=torch.int32, device=dev)
+    L = nrc._lib.lib()
+    nrc._lib.check(L.nrc_debug_hash_scatter_inputs(hnet._h, pos.data_ptr(), dy.data_ptr(), b))
+    torch.cuda.synchronize()
+    gg = g.cpu().numpy()[orc.HASH_MLP_PARAMS:orc.HASH_NUM_PARAMS]
+    ref = _exact_grid_gradient(orc, pos.cpu().numpy(), dy.cpu().numpy().astype(np.uint32), b)
+    assert (ref != 0).sum() > 1000
+    np.testing.assert_array_equal(gg, ref)
+
+
+def test_hash_training_is_deterministic(nrc, orc, dev):
+    """Two handles stepped through the same minibatches end in bitwise-identical state (MLP and grid, Adam
+    moments, EMA, step counters): the grid gradient is an exact integer sum, the MLP gradient a fixed-order one."""
+    import torch
+    nets = []
+    for _ in range(2):
+        n = nrc.Network()
+        n.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+        nets.append(n)
+    try:
+        for it in range(3):
+            q, t = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=500 + it)
+            losses = [n.train(_t(q, dev), _t(t, dev), loss=True) for n in nets]
+            assert losses[0] == losses[1]
+        for slot in nrc.StateSlot:
+            np.testing.assert_array_equal(nets[0].get_state(slot), nets[1].get_state(slot))
     finally:
         for n in nets:
             n.destroy()
