@@ -2554,6 +2554,7 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
     switch (mode) {
         case -1: return launch_persistent_infer(infer_hash_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi, g);
         case 0: return launch_persistent_infer(infer_hash_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi, g);
+        case 2: return launch_persistent_infer(infer_hash_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi, g);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2567,6 +2568,7 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
     switch (mode) {
         case -1: return launch_persistent_infer(infer_sh_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
         case 0: return launch_persistent_infer(infer_sh_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2686,6 +2688,7 @@ hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, 
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     switch (mode) {
         case 0: return launch_persistent_infer(infer_accumulate_kernel<0>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_accumulate_kernel<2>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
