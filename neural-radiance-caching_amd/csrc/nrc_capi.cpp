@@ -295,6 +295,7 @@ struct nrc_net {
 
     float *params = nullptr, *m = nullptr, *v = nullptr, *ema = nullptr, *infer = nullptr;
     _Float16 *wf_train = nullptr, *wb_train = nullptr, *wf_infer = nullptr;
+    _Float16* wf_infer16 = nullptr;  // t16 nets: inference image in the t16 layout (nrc_infer16.hip)
     int *fwd_pos = nullptr, *bwd_pos = nullptr;
     int* fwdt_pos = nullptr;  // t16 training layout only (else the training image is laid out as fwd_pos)
     bool t16 = false;         // Frequency training on nrc_train16.hip
@@ -351,7 +352,7 @@ struct nrc_net {
             if (p) (void)hipFree(p);
         };
         f(params); f(m); f(v); f(ema); f(infer);
-        f(wf_train); f(wb_train); f(wf_infer);
+        f(wf_train); f(wb_train); f(wf_infer); f(wf_infer16);
         f(fwd_pos); f(bwd_pos); f(fwdt_pos); f(slab_param);
         f(slabs); f(loss_partials);  // loss_dev aliases loss_host (freed below)
         f(work_queue);
@@ -375,7 +376,7 @@ struct nrc_net {
         table_train = table_infer = nullptr;
         if (loss_host) (void)hipHostFree(loss_host);
         params = m = v = ema = infer = nullptr;
-        wf_train = wb_train = wf_infer = nullptr;
+        wf_train = wb_train = wf_infer = wf_infer16 = nullptr;
         fwd_pos = bwd_pos = fwdt_pos = nullptr;
         t16 = false;
         slab_param = nullptr;
@@ -387,7 +388,7 @@ struct nrc_net {
     ModelBuffers buffers() const {
         ModelBuffers b;
         b.params = params; b.m = m; b.v = v; b.ema = ema; b.infer = infer;
-        b.wf_train = wf_train; b.wb_train = wb_train; b.wf_infer = wf_infer;
+        b.wf_train = wf_train; b.wb_train = wb_train; b.wf_infer = wf_infer; b.wf_infer16 = wf_infer16;
         b.fwd_pos = fwd_pos; b.bwd_pos = bwd_pos;
         b.fwdt_pos = fwdt_pos ? fwdt_pos : fwd_pos;
         b.slab_f16 = t16;
@@ -726,6 +727,14 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             build_t16_maps(fwdt, bwd);
             HIP_CHECK(hipMalloc(&net->fwdt_pos, sizeof(int) * net->n_mlp));
             HIP_CHECK(hipMemcpy(net->fwdt_pos, fwdt.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
+            // A/B only (debug variants 50/51, nrc_infer16.hip, rejected in round 2: DESIGN.md §8): the t16-layout
+            // inference image, packed by the optimizer only when NRC_DEBUG_INFER16 is set
+            static_assert(kT16FwdFrags * kFragHalves == kFwdHalves, "t16 forward image size");
+            const char* e = std::getenv("NRC_DEBUG_INFER16");
+            if (e && *e && *e != '0') {
+                HIP_CHECK(hipMalloc(&net->wf_infer16, sizeof(_Float16) * kFwdHalves));
+                HIP_CHECK(hipMemset(net->wf_infer16, 0, sizeof(_Float16) * kFwdHalves));  // dummy slots stay 0
+            }
         }
         HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
@@ -1121,6 +1130,11 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
         if (variant < 0 || variant >= kNumInferVariants) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown variant");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+        if (variant == 50 || variant == 51) {  // 51 (debug): the t16 training image (master weights)
+            if (!net->wf_infer16) throw ApiError(NRC_ERR_UNSUPPORTED, "variants 50/51 need NRC_DEBUG_INFER16=1 at init (t16 inference image)");
+            HIP_CHECK(launch_infer16(in, out, n, variant == 50 ? net->wf_infer16 : net->wf_train, stream));
+            return;
+        }
         HIP_CHECK(launch_infer_variant(variant, in, out, n, net->wf_infer, stream, net->work_queue));
     });
 }

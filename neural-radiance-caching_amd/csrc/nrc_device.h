@@ -194,6 +194,7 @@ __device__ __forceinline__ void adam_pack_pre(int p, float gsum, const AdamIn& i
     mb.infer[p] = inf;
     mb.wf_train[in.ft] = (_Float16)w;
     mb.wf_infer[in.fp] = (_Float16)inf;
+    if (mb.wf_infer16) mb.wf_infer16[in.ft] = (_Float16)inf;
     if (in.bp >= 0) mb.wb_train[in.bp] = (_Float16)w;
 }
 

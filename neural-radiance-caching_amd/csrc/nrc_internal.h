@@ -178,7 +178,9 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
 // queue variants were removed
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s, uint32_t* wq = nullptr);
-constexpr int kNumInferVariants = 41;
+constexpr int kNumInferVariants = 52;  // 50: launch_infer16 (the t16 image)
+// Frequency inference on v_mfma_f32_16x16x32_f16 (nrc_infer16.hip) from the t16-layout inference image
+hipError_t launch_infer16(const float* queries, float* out, int64_t n, const _Float16* wf16, hipStream_t s);
 // per-wave (cycles, 100 MHz ticks) of the last clocked variant launch (31, 32)
 hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves);
 // inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
@@ -226,6 +228,7 @@ static_assert(slab_floats(0) == 23552 && slab_floats(1) == NRC_HASH_MLP_PARAMS, 
 struct ModelBuffers {
     float *params, *m, *v, *ema, *infer;  // f32 master / Adam / EMA / debiased EMA (inference)
     _Float16 *wf_train, *wb_train, *wf_infer;
+    _Float16* wf_infer16;  // t16 nets: the inference image in the t16 layout (at fwdt_pos), else null
     const int *fwd_pos, *bwd_pos;
     const int* fwdt_pos;  // position in wf_train (the t16 layout for Frequency; fwd_pos otherwise)
     bool slab_f16;        // slabs hold f16 partials (t16)

@@ -2034,6 +2034,7 @@ __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const
     }
     mb.wf_train[mb.fwdt_pos[p]] = (_Float16)w;
     mb.wf_infer[mb.fwd_pos[p]] = (_Float16)inf;
+    if (mb.wf_infer16) mb.wf_infer16[mb.fwdt_pos[p]] = (_Float16)inf;
     const int bp = mb.bwd_pos[p];
     if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
 }

@@ -17,15 +17,18 @@
 //   LDS), the next layer's images written to the other buffer, the dW tiles streamed to the block's slab.
 #include <cstdlib>
 
-#include "nrc_device.h"
+#include "nrc_t16.h"
 
 namespace nrc_amd {
 namespace {
 
-typedef float f4 __attribute__((ext_vector_type(4)));
+using t16::f4;
+using t16::mfma16;
+using t16::relu_pk;
+using t16::relu_b;
+using t16::encode16;
 typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
 }
@@ -65,30 +68,17 @@ __device__ __forceinline__ h8 tr_pair(const char* p0, const char* p1) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// f16 ReLU of a packed pair as an integer max: negative halves (sign bit set, -0 included) become +0, so an
-// activation is +0 or has positive bits, and RNE conversion commuting with ReLU makes this f16(max(x, 0)).
-__device__ __forceinline__ uint32_t relu_pk(uint32_t x) {
-    uint32_t r;
-    asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
-    return r;
-}
 // backward ReLU gate on packed halves: d where the activation m > 0, else +0. m is +0 or positive bits (relu_pk),
-// so min_u16(m, 1) is the 0/1 mask and an integer multiply selects (2 VALU per dword).
+// so min_u16(m, 1) is the 0/1 mask and an integer multiply selects (2 VALU per dword). The min is inline asm (the
+// compiler turns a visible min-and-multiply into compares and selects); the multiply, whose result MFMAs read, is
+// compiler-visible so that the hazard recognizer sees it (nrc_t16.h).
+typedef unsigned short u2h __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t gate_pk(uint32_t d, uint32_t m) {
-    uint32_t r;
-    asm("v_pk_min_u16 %0, %1, %3\n\t"
-        "v_pk_mul_lo_u16 %0, %0, %2"
-        : "=&v"(r)
-        : "v"(m), "v"(d), "s"(0x00010001u));
-    return r;
+    uint32_t mask;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(mask) : "v"(m), "s"(0x00010001u));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2h, mask) * __builtin_bit_cast(u2h, d));
 }
 
-// accumulators of M-blocks 2s, 2s + 1 -> B operand of k-step s (rows t16_row(s, g, j)), ReLU applied
-__device__ __forceinline__ h8 relu_b(const f4& lo, const f4& hi) {
-    const u4 w = {relu_pk(pk2(lo[0], lo[1])), relu_pk(pk2(lo[2], lo[3])), relu_pk(pk2(hi[0], hi[1])),
-                  relu_pk(pk2(hi[2], hi[3]))};
-    return __builtin_bit_cast(h8, w);
-}
 // the same rows as a delta, gated by the forward activation (B-operand form, same rows)
 __device__ __forceinline__ h8 gate_b(const f4& lo, const f4& hi, const h8& a) {
     const u4 m = __builtin_bit_cast(u4, a);
@@ -110,37 +100,6 @@ __device__ __forceinline__ void put_rows64(char* img, const int (&wo)[4], const 
 __device__ __forceinline__ void row_offsets(int r, int g, int (&wo)[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) wo[k] = off64(r, 8 * (k >> 1) + 4 * (k & 1) + g);
-}
-
-// Encoded input of sample c in lane group g: 24 K slots (t16_slot_feature) as three B-operand k-steps.
-// TriangleWave by the tent map (as encode_v3, octaves 3g .. 3g + 2 of each position dim), OneBlob in closed form
-// with the clamped wrap (blob_v3), Identity, padding 1.0.
-__device__ __forceinline__ void encode16(float p0, float p1, float p2, float bA, float bB, float iA, float iB, int g,
-                                         h8 (&x)[3]) {
-    const float sc = (float)(1 << (3 * g));
-    float t[9];
-    const float p[3] = {p0, p1, p2};
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        float v = fmaf(__builtin_amdgcn_fractf(__builtin_fabsf(p[d]) * sc), 2.0f, -1.0f);
-        t[3 * d] = v;
-        v = tent_step(v);
-        t[3 * d + 1] = v;
-        v = tent_step(v);
-        t[3 * d + 2] = v;
-    }
-    uint32_t w[12];
-    w[0] = pk2_abs(t[0], t[1]);
-    w[1] = pk2_abs(t[2], t[3]);
-    w[2] = pk2_abs(t[4], t[5]);
-    w[3] = pk2_abs(t[6], t[7]);
-    w[4] = pk2(__builtin_fabsf(t[8]), iA);
-    w[5] = pk2(iB, 1.0f);
-    blob_v3(bA, w[6], w[7]);
-    blob_v3(bB, w[8], w[9]);
-    w[10] = w[11] = 0x3C003C00u;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) x[s] = __builtin_bit_cast(h8, u4{w[4 * s], w[4 * s + 1], w[4 * s + 2], w[4 * s + 3]});
 }
 
 // dW tiles into the block's slab as f16 (t16_slab_pos: column pairs, one 16-byte store per lane for both tiles of a

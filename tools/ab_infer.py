@@ -17,7 +17,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import nrc_loader  # noqa: E402
 
-CLOCKED = {40}  # variants that record the in-kernel clock (nrc_debug_read_infer_clock)
+CLOCKED = {40}
+# 50: the rejected 16x16x32 inference kernel (nrc_infer16.hip)  # variants that record the in-kernel clock (nrc_debug_read_infer_clock)
 
 
 def main() -> None:
@@ -39,6 +40,9 @@ def main() -> None:
     stream = torch.cuda.current_stream()
     sp = int(stream.cuda_stream)
     variants = [int(v) for v in args.variants.split(",")]
+    if 50 in variants or 51 in variants:  # the 16x16x32 kernel reads the t16 inference image (debug only)
+        import os
+        os.environ["NRC_DEBUG_INFER16"] = "1"
 
     net = nrc.Network()
     net.init(stream=stream)
