@@ -299,6 +299,7 @@ struct nrc_net {
     int *fwd_pos = nullptr, *bwd_pos = nullptr;
     int* fwdt_pos = nullptr;  // t16 training layout only (else the training image is laid out as fwd_pos)
     bool t16 = false;         // Frequency training on nrc_train16.hip
+    bool t16_split = false;   // the role-split t16 kernel (default; NRC_T16_SPLIT=0 at init: the 4-wave one)
     int* slab_param = nullptr;  // [n_slab] parameter of each weight-gradient slab position
     int n_slab = 0;
     float* slabs = nullptr;
@@ -494,7 +495,8 @@ void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b,
                     uint64_t* stamps = nullptr) {
     if (net->t16)
         HIP_CHECK(launch_train16(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                 reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream));
+                                 reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream,
+                                 net->t16_split));
     else if (stamps)
         HIP_CHECK(launch_train_stamped(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                        net->slabs, net->loss_partials, stamps, net->stream));
@@ -722,6 +724,12 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         std::vector<int> fwd, bwd;
         build_scatter_maps(fwd, bwd, net->encoding);
         net->t16 = want_t16(net->encoding);
+        {
+            // the role-split kernel is the default (in-process A/B: step 14.1 vs 14.8 us, bitwise-identical
+            // gradient, profiles/r02_train/); NRC_T16_SPLIT=0 selects the 4-wave kernel
+            const char* e = std::getenv("NRC_T16_SPLIT");
+            net->t16_split = net->t16 && !(e && *e == '0');
+        }
         if (net->t16) {
             std::vector<int> fwdt;
             build_t16_maps(fwdt, bwd);

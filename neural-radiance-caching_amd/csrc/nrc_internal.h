@@ -241,7 +241,7 @@ struct ModelBuffers {
 // slabs: f16 (nrc_train16.hip slab_pair), reduced by launch_reduce_adam (ModelBuffers::slab_f16)
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s);
+                          hipStream_t s, bool split = false);  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // host-f32 Adam step-size and EMA debias of optimizer step oa.step (tcnn adam.h; identical to the oracle's)
 void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias);
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state

@@ -573,13 +573,312 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
     stamp();
 }
 
+// Role-split variant (NRC_T16_SPLIT, A/B): 8 waves per block, 2 per SIMD. Waves 0..3 ("chain") do what
+// train16_kernel's waves do except the weight gradients: encode, forward, loss, then per backward step the delta chain
+// (W_L^T delta_L, ReLU gate) and the image writes. Waves 4..7 ("dW") sit through the forward at its barriers and then,
+// in each backward step, compute the block's dW_L tiles from the images the chain waves wrote in the step before and
+// stream them to the slab. The two halves of a step share the SIMDs' MFMA pipes and hide each other's LDS and
+// dependency latency; the step's critical path is the chain alone instead of chain + dW.
+__global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
+                                                               int64_t b, float n_total, float loss_scale,
+                                                               const h8* __restrict__ wf, const h8* __restrict__ wb,
+                                                               _Float16* __restrict__ slabs,
+                                                               float* __restrict__ loss_partials) {
+    const int lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) char smem[kLds];
+    h8* lwb = (h8*)(smem + kOffWb);
+    h8* lwf = (h8*)(smem + kOffWf);
+    char* const img_a0 = smem + kOffImg;
+    char* const img_a1 = smem + kOffImg + kImg;
+    char* const img_d0 = smem + kOffImg + 2 * kImg;
+    char* const img_d1 = smem + kOffImg + 3 * kImg;
+    char* const img_x2 = smem + kOffX2;
+    float* red = (float*)(smem + kOffRed);
+    const int wave_all = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool dw_wave = wave_all >= kWaves;
+    const int wave = dw_wave ? wave_all - kWaves : wave_all;
+    const int g = lane >> 4, c = lane & 15;
+    _Float16* slab = slabs + (int64_t)blockIdx.x * slab_floats(0);
+
+    if (dw_wave) {
+        // ---- dW waves: the forward's six barriers, then one dW step per backward step
+        for (int i = 0; i < 6; ++i) lds_barrier();
+        const int G = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+        const int r0 = 8 * G + qq, r1 = r0 + 4;
+        const int tm0 = 2 * (wave >> 1), tn0 = 2 * (wave & 1);
+        int oa[2][2], ob[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            oa[i][0] = off64(r0, 4 * (tm0 + i) + pp);
+            oa[i][1] = off64(r1, 4 * (tm0 + i) + pp);
+            ob[i][0] = off64(r0, 4 * (tn0 + i) + pp);
+            ob[i][1] = off64(r1, 4 * (tn0 + i) + pp);
+        }
+        // step 5 (buffer 1): dW5 tile (0, wave)
+        {
+            f4 acc[1][1];
+            const TrTile ta[1] = {TrTile{img_d1, off64(r0, pp), off64(r1, pp), 4096}};
+            const TrTile tb[1] = {TrTile{img_a1, off64(r0, 4 * wave + pp), off64(r1, 4 * wave + pp), 4096}};
+            dw_tiles<1, 1>(ta, tb, acc);
+            slab_single(slab, 5, 0, wave, lane, acc[0][0]);
+        }
+        lds_barrier();
+        // steps 4..1: dW_L tiles (tm0 + i, tn0 + j) from buffer L & 1
+#pragma unroll
+        for (int L = 4; L >= 1; --L) {
+            const char* imgd = (L & 1) ? img_d1 : img_d0;
+            const char* imga = (L & 1) ? img_a1 : img_a0;
+            TrTile ta[2], tb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ta[i] = TrTile{imgd, oa[i][0], oa[i][1], 4096};
+                tb[i] = TrTile{imga, ob[i][0], ob[i][1], 4096};
+            }
+            f4 acc[2][2];
+            dw_tiles<2, 2>(ta, tb, acc);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) slab_pair(slab, L, tm0 + i, tn0, lane, pack_pair(acc[i][0], acc[i][1]));
+            lds_barrier();
+        }
+        // step 0 (buffer 0): dW0 tiles (tm0 + i, 3 (wave & 1) + j); columns 4, 5 are K slots 64..95 (img_x2)
+        {
+            f4 acc[2][3];
+            const TrTile ta[2] = {TrTile{img_d0, oa[0][0], oa[0][1], 4096}, TrTile{img_d0, oa[1][0], oa[1][1], 4096}};
+            if ((wave & 1) == 0) {
+                const TrTile tb[3] = {TrTile{img_a0, off64(r0, pp), off64(r1, pp), 4096},
+                                      TrTile{img_a0, off64(r0, 4 + pp), off64(r1, 4 + pp), 4096},
+                                      TrTile{img_a0, off64(r0, 8 + pp), off64(r1, 8 + pp), 4096}};
+                dw_tiles<2, 3>(ta, tb, acc);
+            } else {
+                const TrTile tb[3] = {TrTile{img_a0, off64(r0, 12 + pp), off64(r1, 12 + pp), 4096},
+                                      TrTile{img_x2, off32(r0, pp), off32(r1, pp), 2048},
+                                      TrTile{img_x2, off32(r0, 4 + pp), off32(r1, 4 + pp), 2048}};
+                dw_tiles<2, 3>(ta, tb, acc);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if ((wave & 1) == 0) {
+                    slab_pair(slab, 0, tm0 + i, 0, lane, pack_pair(acc[i][0], acc[i][1]));
+                    slab_single(slab, 0, tm0 + i, 2, lane, acc[i][2]);
+                } else {
+                    slab_single(slab, 0, tm0 + i, 3, lane, acc[i][0]);
+                    slab_pair(slab, 0, tm0 + i, 4, lane, pack_pair(acc[i][1], acc[i][2]));
+                }
+            }
+        }
+        return;
+    }
+
+    // ---- chain waves: as train16_kernel
+    int r[2];
+    bool valid[2];
+    typedef float f3 __attribute__((ext_vector_type(3)));
+    f3 pq[2], tq[2];
+    f2 bl[2], id[2];
+    const int gg = g < 3 ? g : 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        r[u] = 32 * wave + 16 * u + c;
+        const int64_t s = (int64_t)blockIdx.x * kTrainSamplesPerBlock + r[u];
+        valid[u] = s < b;
+        const int64_t sc = valid[u] ? s : b - 1;
+        const float* qr = q + sc * NRC_INPUT_DIMS;
+        asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(pq[u]) : "v"(qr) : "memory");
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(bl[u]) : "v"(qr + 3 + 2 * gg) : "memory");
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(id[u]) : "v"(qr + 9 + 2 * gg) : "memory");
+        asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(tq[u]) : "v"(t + sc * 3) : "memory");
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const int f = wave + kWaves * k;
+        __builtin_amdgcn_global_load_lds((const void*)(wf + (f < kT16FwdFrags ? f : kT16FwdFrags - 1) * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(lwf + f * 64), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(12)"
+                 : "+v"(pq[0]), "+v"(pq[1]), "+v"(bl[0]), "+v"(bl[1]), "+v"(id[0]), "+v"(id[1]), "+v"(tq[0]), "+v"(tq[1])
+                 :
+                 : "memory");
+    h8 x[2][3];
+    float tg[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        tg[u][0] = tq[u].x; tg[u][1] = tq[u].y; tg[u][2] = tq[u].z;
+        encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u]);
+        const u4 w = __builtin_bit_cast(u4, x[u][2]);
+        *(u2*)(img_x2 + off32(r[u], 2 * g)) = u2{w.x, w.y};
+        *(u2*)(img_x2 + off32(r[u], 2 * g + 1)) = u2{w.z, w.w};
+    }
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    lds_barrier();  // barrier 1
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const int f = wave + kWaves * k;
+        __builtin_amdgcn_global_load_lds((const void*)(wb + f * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(lwb + f * 64), 16, 0, 0);
+    }
+    h8 a[5][2][2];
+    f4 o[2];
+    {
+        h8 w0[12], w1[8];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks) w0[mb * 3 + ks] = lwf[t16_fwd_frag(0, mb, ks) * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w1[i] = lwf[t16_fwd_frag(1, i >> 1, i & 1) * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
+        f4 cc[2][4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            cc[0][mb] = cc[1][mb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks) {
+                cc[0][mb] = mfma16(w0[mb * 3 + ks], x[0][ks], cc[0][mb]);
+                cc[1][mb] = mfma16(w0[mb * 3 + ks], x[1][ks], cc[1][mb]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            a[0][u][0] = relu_b(cc[u][0], cc[u][1]);
+            a[0][u][1] = relu_b(cc[u][2], cc[u][3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int l = 1; l < 6; ++l) {
+            h8 wn[8];
+            if (l < 5) {
+                if (l == 1) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+                if (l == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                if (l == 3) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+                if (l == 4) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+                lds_barrier();  // barriers 2..5
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (l + 1 < 5 || i < 2) wn[i] = lwf[t16_fwd_frag(l + 1, l + 1 < 5 ? i >> 1 : 0, i & 1) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (l < 5) {
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb) {
+                    cc[0][mb] = cc[1][mb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks) {
+                        cc[0][mb] = mfma16(w1[mb * 2 + ks], a[l - 1][0][ks], cc[0][mb]);
+                        cc[1][mb] = mfma16(w1[mb * 2 + ks], a[l - 1][1][ks], cc[1][mb]);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    a[l][u][0] = relu_b(cc[u][0], cc[u][1]);
+                    a[l][u][1] = relu_b(cc[u][2], cc[u][3]);
+                }
+            } else {
+                o[0] = o[1] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    o[0] = mfma16(w1[ks], a[4][0][ks], o[0]);
+                    o[1] = mfma16(w1[ks], a[4][1][ks], o[1]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w1[i] = wn[i];
+        }
+    }
+    float lossv = 0.0f;
+    h4 d5[2] = {h4{}, h4{}};
+    if (g == 0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float y[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) y[k] = (float)(_Float16)fmaxf(o[u][k], 0.0f);
+            const float lum = 0.299f * y[0] + 0.587f * y[1] + 0.114f * y[2];
+            const float inv = 1.0f / ((lum * lum + NRC_LUM_EPS) * n_total);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float diff = y[k] - tg[u][k];
+                lossv += valid[u] ? diff * diff * inv : 0.0f;
+                d5[u][k] = (valid[u] && y[k] > 0.0f) ? (_Float16)(loss_scale * 2.0f * diff * inv) : (_Float16)0.0f;
+            }
+        }
+    }
+    lossv = row_sum16(lossv);
+    if (lane == 0) red[wave] = lossv;
+    int wo[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        row_offsets(r[u], g, wo[u]);
+        asm volatile("" : "+v"(wo[u][0]), "+v"(wo[u][1]), "+v"(wo[u][2]), "+v"(wo[u][3]));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        *(h4*)(img_d1 + off64(r[u], g)) = d5[u];
+        put_rows64(img_a1, wo[u], a[4][u]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // backward image landed
+    lds_barrier();  // barrier 6
+    if (threadIdx.x == 0) {
+        const float lp = (red[0] + red[1]) + (red[2] + red[3]);
+        loss_partials[blockIdx.x] = lp;
+    }
+
+    h8 d[2][2], dn[2][2], W[4][2];
+    // step 5: delta_4 = W5^T delta_5 * [a_4 > 0] (16x16x16: K = 16 output rows) into buffer 0 with a_3
+    {
+        const h4* lwb4 = (const h4*)lwb;
+        h4 W5[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) W5[mb] = lwb4[t16_bwd_frag(5, mb, 0) * 128 + lane];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f4 cc[4];
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) cc[mb] = mfma16k16(W5[mb], d5[u], f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) d[u][s2] = gate_b(cc[2 * s2], cc[2 * s2 + 1], a[4][u][s2]);
+            put_rows64(img_d0, wo[u], d[u]);
+            put_rows64(img_a0, wo[u], a[3][u]);
+        }
+        load_wt<4>(lwb, lane, W);
+    }
+    lds_barrier();
+    // steps 4..1: delta_{L-1} into the other buffer with a_{L-2} (step 1: the input slots 0..63)
+#define NRC_T16S_STEP(L, NIMGD, NIMGA)                                                                              \
+    {                                                                                                              \
+        _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
+            if constexpr (L > 1) {                                                                                 \
+                put_rows64(NIMGA, wo[u], a[L > 1 ? L - 2 : 0][u]);                                                 \
+            } else {                                                                                               \
+                _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                                 \
+                    const u4 w = __builtin_bit_cast(u4, x[u][ks]);                                                 \
+                    *(u2*)(NIMGA + off64(r[u], 8 * ks + 2 * g)) = u2{w.x, w.y};                                    \
+                    *(u2*)(NIMGA + off64(r[u], 8 * ks + 2 * g + 1)) = u2{w.z, w.w};                                \
+                }                                                                                                  \
+            }                                                                                                      \
+        }                                                                                                          \
+        chain2(W, d, a[L - 1], dn);                                                                                \
+        if constexpr (L > 1) load_wt<(L > 1 ? L - 1 : 1)>(lwb, lane, W);                                           \
+        _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
+            put_rows64(NIMGD, wo[u], dn[u]);                                                                       \
+            _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) d[u][s2] = dn[u][s2];                                 \
+        }                                                                                                          \
+    }                                                                                                              \
+    lds_barrier();
+    NRC_T16S_STEP(4, img_d1, img_a1)
+    NRC_T16S_STEP(3, img_d0, img_a0)
+    NRC_T16S_STEP(2, img_d1, img_a1)
+    NRC_T16S_STEP(1, img_d0, img_a0)
+#undef NRC_T16S_STEP
+}
+
 int t16_blocks(int64_t b) { return (int)((b + kTrainSamplesPerBlock - 1) / kTrainSamplesPerBlock); }
 
 }  // namespace
 
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s) {
+                          hipStream_t s, bool split) {
     if (b <= 0) return hipSuccess;
     static const int abl = [] {
         const char* e = std::getenv("NRC_T16_ABL");
@@ -587,6 +886,11 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
     }();
     const dim3 grid(t16_blocks(b)), block(64 * kWaves);
     const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
+    if (split && !stamps) {
+        hipLaunchKernelGGL(train16_split_kernel, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total, loss_scale,
+                           f, bw, slabs, loss_partials);
+        return hipGetLastError();
+    }
     if (stamps) {
         switch (abl) {
             case 1: hipLaunchKernelGGL((train16_kernel<true, 1>), grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, stamps); break;

@@ -30,15 +30,18 @@ def main():
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     nets = {}
-    for name, env in (("t16", None), ("k32", "32")):
+    # t16: the default; t16s: the role-split t16 kernel (NRC_T16_SPLIT=1); k32: the round-1 kernel
+    for name, env, split in (("t16", None, "0"), ("t16s", None, "1"), ("k32", "32", "0")):
         if env:
             os.environ["NRC_TRAIN_KERNEL"] = env
         else:
             os.environ.pop("NRC_TRAIN_KERNEL", None)
+        os.environ["NRC_T16_SPLIT"] = split
         n = nrc.Network()
         n.init(stream=st)
         nets[name] = n
     os.environ.pop("NRC_TRAIN_KERNEL", None)
+    os.environ.pop("NRC_T16_SPLIT", None)
     B = nrc.BATCH_SIZE
     q_np, t_np = nrc.synthetic.cornell_batch(B, seed=3)
     q, t = torch.from_numpy(q_np).to(dev), torch.from_numpy(t_np).to(dev)
@@ -56,6 +59,7 @@ def main():
     check = {k: {"grad_rel_l2_vs_oracle": rel(gk[k][:P], g_ref),
                  "loss": float(gk[k][P]), "loss_oracle": float(loss_ref)} for k in nets}
     check["t16_vs_k32_rel_l2"] = rel(gk["t16"][:P], gk["k32"][:P])
+    check["t16s_vs_t16_max_abs"] = float(np.abs(gk["t16s"] - gk["t16"]).max())
 
     def timeit(fn, iters):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
