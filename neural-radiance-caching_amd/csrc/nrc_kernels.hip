@@ -1059,12 +1059,13 @@ __global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __rest
     infer_v2_body<1, 512, false, kDefaultAbl | 256, -1>(q, out, n, wf, e);
 }
 
-// the default inference configuration (variant 22) with the accumulation epilogue
-template <int EPI>
-__global__ __launch_bounds__(512, 4) void infer_accumulate_kernel(const float* __restrict__ q, float* __restrict__ out,
-                                                                  int64_t n, const h8* __restrict__ wf,
-                                                                  InferEpilogue epi) {
-    infer_v2_body<1, 512, false, kDefaultAbl | 1024 | 8192, EPI>(q, out, n, wf, epi);  // encoder v3, buffer-load prefetch
+// the default inference configuration with the accumulation epilogue: THREADS 1024 + XABL 2048 = variant 39's
+// shape (one block per CU, LDS work queue); THREADS 512, XABL 0 = the round-1 shape
+template <int EPI, int THREADS = 512, int XABL = 0>
+__global__ __launch_bounds__(THREADS, 4) void infer_accumulate_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                                      int64_t n, const h8* __restrict__ wf,
+                                                                      InferEpilogue epi) {
+    infer_v2_body<1, THREADS, false, kDefaultAbl | 1024 | 8192 | XABL, EPI>(q, out, n, wf, epi);  // encoder v3, buffer-load prefetch
 }
 
 // InputEncoding::Hash inference (EPI -1: plain infer; 0 / 2: fused accumulation as above)
@@ -2685,11 +2686,17 @@ hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, 
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
-    static int bpc[2] = {};
+    static int bpc[4] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
-    switch (mode) {
+    // NRC_ACC_THREADS=512 (read per launch, for tools/ab_accumulate.py) selects the round-1 shape; the default
+    // 1024-thread LDS-queue shape measured 82.6 vs 86.7 us per 1080p frame, bit-identical (profiles/r02_frame/)
+    const char* e = std::getenv("NRC_ACC_THREADS");
+    const bool q = !(e && std::atoi(e) == 512);
+    switch (mode * 2 + (q ? 1 : 0)) {
         case 0: return launch_persistent_infer(infer_accumulate_kernel<0>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
-        case 2: return launch_persistent_infer(infer_accumulate_kernel<2>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        case 4: return launch_persistent_infer(infer_accumulate_kernel<2>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        case 1: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, 2048>, 1024, bpc[2], ntiles, queries, out, n, wf, s, epi);
+        case 5: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, 2048>, 1024, bpc[3], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
