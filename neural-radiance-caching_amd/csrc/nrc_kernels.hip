@@ -1069,19 +1069,19 @@ __global__ __launch_bounds__(THREADS, 4) void infer_accumulate_kernel(const floa
 }
 
 // InputEncoding::Hash inference (EPI -1: plain infer; 0 / 2: fused accumulation as above)
-template <int EPI>
+template <int EPI, int XABL = 0>
 __global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                             int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
                                                             const uint32_t* __restrict__ grid) {
     // ABL 0: the buffer-store epilogue (32) measured 2 % slower here (536 vs 524 us; gather-bound kernel)
-    infer_v2_body<1, 512, false, 0, EPI, 1>(q, out, n, wf, epi, grid);
+    infer_v2_body<1, 512, false, XABL, EPI, 1>(q, out, n, wf, epi, grid);
 }
 
 // FrequencySH extension inference (EPI -1 plain; 0 / 2 fused accumulation)
-template <int EPI>
-__global__ __launch_bounds__(512, 4) void infer_sh_kernel(const float* __restrict__ q, float* __restrict__ out,
-                                                          int64_t n, const h8* __restrict__ wf, InferEpilogue epi) {
-    infer_v2_body<1, 512, false, kDefaultAbl, EPI, 2>(q, out, n, wf, epi);
+template <int EPI, int THREADS = 512, int XABL = 0>
+__global__ __launch_bounds__(THREADS, 4) void infer_sh_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                              int64_t n, const h8* __restrict__ wf, InferEpilogue epi) {
+    infer_v2_body<1, THREADS, false, kDefaultAbl | XABL, EPI, 2>(q, out, n, wf, epi);
 }
 
 // The production FrequencySH encoder unpacked to canonical order as f32 (parity tests): [n][80].
@@ -2546,6 +2546,13 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, nullptr);
 }
 
+// NRC_EXT_INFER_SHAPE=512 (read per launch, for tools/ab_ext_infer.py): the Hash / FrequencySH inference kernels in
+// their round-1 shape (fixed tiles per wave) instead of the per-block LDS work queue
+static bool ext_infer_round1_shape() {
+    const char* e = std::getenv("NRC_EXT_INFER_SHAPE");
+    return e && std::atoi(e) == 512;
+}
+
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
                              const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
     if (n <= 0) return hipSuccess;
@@ -2553,10 +2560,19 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
     static int bpc[3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
+    if (ext_infer_round1_shape()) {
+        switch (mode) {
+            case -1: return launch_persistent_infer(infer_hash_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi, g);
+            case 0: return launch_persistent_infer(infer_hash_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi, g);
+            case 2: return launch_persistent_infer(infer_hash_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi, g);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    static int bpq[3] = {};
     switch (mode) {
-        case -1: return launch_persistent_infer(infer_hash_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi, g);
-        case 0: return launch_persistent_infer(infer_hash_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi, g);
-        case 2: return launch_persistent_infer(infer_hash_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi, g);
+        case -1: return launch_persistent_infer(infer_hash_kernel<-1, 2048>, 512, bpq[0], ntiles, queries, out, n, wf, s, epi, g);
+        case 0: return launch_persistent_infer(infer_hash_kernel<0, 2048>, 512, bpq[1], ntiles, queries, out, n, wf, s, epi, g);
+        case 2: return launch_persistent_infer(infer_hash_kernel<2, 2048>, 512, bpq[2], ntiles, queries, out, n, wf, s, epi, g);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2567,10 +2583,19 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
     const int64_t ntiles = (n + 31) / 32;
     static int bpc[3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
+    if (ext_infer_round1_shape()) {
+        switch (mode) {
+            case -1: return launch_persistent_infer(infer_sh_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
+            case 0: return launch_persistent_infer(infer_sh_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
+            case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    static int bpq[3] = {};
     switch (mode) {
-        case -1: return launch_persistent_infer(infer_sh_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
-        case 0: return launch_persistent_infer(infer_sh_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
-        case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
+        case -1: return launch_persistent_infer(infer_sh_kernel<-1, 1024, 2048>, 1024, bpq[0], ntiles, queries, out, n, wf, s, epi);
+        case 0: return launch_persistent_infer(infer_sh_kernel<0, 1024, 2048>, 1024, bpq[1], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_sh_kernel<2, 1024, 2048>, 1024, bpq[2], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
