@@ -122,3 +122,26 @@ def test_wide_infer_full_frame_deterministic(nrc, orc, dev, precision):
         assert np.isfinite(a).all() and (a != 777.0).all()
     finally:
         net.destroy()
+
+
+@pytest.mark.parametrize("width", [64, 128])
+def test_training_full_batch_deterministic_every_slot(nrc, dev, width):
+    """Two handles stepped through the same 16,384-sample minibatches end bitwise identical in every state slot
+    (weights, Adam moments, EMA, inference weights): the weight-gradient partials are summed in a fixed order."""
+    import torch
+    e = nrc.InputEncoding.Frequency
+    nets = []
+    for _ in range(2):
+        n = nrc.Network()
+        n.init(stream=torch.cuda.current_stream(), encoding=e, config=nrc.default_config(e, width=width))
+        nets.append(n)
+    try:
+        for it in range(3):
+            q, t = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=700 + it)
+            losses = [n.train(_t(q, dev), _t(t, dev), loss=True) for n in nets]
+            assert losses[0] == losses[1]
+        for slot in nrc.StateSlot:
+            np.testing.assert_array_equal(nets[0].get_state(slot), nets[1].get_state(slot))
+    finally:
+        for n in nets:
+            n.destroy()
