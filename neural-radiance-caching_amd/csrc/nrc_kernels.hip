@@ -1243,7 +1243,9 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
 // ENC 0 = Frequency, 2 = FrequencySH (both 80-wide); EPI -1 plain, 0 / 2 fused accumulate_render_radiance.
 // Persistent waves, 2 per SIMD (one 512-thread block per CU: the f16 image takes 156 KiB of LDS).
 // THREADS 1024 (debug variant 1): 4 waves per SIMD within 128 VGPRs.
-template <int ENC, int PREC, int EPI, int THREADS = 512>
+// QUEUE (round 2, default): the block owns a contiguous range of tiles and its waves draw from an LDS counter (as the
+// 64-wide variant 39) instead of a fixed tile sequence per wave.
+template <int ENC, int PREC, int EPI, int THREADS = 512, bool QUEUE = false>
 __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(const float* __restrict__ q,
                                                                             float* __restrict__ out, int64_t n,
                                                                             const h8* __restrict__ img,
@@ -1251,8 +1253,10 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
                                                                             const uint32_t* __restrict__ wscale) {
     constexpr int NH8 = (PREC == 0 ? kWideF16Bytes : kWide8Bytes) / 16;
     __shared__ __attribute__((aligned(16))) h8 lw[NH8];
+    __shared__ uint32_t wq_next;
     fp32_flush_output_denorms();  // the omod doubling-chain encoder
     copy_to_lds_chunked<THREADS, NH8>(lw, img);
+    if (QUEUE && threadIdx.x == 0) wq_next = 0;
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1262,19 +1266,46 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
 #pragma unroll
         for (int l = 0; l < 5; ++l) sc[l] = wscale[l * 32 + r];
     }
-    const int64_t ngroups = (n + 31) >> 5;
+    const int64_t ntiles = (n + 31) >> 5;
     const int64_t wstride = (int64_t)gridDim.x * (THREADS / 64);
-    int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (g >= ngroups) return;
+    int64_t g, ngroups = ntiles, gbase = 0, ng = 0;
+    uint32_t nn_raw = 0;
+    if constexpr (QUEUE) {
+        gbase = (int64_t)blockIdx.x * ntiles / gridDim.x;
+        ngroups = (int64_t)(blockIdx.x + 1) * ntiles / gridDim.x;  // end of this block's range
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&wq_next, 1u);
+        g = gbase + (int64_t)__builtin_amdgcn_readfirstlane(t);
+        if (g >= ngroups) return;
+        if (lane == 0) t = atomicAdd(&wq_next, 1u);
+        ng = gbase + (int64_t)__builtin_amdgcn_readfirstlane(t);
+    } else {
+        g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        if (g >= ngroups) return;
+    }
     const int64_t last = n - 1;
     QLane Q = load_q_enc<ENC>(q, min(g * 32 + r, last), h);
     if constexpr (EPI >= 0) __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b96(u3{0u, 0u, 0u}, buffer_rsrc(out, 0), 0, 0, 0);
-    for (; g < ngroups; g += wstride) {
+    for (bool first = true; g < ngroups; first = false) {
+        if constexpr (QUEUE) {
+            if (!first) {
+                // the draw issued one iteration ago (an asm readfirstlane stays here; the builtin would be hoisted
+                // to the atomic and the wave would wait for it there)
+                uint32_t t;
+                asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(t) : "v"(nn_raw));
+                ng = gbase + (int64_t)t;
+            }
+        } else {
+            ng = g + wstride;
+        }
         h8 x[5];
         if constexpr (ENC == 2) encode_sh<true>(Q, h, x);
         else encode_fast<true>(Q, h, x);
-        Q = load_q_enc<ENC>(q, min((g + wstride) * 32 + r, last), h);  // clamped, branch-free prefetch
+        if constexpr (QUEUE) {
+            if (lane == 0) nn_raw = atomicAdd(&wq_next, 1u);  // the tile after next
+        }
+        Q = load_q_enc<ENC>(q, min(ng * 32 + r, last), h);  // clamped, branch-free prefetch
         const int64_t s0 = g * 32, sq = s0 + r;
         float tr[3] = {};
         float4 acc = {};
@@ -1320,6 +1351,7 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
                        __builtin_bit_cast(uint32_t, L2)};
         __builtin_amdgcn_raw_buffer_store_b96(ov, buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12),
                                               to_out ? r * 12 : kBufferOff, 0, 0);
+        g = ng;
     }
 }
 
@@ -2627,12 +2659,18 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
         return launch_persistent_infer(infer_wide_kernel<0, 1, -1, 1024>, 1024, bv[1], ntiles, queries, out, n,
                                        reinterpret_cast<const _Float16*>(img), s, e, scales);
     }
-    static int bpc[2][2][3] = {};
+    static int bpc[2][2][2][3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     const _Float16* im = reinterpret_cast<const _Float16*>(img);
-    int& b = bpc[prec][enc >> 1][mode + 1 == 0 ? 0 : mode == 0 ? 1 : 2];
-#define NRC_WIDE_LAUNCH(E, P, M) \
-    return launch_persistent_infer(infer_wide_kernel<E, P, M>, 512, b, ntiles, queries, out, n, im, s, epi, scales)
+    // NRC_WIDE_SHAPE=512 (read per launch, tools/ab_ext_infer.py --wide): the round-1 fixed-tiles-per-wave shape
+    const char* env = std::getenv("NRC_WIDE_SHAPE");
+    const bool queue = !(env && std::atoi(env) == 512);
+    int& b = bpc[queue][prec][enc >> 1][mode + 1 == 0 ? 0 : mode == 0 ? 1 : 2];
+#define NRC_WIDE_LAUNCH(E, P, M)                                                                                      \
+    return queue ? launch_persistent_infer(infer_wide_kernel<E, P, M, 512, true>, 512, b, ntiles, queries, out, n, im, \
+                                           s, epi, scales)                                                            \
+                 : launch_persistent_infer(infer_wide_kernel<E, P, M>, 512, b, ntiles, queries, out, n, im, s, epi,   \
+                                           scales)
 #define NRC_WIDE_MODES(E, P)                  \
     switch (mode) {                           \
         case -1: NRC_WIDE_LAUNCH(E, P, -1);   \
