@@ -118,6 +118,20 @@ __device__ __forceinline__ void slab_single(_Float16* __restrict__ slab, int L, 
     __builtin_nontemporal_store(u2{pk2(v[0], v[1]), pk2(v[2], v[3])}, (u2*)(slab + t16_slab_pos(L, tm, tn, lane, 0)));
 }
 
+// The same stores as raw buffer stores with an explicit cache policy AUX (gfx950 cpol bits: 1 sc0, 2 nt, 16 sc1):
+// the role-split kernel's slab stores (A/B of the policy, NRC_T16_SLAB_AUX)
+template <int AUX>
+__device__ __forceinline__ void slab_pair_b(_Float16* __restrict__ slab, int L, int tm, int tn_even, int lane, const u4& v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, buffer_rsrc(slab, slab_floats(0) * 2),
+                                           t16_slab_base(L, tm, tn_even) * 2 + lane * 16, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void slab_single_b(_Float16* __restrict__ slab, int L, int tm, int tn, int lane, const f4& v) {
+    const u2 w = {pk2(v[0], v[1]), pk2(v[2], v[3])};
+    __builtin_amdgcn_raw_buffer_store_b64(w, buffer_rsrc(slab, slab_floats(0) * 2), t16_slab_pos(L, tm, tn, lane, 0) * 2,
+                                          0, AUX);
+}
+
 // DPP sum over a 16-lane row (row_ror 8, 4, 2, 1): every lane of the row ends with the row's total
 __device__ __forceinline__ float row_sum16(float v) {
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
@@ -579,6 +593,7 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // in each backward step, compute the block's dW_L tiles from the images the chain waves wrote in the step before and
 // stream them to the slab. The two halves of a step share the SIMDs' MFMA pipes and hide each other's LDS and
 // dependency latency; the step's critical path is the chain alone instead of chain + dW.
+template <int AUX>
 __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                                int64_t b, float n_total, float loss_scale,
                                                                const h8* __restrict__ wf, const h8* __restrict__ wb,
@@ -620,7 +635,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
             const TrTile ta[1] = {TrTile{img_d1, off64(r0, pp), off64(r1, pp), 4096}};
             const TrTile tb[1] = {TrTile{img_a1, off64(r0, 4 * wave + pp), off64(r1, 4 * wave + pp), 4096}};
             dw_tiles<1, 1>(ta, tb, acc);
-            slab_single(slab, 5, 0, wave, lane, acc[0][0]);
+            slab_single_b<AUX>(slab, 5, 0, wave, lane, acc[0][0]);
         }
         lds_barrier();
         // steps 4..1: dW_L tiles (tm0 + i, tn0 + j) from buffer L & 1
@@ -637,7 +652,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
             f4 acc[2][2];
             dw_tiles<2, 2>(ta, tb, acc);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) slab_pair(slab, L, tm0 + i, tn0, lane, pack_pair(acc[i][0], acc[i][1]));
+            for (int i = 0; i < 2; ++i) slab_pair_b<AUX>(slab, L, tm0 + i, tn0, lane, pack_pair(acc[i][0], acc[i][1]));
             lds_barrier();
         }
         // step 0 (buffer 0): dW0 tiles (tm0 + i, 3 (wave & 1) + j); columns 4, 5 are K slots 64..95 (img_x2)
@@ -658,11 +673,11 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if ((wave & 1) == 0) {
-                    slab_pair(slab, 0, tm0 + i, 0, lane, pack_pair(acc[i][0], acc[i][1]));
-                    slab_single(slab, 0, tm0 + i, 2, lane, acc[i][2]);
+                    slab_pair_b<AUX>(slab, 0, tm0 + i, 0, lane, pack_pair(acc[i][0], acc[i][1]));
+                    slab_single_b<AUX>(slab, 0, tm0 + i, 2, lane, acc[i][2]);
                 } else {
-                    slab_single(slab, 0, tm0 + i, 3, lane, acc[i][0]);
-                    slab_pair(slab, 0, tm0 + i, 4, lane, pack_pair(acc[i][1], acc[i][2]));
+                    slab_single_b<AUX>(slab, 0, tm0 + i, 3, lane, acc[i][0]);
+                    slab_pair_b<AUX>(slab, 0, tm0 + i, 4, lane, pack_pair(acc[i][1], acc[i][2]));
                 }
             }
         }
@@ -887,8 +902,21 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
     const dim3 grid(t16_blocks(b)), block(64 * kWaves);
     const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
     if (split && !stamps) {
-        hipLaunchKernelGGL(train16_split_kernel, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total, loss_scale,
-                           f, bw, slabs, loss_partials);
+        // NRC_T16_SLAB_AUX (read per launch, A/B of the slab stores' cache policy, tools/ab_slab_aux.py): 16 sc1
+        // (default), 2 nt, 18 sc1 nt. sc1 stores write through and drop the line from the XCD's L2, so the kernel
+        // does not end with 5.9 MB of dirty slab lines to write back, and the reduce (on every XCD) reads them from
+        // memory either way: fused step 14.2 -> 12.7 us, gradients bitwise equal (profiles/r02_train/)
+        const char* e = std::getenv("NRC_T16_SLAB_AUX");
+        const int aux = e ? std::atoi(e) : 16;
+        if (aux == 16)
+            hipLaunchKernelGGL(train16_split_kernel<16>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
+                               loss_scale, f, bw, slabs, loss_partials);
+        else if (aux == 18)
+            hipLaunchKernelGGL(train16_split_kernel<18>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
+                               loss_scale, f, bw, slabs, loss_partials);
+        else
+            hipLaunchKernelGGL(train16_split_kernel<2>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
+                               loss_scale, f, bw, slabs, loss_partials);
         return hipGetLastError();
     }
     if (stamps) {
