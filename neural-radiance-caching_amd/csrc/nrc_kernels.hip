@@ -1680,13 +1680,19 @@ template <int L, int ENC = 0>
 __device__ __forceinline__ void dw_block_store(const f16v& acc, int mb, int nb, int lane, float* __restrict__ slab) {
     // fragment-major slab block (slab_block_base): 4 (layer 5: 2) lane-contiguous 16-byte stores per lane
     typedef float f4 __attribute__((ext_vector_type(4)));
-    f4* dst = (f4*)(slab + slab_block_base(ENC, L, mb, nb));
     constexpr int J = L == 5 ? 2 : 4;  // layer 5: registers 0..7 hold the 16 real rows
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const f4 v = {acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
+#if defined(NRC_SLAB_NT)
         // streamed: nontemporal (plain stores measured 18.8 -> 20.7 us per step)
-        __builtin_nontemporal_store(v, &dst[j * 64 + lane]);
+        __builtin_nontemporal_store(v, (f4*)(slab + slab_block_base(ENC, L, mb, nb)) + j * 64 + lane);
+#else
+        // sc1: write through, the line dropped from the XCD's L2 (no end-of-launch write-back of the slabs; the
+        // reduce reads them from memory on every XCD anyway; round 2, as nrc_train16.hip's slab stores)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), buffer_rsrc(slab, slab_floats(ENC) * 4),
+                                               (slab_block_base(ENC, L, mb, nb) + (j * 64 + lane) * 4) * 4, 0, 16);
+#endif
     }
 }
 
