@@ -2195,8 +2195,14 @@ __device__ __forceinline__ void store_frag_rows(_Float16* __restrict__ ws, int64
         const uint32_t w[4] = {__builtin_amdgcn_perm(hi0, lo0, 0x05040100u), __builtin_amdgcn_perm(hi0, lo0, 0x07060302u),
                                __builtin_amdgcn_perm(hi1, lo1, 0x05040100u), __builtin_amdgcn_perm(hi1, lo1, 0x07060302u)};
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint32_t*>(ws + (int64_t)acc_row(kk, h, jb + i) * ld + s0) = w[i];
+        for (int i = 0; i < 4; ++i) {
+            uint32_t* const dst = reinterpret_cast<uint32_t*>(ws + (int64_t)acc_row(kk, h, jb + i) * ld + s0);
+#if defined(NRC_WIDE_PLAIN_STORES)
+            *dst = w[i];
+#else
+            __hip_atomic_store(dst, w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1, as the slab stores
+#endif
+        }
     }
 }
 
@@ -2414,7 +2420,12 @@ __global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+#if defined(NRC_WIDE_PLAIN_STORES)
         if (row < out_dim) slab[row * in_dim + i] = sum[reg];
+#else
+        // sc1: written through, not left dirty in this XCD's L2 (wide_adam_kernel reads the chunks on every XCD)
+        if (row < out_dim) __hip_atomic_store(&slab[row * in_dim + i], sum[reg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     }
 }
 
