@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-wide", action="store_true", help="skip the configs[4] width-128 f16/FP8 inference lines")
     ap.add_argument("--no-hash", action="store_true", help="skip the InputEncoding::Hash line")
+    ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the configs[3] per-rank measurement")
+    ap.add_argument("--sustained", type=int, default=1000,
+                    help="N = 1: sustained-inference launches timed after as many untimed ones (0: skip)")
     ap.add_argument("--frame-iters", type=int, default=20, help="timed 1080p post-trace frames (0: skip)")
     ap.add_argument("--rehearse-comm", action="store_true",
                     help="N = 1 only: train through a world-1 RCCL communicator (nrc_train_dp), to rehearse the N > 1 "
@@ -241,6 +244,69 @@ def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
     return res
 
 
+def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_ms: float, step16k_ms: float) -> dict:
+    """configs[3] (C4) per-rank work, measured on ONE GPU: what each of the 8 ranks runs.
+    Inference: its 2^19-query shard (no collective). Training: one 2,048-sample slice of a 16,384-sample global
+    minibatch through nrc_train_dp on a world-1 RCCL communicator (gradient pass normalised by the global batch ->
+    ncclAllReduce -> Adam/EMA), plus the gradient pass (nrc_train_grad) and the apply (nrc_train_apply) on their own.
+    HIP events on the handle's stream. The 8-GPU prediction divides the 1-GPU work by the per-rank time; the
+    all-reduce at 8 ranks is NOT measured here (a world-1 communicator moves no bytes) and is stated as an assumption."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    n = QUERIES_C4 // 8
+    out = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    B, b_local = nrc.BATCH_SIZE, nrc.BATCH_SIZE // 8
+
+    def timed(fn, k: int) -> float:
+        for i in range(3):
+            fn(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(k):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / k
+
+    infer_ms = timed(lambda i: net.infer(q, out, n), iters)
+    state = [net.get_state(s) for s in (nrc.StateSlot.PARAMS, nrc.StateSlot.INFER, nrc.StateSlot.EMA,
+                                        nrc.StateSlot.ADAM_M, nrc.StateSlot.ADAM_V)]
+    step0 = net.step
+    comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
+    net.set_comm(comm)
+    tq, tt = frames_q[0], frames_t[0]
+    k = 4 * iters
+    dp_ms = timed(lambda i: net.train_dp(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B), k)
+    net.set_comm(None)
+    comm.destroy()
+    grad = torch.zeros(net.grad_floats, dtype=torch.float32, device=dev)
+    grad_ms = timed(lambda i: net.train_grad(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B, grad), k)
+    apply_ms = timed(lambda i: net.train_apply(grad), k)
+    local_ms = timed(lambda i: net.train_batch(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local), k)
+    for s, v in zip((nrc.StateSlot.PARAMS, nrc.StateSlot.INFER, nrc.StateSlot.EMA, nrc.StateSlot.ADAM_M,
+                     nrc.StateSlot.ADAM_V), state):
+        net.set_state(s, v)
+    net.step = step0
+    allreduce_assumed_us = 25.0
+    return {"workload": "configs[3] per-rank work on one GPU: 2^19-query inference shard; a 2048-sample slice of a "
+                        "16384-sample global minibatch (nrc_train_dp, world-1 RCCL communicator)",
+            "infer_queries": n, "infer_kernel_ms": infer_ms, "infer_M_queries_per_s": n / (infer_ms * 1e-3) / 1e6,
+            "train_b_local": b_local, "train_global_b": B,
+            "train_dp_step_ms": dp_ms, "train_grad_ms": grad_ms, "train_apply_ms": apply_ms,
+            "train_local_fused_step_ms": local_ms,
+            "prediction_8gpu": {
+                "infer_speedup": (t_full_ms / infer_ms) if infer_ms > 0 else None,
+                "infer_what": "1-GPU kernel time of the whole 2^22-query frame / per-rank 2^19-query kernel time "
+                              "(no collective on the inference path)",
+                "allreduce_us_assumed": allreduce_assumed_us,
+                "train_step_ms_8gpu": grad_ms + apply_ms + allreduce_assumed_us * 1e-3,
+                "train_speedup": step16k_ms / (grad_ms + apply_ms + allreduce_assumed_us * 1e-3),
+                "train_what": "1-GPU 16384-sample step / (per-rank gradient pass + apply + an ASSUMED 88-KiB RCCL "
+                              "all-reduce latency over 8 ranks; unmeasured)"}}
+
+
 def pmc_traffic() -> float | None:
     f = ROOT / "profiles" / f"pmc_infer_{ROUND}.json"
     if f.exists():
@@ -388,6 +454,30 @@ def main() -> None:
     train_frame_ms = max_over_ranks(time.perf_counter() - t0) / args.train_frames * 1e3
     train_step_ms = train_frame_ms / 4
 
+    # ---- sustained inference: the clock the chip holds under a long run of back-to-back
+    # launches is lower than in a short burst; the average of the last `sustained` of 2 x `sustained` launches
+    sustained = None
+    if args.sustained > 0:
+        for _ in range(args.sustained):
+            net.infer(q, out, nq)
+        ev2, ev3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev2.record(stream)
+        for _ in range(args.sustained):
+            net.infer(q, out, nq)
+        ev3.record(stream)
+        torch.cuda.synchronize()
+        s_ms = ev2.elapsed_time(ev3) / args.sustained
+        s_tf = FLOP_PER_QUERY * nq / (s_ms * 1e-3) / 1e12
+        sustained = {"launches": 2 * args.sustained, "timed": args.sustained, "infer_kernel_ms": s_ms,
+                     "achieved": s_tf, "frac": s_tf / PEAK_F16_TFLOPS,
+                     "M_queries_per_s": nq / (s_ms * 1e-3) / 1e6}
+
+    # ---- configs[3] per-rank work on one GPU (C4): 2^19-query shard + 2048-sample slices through nrc_train_dp
+    c4_per_rank = None
+    if world == 1 and not args.no_c4:
+        c4_per_rank = c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, max(10, args.steps // 4),
+                                         kernel_ms * QUERIES_C4 / nq, train_step_ms)
+
     # ---- one whole post-trace frame: fused infer+accumulate over the 1080p frame's
     # render + train-suffix queries, propagate, shuffle, 4 x train with the minibatch-loss read-back (1 GPU)
     frame = None
@@ -427,11 +517,14 @@ def main() -> None:
         "train_frame_ms": train_frame_ms,
         "infer_kernel_ms": kernel_ms,
         "weak": weak,
+        "c4_per_rank": c4_per_rank,
         "frame": frame,
         "wide_c5": wide,
         "hash": hashgrid,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F16_TFLOPS, "traffic": pmc_traffic(),
+                     "frac_burst": achieved / PEAK_F16_TFLOPS,
+                     "frac_sustained": sustained["frac"] if sustained else None, "sustained": sustained,
                      "algorithmic_bytes_per_launch": BYTES_PER_QUERY * nq,
                      "hbm_gbs_algorithmic": BYTES_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e9},
         "cpu_baseline": None,

@@ -170,6 +170,12 @@ nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
 nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 
 /* ---- test / tuning entries ---- */
+/* Process-wide A/B knobs (the library reads no environment variables): "train_kernel" (Frequency training kernel at
+ * nrc_init: -1/0 decoupled chain, 1 / 2 round-2 t16 role-split / 4-wave, 32 round-1 32x32x16), "train_shape" (decoupled
+ * chain block shape 0..5, -1 = by batch size), "scatter_min" / "scatter_max" (Hash grid-scatter slice plan). -1 restores
+ * the production choice. */
+nrc_status nrc_debug_set_knob(const char* name, int value);
+nrc_status nrc_debug_get_knob(const char* name, int* value);
 /* Inference through a specific kernel variant (0..25, see nrc_kernels.hip) for in-process A/B timing;
  * results are identical in meaning to nrc_infer_stream. */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,

@@ -11,8 +11,11 @@ import subprocess
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-# NRC_LIB_PATH: alternate build of the same library (tuning A/B across compile flags only)
-LIB_PATH = Path(os.environ["NRC_LIB_PATH"]) if os.environ.get("NRC_LIB_PATH") else PKG_DIR / "libnrc_amd.so"
+# NRC_LIB_PATH: alternate build of the same C-ABI -- libnrc_amd_debug.so (diagnostic stamps / clocks and the A/B
+# kernels that lost their comparisons) or a build with other compile flags. The product path loads libnrc_amd.so.
+PRODUCT_LIB_PATH = PKG_DIR / "libnrc_amd.so"
+DEBUG_LIB_PATH = PKG_DIR / "libnrc_amd_debug.so"
+LIB_PATH = Path(os.environ["NRC_LIB_PATH"]) if os.environ.get("NRC_LIB_PATH") else PRODUCT_LIB_PATH
 
 NUM_PARAMS = 22528
 GRAD_FLOATS = NUM_PARAMS + 4
@@ -39,7 +42,8 @@ EXPORTS = [
     "nrc_set_step", "nrc_debug_encode_net",
     "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_hash_scatter_inputs", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
-    "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert",
+    "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert", "nrc_debug_set_knob",
+    "nrc_debug_get_knob",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
@@ -128,6 +132,8 @@ def lib() -> ctypes.CDLL:
         "nrc_debug_encode_fast_variant": (st, [ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_infer_precision": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_fp8_convert": (st, [fp, fp, u32, ctypes.c_int, vp]),
+        "nrc_debug_set_knob": (st, [ctypes.c_char_p, ctypes.c_int]),
+        "nrc_debug_get_knob": (st, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -140,6 +146,21 @@ def lib() -> ctypes.CDLL:
 def check(status: int) -> None:
     if status != NRC_OK:
         raise NrcError(status, lib().nrc_last_error().decode(errors="replace"))
+
+
+def set_knob(name: str, value: int) -> None:
+    """Process-wide A/B knob of the library (nrc_debug_set_knob; -1 = the production choice)."""
+    check(lib().nrc_debug_set_knob(name.encode(), int(value)))
+
+
+def get_knob(name: str) -> int:
+    v = ctypes.c_int()
+    check(lib().nrc_debug_get_knob(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+def is_debug_library() -> bool:
+    return LIB_PATH.resolve() == DEBUG_LIB_PATH.resolve()
 
 
 def last_error() -> str:

@@ -1,5 +1,6 @@
 // nrc_capi.cpp — C-ABI implementation (include/nrc/nrc_c.h). Owns parameters, optimizer state,
 // MFMA weight images and workspaces (the reference's tcnn::TrainableModel, NRCNetwork.cu:15-20).
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -229,13 +230,12 @@ std::vector<int> build_t16_slab_map() {
     return m;
 }
 
-// Training kernel of a 64-wide Frequency network: the t16 kernel unless NRC_TRAIN_KERNEL=32 selects the round-1
-// 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
-bool want_t16(int encoding) {
-    if (encoding != NRC_ENCODING_FREQUENCY) return false;
-    const char* e = std::getenv("NRC_TRAIN_KERNEL");
-    return !(e && std::string(e) == "32");
-}
+// Training kernel of a 64-wide Frequency network: the t16-layout kernels (f16 slabs) unless the train_kernel knob
+// selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
+bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
+
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1};
+const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max"};
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -298,8 +298,9 @@ struct nrc_net {
     _Float16* wf_infer16 = nullptr;  // t16 nets: inference image in the t16 layout (nrc_infer16.hip)
     int *fwd_pos = nullptr, *bwd_pos = nullptr;
     int* fwdt_pos = nullptr;  // t16 training layout only (else the training image is laid out as fwd_pos)
-    bool t16 = false;         // Frequency training on nrc_train16.hip
-    bool t16_split = false;   // the role-split t16 kernel (default; NRC_T16_SPLIT=0 at init: the 4-wave one)
+    bool t16 = false;         // Frequency training in the t16 layout (f16 slabs)
+    int t16_kernel = 0;       // 0 decoupled chain (nrc_train_dc.hip, default), 1 / 2 round-2 role split / 4-wave
+                              // (nrc_train16.hip); the train_kernel knob at nrc_init
     int* slab_param = nullptr;  // [n_slab] parameter of each weight-gradient slab position
     int n_slab = 0;
     float* slabs = nullptr;
@@ -490,13 +491,31 @@ void wide_grad_partials(nrc_net* net, const float* in, const float* tgt, uint32_
                                         net->wide_ws_d, net->wide_slabs, net->wide_loss_partials, net->stream));
 }
 
+// dc shape of a b-sample step (train_shape knob, else by batch size)
+int dc_shape(uint32_t b) {
+    const int k = knob(kKnobTrainShape);
+    return k >= 0 ? k : dc_auto_shape(b);
+}
+
+// training blocks = weight-gradient slabs of a b-sample step of this handle's training kernel
+int train_block_count(const nrc_net* net, uint32_t b) {
+    if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0) {
+        const int S = dc_samples_per_block(dc_shape(b));
+        return (int)((b + (uint32_t)S - 1) / (uint32_t)S);
+    }
+    return train_blocks(b);
+}
+
 // 64-wide Frequency / FrequencySH fwd + loss + bwd + per-block dW slabs (n_total = 3 x global batch)
 void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total,
                     uint64_t* stamps = nullptr) {
-    if (net->t16)
+    if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0)
+        HIP_CHECK(launch_train_dc(dc_shape(b), in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
+                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, net->stream, stamps));
+    else if (net->t16)
         HIP_CHECK(launch_train16(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream,
-                                 net->t16_split));
+                                 net->t16_kernel != 2));
     else if (stamps)
         HIP_CHECK(launch_train_stamped(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                        net->slabs, net->loss_partials, stamps, net->stream));
@@ -521,7 +540,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
         }
         return;
     }
-    const int blocks = train_blocks(b);
+    const int blocks = train_block_count(net, b);
     net->ensure_slabs(blocks);
     if (net->hash())
         HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
@@ -596,7 +615,38 @@ nrc_loss_slots nrc_amd::net_loss_slots(nrc_net* net) {
     return {net->loss_dev, net->loss_host};
 }
 
+int nrc_amd::knob(Knob k) { return g_knobs[k].load(std::memory_order_relaxed); }
+
+namespace {
+const char* const kDebugOnly =
+    "diagnostic kernel of the debug library: load libnrc_amd_debug.so (NRC_LIB_PATH) for stamps, clocks and A/B variants";
+}
+
 extern "C" {
+
+nrc_status nrc_debug_set_knob(const char* name, int value) {
+    return guarded([&] {
+        if (!name) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null knob name");
+        for (int k = 0; k < kKnobCount; ++k)
+            if (std::strcmp(name, kKnobNames[k]) == 0) {
+                g_knobs[k].store(value, std::memory_order_relaxed);
+                return;
+            }
+        throw ApiError(NRC_ERR_INVALID_ARGUMENT, std::string("unknown knob ") + name);
+    });
+}
+
+nrc_status nrc_debug_get_knob(const char* name, int* value) {
+    return guarded([&] {
+        if (!name || !value) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null argument");
+        for (int k = 0; k < kKnobCount; ++k)
+            if (std::strcmp(name, kKnobNames[k]) == 0) {
+                *value = g_knobs[k].load(std::memory_order_relaxed);
+                return;
+            }
+        throw ApiError(NRC_ERR_INVALID_ARGUMENT, std::string("unknown knob ") + name);
+    });
+}
 
 const char* nrc_version(void) { return "nrc-mi355x 0.1 (gfx950)"; }
 const char* nrc_last_error(void) { return g_last_error.c_str(); }
@@ -725,24 +775,23 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         build_scatter_maps(fwd, bwd, net->encoding);
         net->t16 = want_t16(net->encoding);
         {
-            // the role-split kernel is the default (in-process A/B: step 14.1 vs 14.8 us, bitwise-identical
-            // gradient, profiles/r02_train/); NRC_T16_SPLIT=0 selects the 4-wave kernel
-            const char* e = std::getenv("NRC_T16_SPLIT");
-            net->t16_split = net->t16 && !(e && *e == '0');
+            // the decoupled-chain kernel is the default; knob train_kernel = 1 / 2 selects round 2's role-split /
+            // 4-wave t16 kernels (in-process A/B)
+            const int k = knob(kKnobTrainKernel);
+            net->t16_kernel = (k == 1 || (k == 2 && NRC_DEBUG_KERNELS)) ? k : 0;
         }
         if (net->t16) {
             std::vector<int> fwdt;
             build_t16_maps(fwdt, bwd);
             HIP_CHECK(hipMalloc(&net->fwdt_pos, sizeof(int) * net->n_mlp));
             HIP_CHECK(hipMemcpy(net->fwdt_pos, fwdt.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
-            // A/B only (debug variants 50/51, nrc_infer16.hip, rejected in round 2: DESIGN.md §8): the t16-layout
-            // inference image, packed by the optimizer only when NRC_DEBUG_INFER16 is set
+#if NRC_DEBUG_KERNELS
+            // debug library only (variants 50/51, nrc_infer16.hip, rejected in round 2: DESIGN.md §8): the t16-layout
+            // inference image, packed by the optimizer
             static_assert(kT16FwdFrags * kFragHalves == kFwdHalves, "t16 forward image size");
-            const char* e = std::getenv("NRC_DEBUG_INFER16");
-            if (e && *e && *e != '0') {
-                HIP_CHECK(hipMalloc(&net->wf_infer16, sizeof(_Float16) * kFwdHalves));
-                HIP_CHECK(hipMemset(net->wf_infer16, 0, sizeof(_Float16) * kFwdHalves));  // dummy slots stay 0
-            }
+            HIP_CHECK(hipMalloc(&net->wf_infer16, sizeof(_Float16) * kFwdHalves));
+            HIP_CHECK(hipMemset(net->wf_infer16, 0, sizeof(_Float16) * kFwdHalves));  // dummy slots stay 0
+#endif
         }
         HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
@@ -759,7 +808,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         net->initialized = true;
         repack(net, nullptr);
         HIP_CHECK(hipDeviceSynchronize());
-        net->ensure_slabs(train_blocks(NRC_BATCH_SIZE));
+        net->ensure_slabs(train_block_count(net, NRC_BATCH_SIZE));
         if (verbose) {
             std::printf("\n----------------------- NETWORK CONFIG -----------------------\n%s\n"
                         "--------------------------------------------------------------\n\n",
@@ -962,7 +1011,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
                                        net->optim(net->step + 1), net->stream));
             return;
         }
-        const int blocks = train_blocks(b);
+        const int blocks = train_block_count(net, b);
         net->ensure_slabs(blocks);
         if (net->hash()) {
             // the grid-table gradient accumulates in the handle's f16 buffer (packed-half atomics) and is exported as
@@ -1138,12 +1187,19 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
         if (variant < 0 || variant >= kNumInferVariants) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown variant");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+#if NRC_DEBUG_KERNELS
         if (variant == 50 || variant == 51) {  // 51 (debug): the t16 training image (master weights)
-            if (!net->wf_infer16) throw ApiError(NRC_ERR_UNSUPPORTED, "variants 50/51 need NRC_DEBUG_INFER16=1 at init (t16 inference image)");
+            if (!net->wf_infer16) throw ApiError(NRC_ERR_UNSUPPORTED, "variants 50/51 need a Frequency t16 handle");
             HIP_CHECK(launch_infer16(in, out, n, variant == 50 ? net->wf_infer16 : net->wf_train, stream));
             return;
         }
-        HIP_CHECK(launch_infer_variant(variant, in, out, n, net->wf_infer, stream, net->work_queue));
+#endif
+        const hipError_t e = launch_infer_variant(variant, in, out, n, net->wf_infer, stream);
+        if (e == hipErrorInvalidValue && variant != kProductInferVariant)
+            throw ApiError(NRC_ERR_UNSUPPORTED, "inference variant " + std::to_string(variant) +
+                                                    " is an A/B kernel of the debug library (libnrc_amd_debug.so via "
+                                                    "NRC_LIB_PATH)");
+        HIP_CHECK(e);
     });
 }
 
@@ -1152,7 +1208,9 @@ nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, ui
         if (!host_dst || !waves) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null pointer");
         int64_t w = 0;
         HIP_CHECK(hipDeviceSynchronize());
-        HIP_CHECK(read_infer_clock(host_dst, (int64_t)cap_waves, &w));
+        const hipError_t e = read_infer_clock(host_dst, (int64_t)cap_waves, &w);
+        if (e == hipErrorNotSupported) throw ApiError(NRC_ERR_UNSUPPORTED, kDebugOnly);
+        HIP_CHECK(e);
         *waves = (uint32_t)w;
     });
 }
@@ -1165,7 +1223,9 @@ nrc_status nrc_debug_infer_stamps(nrc_net* net, const float* in, float* out, uin
         if (net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "inference stamps are a 64-wide diagnostic");
         if (!in || !out || !stamps_d || !waves_h || n == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
         int64_t waves = 0;
-        HIP_CHECK(launch_infer_stamped(in, out, n, net->wf_infer, stamps_d, &waves, net->stream));
+        const hipError_t e = launch_infer_stamped(in, out, n, net->wf_infer, stamps_d, &waves, net->stream);
+        if (e == hipErrorNotSupported) throw ApiError(NRC_ERR_UNSUPPORTED, kDebugOnly);
+        HIP_CHECK(e);
         if (waves > NRC_INFER_STAMP_WAVES_MAX) throw ApiError(NRC_ERR_INTERNAL, "stamp buffer too small");
         *waves_h = (uint64_t)waves;
     });
@@ -1177,7 +1237,10 @@ nrc_status nrc_debug_train_stamps(nrc_net* net, const float* in, const float* tg
         require_frequency(net, "nrc_debug_train_stamps");
         if (net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "training stamps are a 64-wide diagnostic");
         if (!in || !tgt || !stamps_d || b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad arguments");
-        const int blocks = train_blocks(b);
+#if !NRC_DEBUG_KERNELS
+        throw ApiError(NRC_ERR_UNSUPPORTED, kDebugOnly);
+#endif
+        const int blocks = train_block_count(net, b);
         net->ensure_slabs(blocks);
         train_partials(net, in, tgt, b, 3.0f * (float)b, stamps_d);
     });
@@ -1209,7 +1272,9 @@ nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* i
         if (variant && wide_enc(net) != 0) throw ApiError(NRC_ERR_UNSUPPORTED, "kernel variants are Frequency-only");
         if (n == 0) return;
         if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
-        HIP_CHECK(infer_wide(net, precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, stream));
+        const hipError_t e = infer_wide(net, precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, stream);
+        if (e == hipErrorNotSupported) throw ApiError(NRC_ERR_UNSUPPORTED, kDebugOnly);
+        HIP_CHECK(e);
     });
 }
 

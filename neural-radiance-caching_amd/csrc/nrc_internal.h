@@ -7,6 +7,12 @@
 
 #include "nrc/layout.h"
 
+// 1 in libnrc_amd_debug.so: diagnostic builds (phase stamps, in-kernel clocks) and the A/B kernels that lost their
+// comparisons; 0 in the product library libnrc_amd.so
+#ifndef NRC_DEBUG_KERNELS
+#define NRC_DEBUG_KERNELS 0
+#endif
+
 namespace nrc_amd {
 
 // ---- MFMA fragment images (f16). One fragment = one v_mfma_f32_32x32x16_f16 A operand for a whole
@@ -174,10 +180,11 @@ hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, h
 
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
-// variants kept for A/B: 0, 23, 30, 39 (default), 40 (39 + in-kernel clock); wq is unused since the launch-wide
-// queue variants were removed
+// the product kernel is variant 39; the debug library (NRC_DEBUG_KERNELS) also has the A/B variants 0, 23, 30 and 40
+// (39 + in-kernel clock)
+constexpr int kProductInferVariant = 39;
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
-                                hipStream_t s, uint32_t* wq = nullptr);
+                                hipStream_t s);
 constexpr int kNumInferVariants = 52;  // 50: launch_infer16 (the t16 image)
 // Frequency inference on v_mfma_f32_16x16x32_f16 (nrc_infer16.hip) from the t16-layout inference image
 hipError_t launch_infer16(const float* queries, float* out, int64_t n, const _Float16* wf16, hipStream_t s);
@@ -242,6 +249,28 @@ struct ModelBuffers {
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
                           hipStream_t s, bool split = false);  // split: the role-split kernel (NRC_T16_SPLIT at init)
+// Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16
+// slab format as launch_train16; one slab per block of dc_samples_per_block(shape) samples.
+int dc_samples_per_block(int shape);
+// stamps (diagnostic, may be null): 16 uint64 per wave [block][wave][16], dc_waves_per_block(shape) waves per block
+hipError_t launch_train_dc(int shape, const float* queries, const float* targets, int64_t b, float n_total,
+                           float loss_scale, const _Float16* wf, const _Float16* wb, _Float16* slabs,
+                           float* loss_partials, hipStream_t s, uint64_t* stamps = nullptr);
+int dc_waves_per_block(int shape);
+// the production shape for a batch of b samples
+int dc_auto_shape(int64_t b);
+
+// ---- process-wide A/B knobs (nrc_debug_set_knob; never read from the environment). -1 = the production choice.
+enum Knob : int {
+    kKnobTrainKernel = 0,  // Frequency training: -1 / 0 decoupled chain (dc), 1 round-2 t16 role split, 2 round-2 t16
+                           // 4-wave, 32 round-1 32x32x16 (read at nrc_init)
+    kKnobTrainShape = 1,   // dc shape (0..5), -1 = dc_auto_shape(b)
+    kKnobScatterMin = 2,   // Hash grid scatter slice plan (samples per block at level 0 / cap), -1 = 1024 / 2048
+    kKnobScatterMax = 3,
+    kKnobCount = 4
+};
+int knob(Knob k);
+
 // host-f32 Adam step-size and EMA debias of optimizer step oa.step (tcnn adam.h; identical to the oracle's)
 void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias);
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state

@@ -144,6 +144,7 @@ __device__ __forceinline__ void copy_to_lds(h8* __restrict__ dst, const h8* __re
     }
 }
 
+#if NRC_DEBUG_KERNELS  // round-1 reference kernel (debug library only)
 // ------------------------------------------------------------------------------------------------
 // Inference: persistent waves, 32 queries per wave-iteration.
 // ------------------------------------------------------------------------------------------------
@@ -184,6 +185,8 @@ __global__ __launch_bounds__(kInferThreads) void infer_kernel(const float* __res
         }
     }
 }
+
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // Inference v2: VALU-lean encoding, packed-f16 ReLU, LDS-resident weights, TILES x 32 queries per
@@ -347,8 +350,10 @@ __device__ __forceinline__ void encode_v3(const QLane& Q, int h, h8 (&x)[5]) {
 // Diagnostic clock of the inference kernels (ABL & 512): per wave (s_memtime cycles of the persistent loop, the
 // s_memrealtime 100 MHz ticks at loop start, loop end and wave start, HW_ID and XCC_ID), read back by
 // nrc_debug_read_infer_clock.
+#if NRC_DEBUG_KERNELS
 constexpr int kInferClockWavesMax = 8192;
 __device__ uint64_t g_infer_clock[6 * kInferClockWavesMax];
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // HashGrid (InputEncoding::Hash, NRCNetworkConfigs.h:94-103; spec in oracle/nrc_hash_oracle.c): lane half h
@@ -718,7 +723,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
                                               const h8* __restrict__ wf, const InferEpilogue& epi,
                                               const uint32_t* __restrict__ grid = nullptr) {
     constexpr int KK0 = ENC == 1 ? 4 : 5;
-    uint64_t rstart = 0;
+    [[maybe_unused]] uint64_t rstart = 0;
     if constexpr ((ABL & 512) != 0) rstart = __builtin_amdgcn_s_memrealtime();
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
     // ABL & 8: per-wave staging of a tile's 32 x 12-B results so they leave as 24 contiguous 16-B stores
@@ -804,7 +809,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     uint64_t ph[kInferPhases] = {};
     uint64_t tprev = 0;
     if constexpr ((ABL & 256) != 0) tprev = stamp_now();
-    uint64_t clk0 = 0, rclk0 = 0;
+    [[maybe_unused]] uint64_t clk0 = 0, rclk0 = 0;
     if constexpr ((ABL & 512) != 0) {
         clk0 = __builtin_amdgcn_s_memtime();
         rclk0 = __builtin_amdgcn_s_memrealtime();
@@ -1021,6 +1026,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         }
     }
     finish();
+#if NRC_DEBUG_KERNELS
     if constexpr ((ABL & 512) != 0) {
         const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         const int64_t wid = (int64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
@@ -1033,6 +1039,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             g_infer_clock[6 * wid + 5] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);  // hwreg(HW_REG_XCC_ID)
         }
     }
+#endif
     if constexpr ((ABL & 256) != 0) {
         const uint64_t tn = stamp_now();
         ph[7] += tn - tprev;
@@ -1050,6 +1057,7 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
     infer_v2_body<TILES, THREADS, PREFETCH, ABL, -1>(q, out, n, wf, InferEpilogue{});
 }
 
+#if NRC_DEBUG_KERNELS
 // Diagnostic build of the default inference kernel (variant 23) with per-wave phase stamps (ABL & 256).
 __global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                              int64_t n, const h8* __restrict__ wf,
@@ -1058,6 +1066,8 @@ __global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __rest
     e.stamps = stamps;
     infer_v2_body<1, 512, false, kDefaultAbl | 256, -1>(q, out, n, wf, e);
 }
+
+#endif
 
 // the default inference configuration with the accumulation epilogue: THREADS 1024 + XABL 2048 = variant 39's
 // shape (one block per CU, LDS work queue); THREADS 512, XABL 0 = the round-1 shape
@@ -2521,6 +2531,7 @@ static hipError_t launch_persistent_infer(K kernel, int threads, int& cache_bpc,
     return hipGetLastError();
 }
 
+#if NRC_DEBUG_KERNELS
 static int64_t g_last_clock_waves = 0;
 template <class K, class... Extra>
 static hipError_t launch_clocked(K kernel, int threads, int& cache_bpc, int64_t groups, const float* queries, float* out,
@@ -2539,6 +2550,10 @@ hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_infer_clock), sizeof(uint64_t) * 6 * w, 0, hipMemcpyDeviceToHost);
 }
 
+#else
+hipError_t read_infer_clock(uint64_t*, int64_t, int64_t*) { return hipErrorNotSupported; }
+#endif
+
 // Inference kernel variants (A/B-able in one process through nrc_debug_infer_variant):
 //   0: v1 (weights hoisted into registers, one wave per SIMD)
 //   1: v2, 1 tile (32 queries) per wave iteration, up to 3 waves per SIMD
@@ -2555,15 +2570,15 @@ hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves) {
 static int g_default_infer_variant = 39;
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
-                                hipStream_t s, uint32_t* wq) {
+                                hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
     static int bpc[kNumInferVariants] = {};
-    (void)wq;
     switch (variant) {
         // The kernels kept for in-process A/B (tools/ab_infer.py). The rejected ones of rounds 1-2 (register-resident
         // weights, explicit layer-ahead prefetch, ping-pong tiles, 2-tile waves, SIMD-staggered starts, launch-wide
         // work queue, ablations) were measured, recorded in DESIGN.md §13 / profiles/r02_infer, and removed.
+#if NRC_DEBUG_KERNELS
         // 0: round-1 reference kernel (32-query tiles, one tile per wave iteration)
         case 0: return launch_persistent_infer(infer_kernel, kInferThreads, bpc[0], ntiles, queries, out, n, wf, s);
         // 23: round-1 production (1 tile / 4 waves per SIMD, omod triangle chain, branch-free prefetch, buffer stores)
@@ -2572,12 +2587,14 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 30: return launch_persistent_infer(infer_kernel_v2<1, 4, 512, false, 48 | 1024>, 512, bpc[30], ntiles, queries, out, n, wf, s);
         // 39 (default): 30 with 1024-thread blocks (one per CU) drawing tiles from an LDS work queue, buffer-load query
         // prefetch and the packed output epilogue; 40: 39 with the in-kernel clock (nrc_debug_read_infer_clock)
-        case 39: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192>, 1024, bpc[39], ntiles, queries, out, n, wf, s);
         case 40: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 512>, 1024, bpc[40], ntiles, queries, out, n, wf, s);
+#endif
+        case 39: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192>, 1024, bpc[39], ntiles, queries, out, n, wf, s);
         default: return hipErrorInvalidValue;
     }
 }
 
+#if NRC_DEBUG_KERNELS
 // Diagnostic: the default kernel with phase stamps; stamps gets kInferPhases sums per wave of the persistent grid.
 hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
                                 int64_t* waves, hipStream_t s) {
@@ -2591,37 +2608,27 @@ hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, con
     return hipGetLastError();
 }
 
-hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
-    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, nullptr);
+#else
+hipError_t launch_infer_stamped(const float*, float*, int64_t, const _Float16*, uint64_t*, int64_t*, hipStream_t) {
+    return hipErrorNotSupported;
 }
+#endif
 
-// NRC_EXT_INFER_SHAPE=512 (read per launch, for tools/ab_ext_infer.py): the Hash / FrequencySH inference kernels in
-// their round-1 shape (fixed tiles per wave) instead of the per-block LDS work queue
-static bool ext_infer_round1_shape() {
-    const char* e = std::getenv("NRC_EXT_INFER_SHAPE");
-    return e && std::atoi(e) == 512;
+hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
+    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s);
 }
 
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
                              const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
-    static int bpc[3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
-    if (ext_infer_round1_shape()) {
-        switch (mode) {
-            case -1: return launch_persistent_infer(infer_hash_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi, g);
-            case 0: return launch_persistent_infer(infer_hash_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi, g);
-            case 2: return launch_persistent_infer(infer_hash_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi, g);
-            default: return hipErrorInvalidValue;
-        }
-    }
     static int bpq[3] = {};
     switch (mode) {
-        case -1: return launch_persistent_infer(infer_hash_kernel<-1, 2048>, 512, bpq[0], ntiles, queries, out, n, wf, s, epi, g);
-        case 0: return launch_persistent_infer(infer_hash_kernel<0, 2048>, 512, bpq[1], ntiles, queries, out, n, wf, s, epi, g);
-        case 2: return launch_persistent_infer(infer_hash_kernel<2, 2048>, 512, bpq[2], ntiles, queries, out, n, wf, s, epi, g);
+        case -1: return launch_persistent_infer(infer_hash_kernel<-1, 2048 | 32>, 512, bpq[0], ntiles, queries, out, n, wf, s, epi, g);
+        case 0: return launch_persistent_infer(infer_hash_kernel<0, 2048 | 32>, 512, bpq[1], ntiles, queries, out, n, wf, s, epi, g);
+        case 2: return launch_persistent_infer(infer_hash_kernel<2, 2048 | 32>, 512, bpq[2], ntiles, queries, out, n, wf, s, epi, g);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2630,16 +2637,7 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
                            float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
-    static int bpc[3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
-    if (ext_infer_round1_shape()) {
-        switch (mode) {
-            case -1: return launch_persistent_infer(infer_sh_kernel<-1>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
-            case 0: return launch_persistent_infer(infer_sh_kernel<0>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
-            case 2: return launch_persistent_infer(infer_sh_kernel<2>, 512, bpc[2], ntiles, queries, out, n, wf, s, epi);
-            default: return hipErrorInvalidValue;
-        }
-    }
     static int bpq[3] = {};
     switch (mode) {
         case -1: return launch_persistent_infer(infer_sh_kernel<-1, 1024, 2048>, 1024, bpq[0], ntiles, queries, out, n, wf, s, epi);
@@ -2667,6 +2665,7 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
         return hipErrorInvalidValue;
     const int64_t ntiles = (n + 31) / 32;
     if (variant == 1) {
+#if NRC_DEBUG_KERNELS  // 1024-thread blocks (4 waves per SIMD): A/B only, debug library
         if (enc != 0 || mode != -1) return hipErrorInvalidValue;
         static int bv[2] = {};
         const InferEpilogue e{};
@@ -2675,19 +2674,19 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
                                            reinterpret_cast<const _Float16*>(img), s, e, scales);
         return launch_persistent_infer(infer_wide_kernel<0, 1, -1, 1024>, 1024, bv[1], ntiles, queries, out, n,
                                        reinterpret_cast<const _Float16*>(img), s, e, scales);
+#else
+        return hipErrorNotSupported;
+#endif
     }
-    static int bpc[2][2][2][3] = {};
+    static int bpc[2][2][3] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     const _Float16* im = reinterpret_cast<const _Float16*>(img);
-    // NRC_WIDE_SHAPE=512 (read per launch, tools/ab_ext_infer.py --wide): the round-1 fixed-tiles-per-wave shape
-    const char* env = std::getenv("NRC_WIDE_SHAPE");
-    const bool queue = !(env && std::atoi(env) == 512);
-    int& b = bpc[queue][prec][enc >> 1][mode + 1 == 0 ? 0 : mode == 0 ? 1 : 2];
-#define NRC_WIDE_LAUNCH(E, P, M)                                                                                      \
-    return queue ? launch_persistent_infer(infer_wide_kernel<E, P, M, 512, true>, 512, b, ntiles, queries, out, n, im, \
-                                           s, epi, scales)                                                            \
-                 : launch_persistent_infer(infer_wide_kernel<E, P, M>, 512, b, ntiles, queries, out, n, im, s, epi,   \
-                                           scales)
+    // per-block LDS work queue (round 2; the round-1 fixed-tiles-per-wave shape measured 1,010.9 vs 981.8 us f16 and
+    // 714.7 vs 669.2 us FP8 per 2^23 queries, profiles/r02_infer/ab_wide_queue_vs_round1.json, and was removed)
+    int& b = bpc[prec][enc >> 1][mode + 1 == 0 ? 0 : mode == 0 ? 1 : 2];
+#define NRC_WIDE_LAUNCH(E, P, M)                                                                                  \
+    return launch_persistent_infer(infer_wide_kernel<E, P, M, 512, true>, 512, b, ntiles, queries, out, n, im, s, epi, \
+                                   scales)
 #define NRC_WIDE_MODES(E, P)                  \
     switch (mode) {                           \
         case -1: NRC_WIDE_LAUNCH(E, P, -1);   \
@@ -2766,17 +2765,13 @@ hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, 
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
-    static int bpc[4] = {};
+    static int bpc[2] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
-    // NRC_ACC_THREADS=512 (read per launch, for tools/ab_accumulate.py) selects the round-1 shape; the default
-    // 1024-thread LDS-queue shape measured 82.6 vs 86.7 us per 1080p frame, bit-identical (profiles/r02_frame/)
-    const char* e = std::getenv("NRC_ACC_THREADS");
-    const bool q = !(e && std::atoi(e) == 512);
-    switch (mode * 2 + (q ? 1 : 0)) {
-        case 0: return launch_persistent_infer(infer_accumulate_kernel<0>, 512, bpc[0], ntiles, queries, out, n, wf, s, epi);
-        case 4: return launch_persistent_infer(infer_accumulate_kernel<2>, 512, bpc[1], ntiles, queries, out, n, wf, s, epi);
-        case 1: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, 2048>, 1024, bpc[2], ntiles, queries, out, n, wf, s, epi);
-        case 5: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, 2048>, 1024, bpc[3], ntiles, queries, out, n, wf, s, epi);
+    // one 1024-thread block per CU drawing tiles from an LDS work queue (round 2: 82.6 vs 86.7 us per 1080p frame for
+    // the round-1 512-thread shape, bit-identical, profiles/r02_frame/; the round-1 shape was removed in round 3)
+    switch (mode) {
+        case 0: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, 2048>, 1024, bpc[0], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, 2048>, 1024, bpc[1], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2805,6 +2800,7 @@ hipError_t launch_train_fwd_bwd(const float* queries, const float* targets, int6
     return hipGetLastError();
 }
 
+#if NRC_DEBUG_KERNELS
 hipError_t launch_train_stamped(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                                 const _Float16* wf, const _Float16* wb, float* slabs, float* loss_partials,
                                 uint64_t* stamps, hipStream_t s) {
@@ -2813,6 +2809,13 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, stamps);
     return hipGetLastError();
 }
+
+#else
+hipError_t launch_train_stamped(const float*, const float*, int64_t, float, float, const _Float16*, const _Float16*, float*,
+                                float*, uint64_t*, hipStream_t) {
+    return hipErrorNotSupported;
+}
+#endif
 
 // Sparse Adam + EMA + f16 table packs for the HashGrid parameters (tcnn non-matrix params, SURVEY §8(f) row 3;
 // oracle/nrc_hash_oracle.c orc_hash_adam_ema): an entry whose gradient is exactly zero keeps its moments, weight
@@ -3012,10 +3015,9 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
                        reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
                        bcap);
-    static const int smin_env = getenv("NRC_SCATTER_MIN") ? atoi(getenv("NRC_SCATTER_MIN")) : 0;
-    static const int smax_env = getenv("NRC_SCATTER_MAX") ? atoi(getenv("NRC_SCATTER_MAX")) : 0;
-    // tuning overrides (A/B only); defaults from the sweep in profiles/r01_hash/README.md
-    const int smin = smin_env > 0 ? smin_env : 1024, smax = smax_env > 0 ? smax_env : 2048;
+    // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep in profiles/r01_hash/README.md
+    const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);
+    const int smin = kmin > 0 ? kmin : 1024, smax = kmax > 0 ? kmax : 2048;
     ScatterPlan plan;
     int nb = 0;
     for (int l = 0; l < NRC_HASH_LEVELS; ++l) {

@@ -15,23 +15,12 @@
 //   barriers: dW_L = delta_L a_{L-1}^T over the block's 128 samples (16x16 tiles from transposed LDS reads of the
 //   [sample][feature] images) and delta_{L-1} = (W_L^T delta_L) * [a_{L-1} > 0] (register chain, backward image in
 //   LDS), the next layer's images written to the other buffer, the dW tiles streamed to the block's slab.
-#include <cstdlib>
-
 #include "nrc_t16.h"
 
 namespace nrc_amd {
 namespace {
 
-using t16::f4;
-using t16::mfma16;
-using t16::relu_pk;
-using t16::relu_b;
-using t16::encode16;
-typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
-}
+using namespace t16;
 
 // LDS carve-up (bytes). The four [128][64] f16 images (deltas and activations, double-buffered) sit at offset 0, so
 // that an image access is one per-lane offset VGPR plus an immediate (the 16-bit DS offset field reaches every image);
@@ -46,99 +35,17 @@ constexpr int kOffWf = kOffWb + kT16BwdFrags * 1024;      // 110848
 constexpr int kLds = kOffWf + 48 * 1024;                  // 160000
 static_assert(kLds <= 160 * 1024, "LDS budget");
 
-// [sample r][64 features] image, 128-B rows of 16 quads (4 features = 8 B). Quad Q of row r sits at slot
-// Q ^ swz(r), swz a bijection of r's low 4 bits (bit 0 -> 0, 2 -> 1, 1 -> 2, 3 -> 3). Row writes (ds_write_b64, banks
-// (a / 4) mod 32 in 16-lane groups = 16 samples x one quad) see 16 distinct slots; transposed reads (banks (a / 4)
-// mod 64 in 32-lane halves = samples 8G + q, G = 0..1, q = 0..3, x quads 4t + p) get 32 distinct 8-byte bank pairs
-// because bit 0 of r picks the 256-B half and bits 1, 3 the quad group (tests/test_layouts.py checks both).
-__device__ __forceinline__ int swz64(int r) {
-    return (r & 1) | (((r >> 2) & 1) << 1) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3);
-}
-__device__ __forceinline__ int off64(int r, int Q) { return r * 128 + 8 * (Q ^ swz64(r)); }
-// [sample][32 features] image (layer-0 slots 64..95), 64-B rows of 8 quads, swizzled by r's bits 1..3
-__device__ __forceinline__ int swz32(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | (((r >> 3) & 1) << 2); }
-__device__ __forceinline__ int off32(int r, int Q) { return r * 64 + 8 * (Q ^ swz32(r)); }
-
-__device__ __forceinline__ h4 tr16(const char* p) {
-    const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
-    return __builtin_bit_cast(h4, v);
-}
-__device__ __forceinline__ h8 tr_pair(const char* p0, const char* p1) {
-    const h4 a = tr16(p0), b = tr16(p1);
-    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-// backward ReLU gate on packed halves: d where the activation m > 0, else +0. m is +0 or positive bits (relu_pk),
-// so min_u16(m, 1) is the 0/1 mask and an integer multiply selects (2 VALU per dword). The min is inline asm (the
-// compiler turns a visible min-and-multiply into compares and selects); the multiply, whose result MFMAs read, is
-// compiler-visible so that the hazard recognizer sees it (nrc_t16.h).
-typedef unsigned short u2h __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t gate_pk(uint32_t d, uint32_t m) {
-    uint32_t mask;
-    asm("v_pk_min_u16 %0, %1, %2" : "=v"(mask) : "v"(m), "s"(0x00010001u));
-    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2h, mask) * __builtin_bit_cast(u2h, d));
-}
-
-// the same rows as a delta, gated by the forward activation (B-operand form, same rows)
-__device__ __forceinline__ h8 gate_b(const f4& lo, const f4& hi, const h8& a) {
-    const u4 m = __builtin_bit_cast(u4, a);
-    const u4 w = {gate_pk(pk2(lo[0], lo[1]), m.x), gate_pk(pk2(lo[2], lo[3]), m.y), gate_pk(pk2(hi[0], hi[1]), m.z),
-                  gate_pk(pk2(hi[2], hi[3]), m.w)};
-    return __builtin_bit_cast(h8, w);
-}
-
-// B-operand rows of a 64-row operand (2 k-steps) -> its image row: k-step s elements 4h .. 4h + 3 are quad
-// 8s + 4h + g, at the lane's precomputed offsets wo[2s + h] (row_offsets)
-__device__ __forceinline__ void put_rows64(char* img, const int (&wo)[4], const h8 (&v)[2]) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const u4 w = __builtin_bit_cast(u4, v[s]);
-        *(u2*)(img + wo[2 * s]) = u2{w.x, w.y};
-        *(u2*)(img + wo[2 * s + 1]) = u2{w.z, w.w};
-    }
-}
-__device__ __forceinline__ void row_offsets(int r, int g, int (&wo)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) wo[k] = off64(r, 8 * (k >> 1) + 4 * (k & 1) + g);
-}
-
 // dW tiles into the block's slab as f16 (t16_slab_pos: column pairs, one 16-byte store per lane for both tiles of a
 // pair). The slab stores cost the wave a few tens of cycles per store instruction (the CU's stores queue behind one
 // another), so the count of store instructions sets their price: f32 tiles, one dwordx4 each, cost ~600 cycles per
 // backward step (ablation NRC_T16_ABL=1). f16 pairs halve the instructions; rounding a 128-sample partial to f16 adds
 // 2e-5 .. 7e-5 rel-L2 to the summed gradient (oracle partials over 64 training steps) -- tcnn's own
 // gradient is f16.
-__device__ __forceinline__ u4 pack_pair(const f4& e, const f4& o) {
-    return u4{pk2(e[0], e[1]), pk2(e[2], e[3]), pk2(o[0], o[1]), pk2(o[2], o[3])};
-}
 __device__ __forceinline__ void slab_pair(_Float16* __restrict__ slab, int L, int tm, int tn_even, int lane, const u4& v) {
     __builtin_nontemporal_store(v, (u4*)(slab + t16_slab_base(L, tm, tn_even)) + lane);
 }
 __device__ __forceinline__ void slab_single(_Float16* __restrict__ slab, int L, int tm, int tn, int lane, const f4& v) {
     __builtin_nontemporal_store(u2{pk2(v[0], v[1]), pk2(v[2], v[3])}, (u2*)(slab + t16_slab_pos(L, tm, tn, lane, 0)));
-}
-
-// The same stores as raw buffer stores with an explicit cache policy AUX (gfx950 cpol bits: 1 sc0, 2 nt, 16 sc1):
-// the role-split kernel's slab stores (A/B of the policy, NRC_T16_SLAB_AUX)
-template <int AUX>
-__device__ __forceinline__ void slab_pair_b(_Float16* __restrict__ slab, int L, int tm, int tn_even, int lane, const u4& v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, buffer_rsrc(slab, slab_floats(0) * 2),
-                                           t16_slab_base(L, tm, tn_even) * 2 + lane * 16, 0, AUX);
-}
-template <int AUX>
-__device__ __forceinline__ void slab_single_b(_Float16* __restrict__ slab, int L, int tm, int tn, int lane, const f4& v) {
-    const u2 w = {pk2(v[0], v[1]), pk2(v[2], v[3])};
-    __builtin_amdgcn_raw_buffer_store_b64(w, buffer_rsrc(slab, slab_floats(0) * 2), t16_slab_pos(L, tm, tn, lane, 0) * 2,
-                                          0, AUX);
-}
-
-// DPP sum over a 16-lane row (row_ror 8, 4, 2, 1): every lane of the row ends with the row's total
-__device__ __forceinline__ float row_sum16(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
-    return v;
 }
 
 // Transposed-read operand of one 16-feature tile over the block's 128 samples (4 k-steps of 32): the lane's byte
@@ -185,25 +92,9 @@ __device__ __forceinline__ void load_wt(const h8* lwb, int lane, h8 (&W)[4][2]) 
         for (int s = 0; s < 2; ++s) W[mb][s] = lwb[t16_bwd_frag(L, mb, s) * 64 + lane];
 }
 
-// delta_{L-1} = (W_L^T delta_L) * [a_{L-1} > 0] for both 16-sample groups of the wave
-__device__ __forceinline__ void chain2(const h8 (&W)[4][2], const h8 (&d)[2][2], const h8 (&a)[2][2], h8 (&dn)[2][2]) {
-    f4 cc[2][4];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            cc[u][mb] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < 2; ++s) cc[u][mb] = mfma16(W[mb][s], d[u][s], cc[u][mb]);
-        }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) dn[u][s] = gate_b(cc[u][2 * s], cc[u][2 * s + 1], a[u][s]);
-}
-
 constexpr int kWaves = 4;  // 4 waves x 2 groups x 16 samples = 128 samples per block
 
+#if NRC_DEBUG_KERNELS  // the 4-wave kernel (round 2, before the role split) and its stamped build
 // ABL (diagnostic builds, NRC_T16_ABL): 1 drops the slab stores at compile time, which also drops the dW tiles (dead
 // code); 2 keeps the dW tiles and skips only the stores. The product instantiation is ABL = 0.
 template <bool STAMP, int ABL = 0>
@@ -587,6 +478,8 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
     stamp();
 }
 
+#endif
+
 // Role-split variant (NRC_T16_SPLIT, A/B): 8 waves per block, 2 per SIMD. Waves 0..3 ("chain") do what
 // train16_kernel's waves do except the weight gradients: encode, forward, loss, then per backward step the delta chain
 // (W_L^T delta_L, ReLU gate) and the image writes. Waves 4..7 ("dW") sit through the forward at its barriers and then,
@@ -872,7 +765,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
                 }                                                                                                  \
             }                                                                                                      \
         }                                                                                                          \
-        chain2(W, d, a[L - 1], dn);                                                                                \
+        chain_groups<2>(W, d, a[L - 1], dn);                                                                                \
         if constexpr (L > 1) load_wt<(L > 1 ? L - 1 : 1)>(lwb, lane, W);                                           \
         _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
             put_rows64(NIMGD, wo[u], dn[u]);                                                                       \
@@ -895,41 +788,28 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
                           hipStream_t s, bool split) {
     if (b <= 0) return hipSuccess;
-    static const int abl = [] {
-        const char* e = std::getenv("NRC_T16_ABL");
-        return e ? std::atoi(e) : 0;
-    }();
-    const dim3 grid(t16_blocks(b)), block(64 * kWaves);
+    const dim3 grid(t16_blocks(b));
     const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
     if (split && !stamps) {
-        // NRC_T16_SLAB_AUX (read per launch, A/B of the slab stores' cache policy, tools/ab_slab_aux.py): 16 sc1
-        // (default), 2 nt, 18 sc1 nt. sc1 stores write through and drop the line from the XCD's L2, so the kernel
-        // does not end with 5.9 MB of dirty slab lines to write back, and the reduce (on every XCD) reads them from
-        // memory either way: fused step 14.2 -> 12.7 us, gradients bitwise equal (profiles/r02_train/)
-        const char* e = std::getenv("NRC_T16_SLAB_AUX");
-        const int aux = e ? std::atoi(e) : 16;
-        if (aux == 16)
-            hipLaunchKernelGGL(train16_split_kernel<16>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
-                               loss_scale, f, bw, slabs, loss_partials);
-        else if (aux == 18)
-            hipLaunchKernelGGL(train16_split_kernel<18>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
-                               loss_scale, f, bw, slabs, loss_partials);
-        else
-            hipLaunchKernelGGL(train16_split_kernel<2>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
-                               loss_scale, f, bw, slabs, loss_partials);
+        // slab stores as sc1 (AUX 16): they write through and drop the line from the XCD's L2, so the kernel does not end
+        // with 5.9 MB of dirty slab lines to write back, and the reduce (on every XCD) reads them from memory either
+        // way: fused step 14.2 -> 12.7 us against nt, gradients bitwise equal (profiles/r02_train/)
+        hipLaunchKernelGGL(train16_split_kernel<16>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
+                           loss_scale, f, bw, slabs, loss_partials);
         return hipGetLastError();
     }
-    if (stamps) {
-        switch (abl) {
-            case 1: hipLaunchKernelGGL((train16_kernel<true, 1>), grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, stamps); break;
-            case 2: hipLaunchKernelGGL((train16_kernel<true, 2>), grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, stamps); break;
-            default: hipLaunchKernelGGL((train16_kernel<true, 0>), grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, stamps);
-        }
-    } else {
+#if NRC_DEBUG_KERNELS
+    const dim3 block(64 * kWaves);
+    if (stamps)
+        hipLaunchKernelGGL((train16_kernel<true, 0>), grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw,
+                           slabs, loss_partials, stamps);
+    else
         hipLaunchKernelGGL((train16_kernel<false, 0>), grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw,
                            slabs, loss_partials, nullptr);
-    }
     return hipGetLastError();
+#else
+    return hipErrorNotSupported;  // the 4-wave kernel and the stamped builds live in libnrc_amd_debug.so
+#endif
 }
 
 }  // namespace nrc_amd

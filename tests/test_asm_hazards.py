@@ -20,6 +20,7 @@ import asm_hazard_check  # noqa: E402
 HIPCC = "/opt/rocm/bin/hipcc"
 # (source, extra flags) as the Makefile builds them
 UNITS = [("nrc_kernels.hip", []), ("nrc_train16.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form"]),
+         ("nrc_train_dc.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form"]),
          ("nrc_infer16.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form"])]
 
 

@@ -138,13 +138,15 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_two_ranks_on_one_gpu_gloo(tmp_path, nrc, torch, dev, golden):
-    """tools/dp_rank_worker.py x 2 (gloo, both on cuda:0): bit-identical replicas, equal to nrc_train on the full
-    minibatches within the summation-order tolerance."""
+@pytest.mark.parametrize("B", [16384, 4096])
+def test_two_ranks_on_one_gpu_gloo(tmp_path, nrc, torch, dev, golden, B):
+    """tools/dp_rank_worker.py x 2 (gloo, both on cuda:0): bit-identical replicas, equal to the single-process step
+    on the full minibatches within the summation-order tolerance. B = 4,096: each rank trains configs[3]'s per-rank
+    slice of 2,048 samples (the small-block shape of the decoupled-chain kernel)."""
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
     np.save(tmp_path / "params.npy", golden["params_b"])
-    procs = [subprocess.Popen([sys.executable, str(ROOT / "tools" / "dp_rank_worker.py"), str(tmp_path)],
+    procs = [subprocess.Popen([sys.executable, str(ROOT / "tools" / "dp_rank_worker.py"), str(tmp_path), str(B)],
                               env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(2)]
     logs = [p.communicate(timeout=240)[0] for p in procs]
@@ -155,8 +157,8 @@ def test_two_ranks_on_one_gpu_gloo(tmp_path, nrc, torch, dev, golden):
     ref.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
     ref_losses = []
     for it in range(steps):
-        q_np, t_np = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=80 + it)
-        ref_losses.append(ref.train(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np), loss=True))
+        q_np, t_np = nrc.synthetic.cornell_batch(B, seed=80 + it)
+        ref_losses.append(ref.train_batch(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np), B, loss=True))
     for slot in ("params", "infer"):
         a, b = np.load(tmp_path / f"{slot}_0.npy"), np.load(tmp_path / f"{slot}_1.npy")
         np.testing.assert_array_equal(a, b)

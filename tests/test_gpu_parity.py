@@ -90,7 +90,10 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
 @pytest.mark.parametrize("variant", [0, 23, 30, 39, 40])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every kernel variant kept for A/B at sizes
-    that exercise partial tiles / single blocks."""
+    that exercise partial tiles / single blocks. The product library holds variant 39 only; the A/B variants are
+    checked when the debug library is loaded (tests/test_gpu_debug_lib.py runs this test under it)."""
+    if variant != 39 and not nrc._lib.is_debug_library():
+        pytest.skip("A/B variant of the debug library (libnrc_amd_debug.so)")
     net.set_state(nrc.StateSlot.INFER, golden["params_b"])
     L = nrc._lib.lib()
     for n in [1, 33, 1000, 70001]:

@@ -1,0 +1,112 @@
+"""The decoupled-chain training kernel (nrc_train_dc.hip, round 3) and configs[3]'s per-rank training work.
+
+* At 128 samples per block (shape 3) it computes bitwise the slabs, hence the gradient, of round 2's role-split t16
+  kernel (same MFMA sequence per accumulator, same tile k order, same f16 slab rounding) — full and ragged batches.
+* Every shape (16 / 32 / 64 / 128 samples per block) against the oracle (ORC_MIXED) within the gradient tolerance of
+  tests/test_gpu_parity.py (rel-L2 <= 2e-3), including the C4 per-rank case: 2,048 samples normalised by a global
+  minibatch of 16,384 (Device.cpp:1503-1509 split over 8 ranks), odd and tiny batches.
+* nrc_train_dp at b_local = 2,048, global_b = 16,384 on a world-1 RCCL communicator equals nrc_train_grad +
+  nrc_train_apply bitwise, and the Adam step it applies is the oracle's from the globally normalised gradient.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as _t
+
+    return _t
+
+
+def to_dev(torch, dev, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.fixture()
+def knobs(nrc):
+    yield nrc._lib
+    nrc._lib.set_knob("train_kernel", -1)
+    nrc._lib.set_knob("train_shape", -1)
+
+
+def make_net(nrc, torch, params):
+    n = nrc.Network()
+    n.init(stream=torch.cuda.current_stream())
+    n.set_state(nrc.StateSlot.PARAMS, params)
+    return n
+
+
+def grad_of(nrc, torch, dev, net, q_np, t_np, b, global_b):
+    g = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
+    net.train_grad(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np), b, global_b, g)
+    torch.cuda.synchronize()
+    return g.cpu().numpy()
+
+
+@pytest.mark.parametrize("b", [16384, 5000])
+def test_dc_128_is_bitwise_round2_split(nrc, torch, dev, golden, knobs, b):
+    q_np, t_np = nrc.synthetic.cornell_batch(b, seed=1200 + b)
+    knobs.set_knob("train_kernel", 1)
+    ref = make_net(nrc, torch, golden["params_b"])
+    knobs.set_knob("train_kernel", -1)
+    knobs.set_knob("train_shape", 3)
+    dc = make_net(nrc, torch, golden["params_b"])
+    g_ref = grad_of(nrc, torch, dev, ref, q_np, t_np, b, b)
+    g_dc = grad_of(nrc, torch, dev, dc, q_np, t_np, b, b)
+    np.testing.assert_array_equal(g_dc, g_ref)
+    ref.destroy()
+    dc.destroy()
+
+
+@pytest.mark.parametrize("shape", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("b,global_b", [(2048, 16384), (1, 16384), (17, 17), (3001, 3001)])
+def test_dc_shapes_match_oracle(nrc, orc, torch, dev, golden, knobs, shape, b, global_b):
+    knobs.set_knob("train_shape", shape)
+    net = make_net(nrc, torch, golden["params_b"])
+    q_np, t_np = nrc.synthetic.cornell_batch(b, seed=1300 + b)
+    g = grad_of(nrc, torch, dev, net, q_np, t_np, b, global_b)
+    g_ref, loss_ref = orc.grad(golden["params_b"], q_np, t_np, mode=orc.MIXED)
+    scale = b / global_b  # the oracle normalises by its own batch
+    r = rel(g[:nrc.NUM_PARAMS], g_ref * scale)
+    print(f"shape {shape} b={b} global_b={global_b}: grad rel {r:.2e}")
+    assert r <= 2e-3
+    assert abs(g[nrc.NUM_PARAMS] - loss_ref * scale) <= 1e-3 * abs(loss_ref * scale) + 1e-30
+    assert (g[21504:22528].reshape(16, 64)[3:] == 0).all()  # padded output rows get no gradient
+    net.destroy()
+
+
+def test_c4_rank_slice_train_dp(nrc, orc, torch, dev, golden):
+    """configs[3] per-rank step on one GPU: 2,048 samples of a 16,384-sample global minibatch through nrc_train_dp
+    (world-1 RCCL communicator) == nrc_train_grad + nrc_train_apply, and tracks the oracle's Adam/EMA step."""
+    B, b = nrc.BATCH_SIZE, nrc.BATCH_SIZE // 8
+    comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
+    a = make_net(nrc, torch, golden["params_b"])
+    c = make_net(nrc, torch, golden["params_b"])
+    a.set_comm(comm)
+    st = orc.AdamEmaState(golden["params_b"])
+    for it in range(3):
+        q_np, t_np = nrc.synthetic.cornell_batch(b, seed=1400 + it)
+        q, t = to_dev(torch, dev, q_np), to_dev(torch, dev, t_np)
+        la = a.train_dp(q, t, b, B, loss=True)
+        g = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
+        c.train_grad(q, t, b, B, g)
+        lc = c.train_apply(g, loss=True)
+        assert la == lc
+        g_ref, _ = orc.grad(st.params, q_np, t_np, mode=orc.MIXED)
+        st.apply(g_ref * (b / B))
+    for slot in nrc.StateSlot:
+        np.testing.assert_array_equal(a.get_state(slot), c.get_state(slot))
+    assert rel(a.get_state(nrc.StateSlot.PARAMS), st.params) <= 1e-3
+    a.set_comm(None)
+    a.destroy()
+    c.destroy()
+    comm.destroy()

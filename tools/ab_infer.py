@@ -1,7 +1,9 @@
 """In-process A/B timing of the inference kernel variants (interleaved rounds, one process, one device;
 cdna_hip_programming.md §5.4 rule 24). Also checks every variant against the oracle on a sample.
 
-    python tools/ab_infer.py [--n 2097152] [--rounds 7] [--iters 20] [--variants 0,1,2]
+    NRC_LIB_PATH=neural-radiance-caching_amd/libnrc_amd_debug.so python tools/ab_infer.py [--variants 23,30,39]
+
+The A/B variants other than the product's 39 live in the debug library (libnrc_amd_debug.so).
 """
 from __future__ import annotations
 
@@ -40,9 +42,6 @@ def main() -> None:
     stream = torch.cuda.current_stream()
     sp = int(stream.cuda_stream)
     variants = [int(v) for v in args.variants.split(",")]
-    if 50 in variants or 51 in variants:  # the 16x16x32 kernel reads the t16 inference image (debug only)
-        import os
-        os.environ["NRC_DEBUG_INFER16"] = "1"
 
     net = nrc.Network()
     net.init(stream=stream)

@@ -1,7 +1,9 @@
 """One rank of tests/test_gpu_dp.py::test_two_ranks_on_one_gpu_gloo: torch.distributed over gloo, the real HIP
 nrc_train_grad / nrc_train_apply through nrc_amd.dp.DataParallelTrainer, every rank on cuda:0.
 
-    RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tools/dp_rank_worker.py <out_dir>
+    RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tools/dp_rank_worker.py <out_dir> [global_batch]
+
+global_batch (default 16,384) is split over the ranks; 4,096 gives configs[3]'s per-rank slice of 2,048 samples.
 """
 import os
 import sys
@@ -19,6 +21,7 @@ def main() -> None:
     import torch.distributed as dist
 
     out = Path(sys.argv[1])
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     nrc = nrc_loader.load()
@@ -32,11 +35,11 @@ def main() -> None:
     trainer.broadcast_state(net, dev)
     losses = []
     for it in range(3):
-        q, t = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE, seed=80 + it)
-        s, c = nrc.dp.shard_range(nrc.BATCH_SIZE, rank, world)
+        q, t = nrc.synthetic.cornell_batch(B, seed=80 + it)
+        s, c = nrc.dp.shard_range(B, rank, world)
         qd = torch.from_numpy(np.ascontiguousarray(q[s:s + c])).to(dev)
         td = torch.from_numpy(np.ascontiguousarray(t[s:s + c])).to(dev)
-        losses.append(trainer.step(qd, td, c, nrc.BATCH_SIZE, loss=True))
+        losses.append(trainer.step(qd, td, c, B, loss=True))
     torch.cuda.synchronize()
     np.save(out / f"params_{rank}.npy", net.get_state(nrc.StateSlot.PARAMS))
     np.save(out / f"infer_{rank}.npy", net.get_state(nrc.StateSlot.INFER))
