@@ -176,24 +176,25 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
  * the production choice. */
 nrc_status nrc_debug_set_knob(const char* name, int value);
 nrc_status nrc_debug_get_knob(const char* name, int* value);
-/* Inference through a specific kernel variant (0..25, see nrc_kernels.hip) for in-process A/B timing;
- * results are identical in meaning to nrc_infer_stream. */
+/* Inference through a specific kernel variant for in-process A/B timing; results are identical in meaning to
+ * nrc_infer_stream. The product library has variant 39 (the production kernel) only; the debug library
+ * (libnrc_amd_debug.so) also has 0, 23, 30, 40 (39 + in-kernel clock) and 50 / 51 (the 16x16x32 kernel). */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
                                    hipStream_t stream);
-/* Diagnostic: after a launch of a clocked inference variant (31, 32, 34, 36, 38), per wave 6 uint64: s_memtime cycles
+/* Diagnostic (debug library): after a launch of the clocked inference variant 40, per wave 6 uint64: s_memtime cycles
  * of its persistent loop, s_memrealtime (100 MHz) at loop start, at loop end and at wave start, HW_ID, XCC_ID:
  * 6 * *waves values into host_dst (at most cap_waves waves). */
 nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, uint32_t* waves);
-/* Diagnostic: the training fwd/bwd kernel with s_memtime phase stamps written to stamps_d: 16 uint64 per wave,
- * [block][wave 0..3][16] for the Frequency kernel (nrc_train16.hip; size 64 * ceil(b / 128)), [block][16] under
- * NRC_TRAIN_KERNEL=32; performs no optimizer step. */
+/* Diagnostic (debug library): the training fwd/bwd kernel with s_memtime phase stamps written to stamps_d: 16 uint64
+ * per wave, [block][wave][16]: the decoupled-chain kernel for b <= 4096 (nrc_train_dc.hip, dc_waves_per_block waves
+ * per block), else the 4-wave t16 kernel [block][4][16]; performs no optimizer step. */
 nrc_status nrc_debug_train_stamps(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
                                   uint64_t* stamps_d);
 /* Diagnostic (InputEncoding::Hash): the inputs of the last training call's grid-gradient scatter, copied on the
  * handle's stream into device buffers: pos_d [b][4] floats (position, 0), dy_d [16 levels][b] packed f16 pairs
  * (dL/d feature 0, 1 of that level, loss-scaled). b <= the last call's sample count. */
 nrc_status nrc_debug_hash_scatter_inputs(nrc_net* net, float* pos_d, uint32_t* dy_d, uint32_t b);
-/* Diagnostic: the default inference kernel with s_memtime phase stamps; per wave of its persistent grid, 8 uint64
+/* Diagnostic (debug library): the round-1 inference kernel with s_memtime phase stamps; per wave of its grid, 8 uint64
  * cycle sums (encode + prefetch, layers 0..4, output layer, epilogue) go to stamps_d, which must hold
  * 8 * NRC_INFER_STAMP_WAVES_MAX entries; *waves_h receives the number of waves written. */
 #define NRC_INFER_STAMP_WAVES_MAX 8192

@@ -3,7 +3,7 @@ across the frame match the oracle row by row.
 
 Why (round 2): the round-1 Hash inference kernel shape (fixed tiles per wave) returned garbage for ~0.25 % of the
 rows of a 2^21-query launch, whole 32-query tiles at a time and different tiles in every launch
-(tools/hash_diff_probe.py); the parity tests at n <= 70,001 allow 0.1 % of queries beyond their per-query bound, and
+(round 3 bisect: profiles/r03_hash/); the parity tests at n <= 70,001 allow 0.1 % of queries beyond their per-query bound, and
 two corrupted tiles fit inside that. This test has no such allowance: a tile either matches or fails.
 """
 from __future__ import annotations
@@ -116,10 +116,25 @@ def test_wide_infer_full_frame_deterministic(nrc, orc, dev, precision):
     try:
         n = N
         q = _t(nrc.synthetic.cornell_queries(n, seed=33), dev)
+        q_np = nrc.synthetic.cornell_queries(n, seed=33)
         fn = lambda qq, o, nn: net.infer_precision(precision, qq, o, nn)  # noqa: E731
         a, b = _run_twice(net, q, n, dev, fn)
         assert np.array_equal(a, b), f"{int((a != b).any(axis=1).sum())} rows differ between two launches"
         assert np.isfinite(a).all() and (a != 777.0).all()
+        # sampled whole tiles against the width-128 oracle (the round-1 Hash shape's corrupted tiles hid
+        # below the n <= 70k parity tests; this path now gets the same full-frame tile check)
+        rows = _sample_rows(n)
+        params = net.get_state(nrc.StateSlot.INFER)
+        y = orc.wide_forward(params, q_np[rows], orc.FP8 if precision else orc.MIXED)
+        if precision == 0:
+            _check_rows(a[rows], y, 0.02)
+        else:
+            # FP8: e4m3 rounding-boundary cascades move single rows (tests/test_gpu_wide.py: 98 % within 2^-10, rel-L2
+            # <= 3e-2); a corrupted tile is off in most of its rows, so its median row error is the test
+            scale = np.maximum(np.abs(y).max(axis=1), 0.05)
+            err = (np.abs(a[rows] - y).max(axis=1) / scale).reshape(-1, 32)
+            assert np.median(err, axis=1).max() <= 0.1, f"tile median error {np.median(err, axis=1).max():.3g}"
+            assert float(np.linalg.norm(a[rows] - y) / np.linalg.norm(y)) <= 3e-2
     finally:
         net.destroy()
 
