@@ -308,15 +308,16 @@ struct nrc_net {
     float* loss_partials = nullptr;
     // minibatch-loss slots: host-mapped fine-grained (coherent) pinned memory written directly by the reduce/Adam
     // kernels, so reading a loss back costs one stream sync and no D2H copy launch (the copy was ~4.5 us)
-    uint32_t* work_queue = nullptr;  // inference work-queue counters {next tile, finished waves}; zero between launches
+    uint32_t* work_queue = nullptr;  // inference work-pool counters (two sets, launch parity pool_parity)
+    int pool_parity = 0;
     ncclComm_t comm = nullptr;       // attached RCCL communicator (not owned), nrc_set_comm
     int comm_rank = 0, comm_world = 1;
     float* dp_grad = nullptr;        // [grad_floats] gradient exchange buffer of nrc_train_dp
     float* loss_dev = nullptr;   // device view of loss_host
     float* loss_host = nullptr;
     void alloc_loss_slots() {
-        HIP_CHECK(hipMalloc(&work_queue, 256));
-        HIP_CHECK(hipMemset(work_queue, 0, 256));
+        HIP_CHECK(hipMalloc(&work_queue, kInferPoolBytes));
+        HIP_CHECK(hipMemset(work_queue, 0, kInferPoolBytes));
         HIP_CHECK(hipHostMalloc(&loss_host, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_CHECK(hipHostGetDevicePointer((void**)&loss_dev, loss_host, 0));
         for (int i = 0; i < 4; ++i) loss_host[i] = 0.0f;
@@ -572,7 +573,7 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
         return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
         return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
-    return launch_infer(in, out, n, net->wf_infer, net->stream);
+    return launch_infer(in, out, n, net->wf_infer, net->stream, net->work_queue, &net->pool_parity);
 }
 
 void require_frequency(const nrc_net* net, const char* what) {
@@ -1194,7 +1195,8 @@ nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* in, f
             return;
         }
 #endif
-        const hipError_t e = launch_infer_variant(variant, in, out, n, net->wf_infer, stream);
+        const hipError_t e = launch_infer_variant(variant, in, out, n, net->wf_infer, stream, net->work_queue,
+                                                  &net->pool_parity);
         if (e == hipErrorInvalidValue && variant != kProductInferVariant)
             throw ApiError(NRC_ERR_UNSUPPORTED, "inference variant " + std::to_string(variant) +
                                                     " is an A/B kernel of the debug library (libnrc_amd_debug.so via "

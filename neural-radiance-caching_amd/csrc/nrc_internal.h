@@ -179,12 +179,16 @@ hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const flo
 hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s);
 
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
-hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s);
+// pools / parity: the handle's work-pool counters (kInferPoolBytes, zeroed at allocation) and its launch parity, which
+// the pooled variants flip (see ABL & 16384 in nrc_kernels.hip); variants that do not pool ignore both
+constexpr int kInferPoolBytes = 2 * 32 * 32 * 4;
+hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s,
+                        uint32_t* pools = nullptr, int* parity = nullptr);
 // the product kernel is variant 39; the debug library (NRC_DEBUG_KERNELS) also has the A/B variants 0, 23, 30 and 40
 // (39 + in-kernel clock)
 constexpr int kProductInferVariant = 39;
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
-                                hipStream_t s);
+                                hipStream_t s, uint32_t* pools = nullptr, int* parity = nullptr);
 constexpr int kNumInferVariants = 52;  // 50: launch_infer16 (the t16 image)
 // Frequency inference on v_mfma_f32_16x16x32_f16 (nrc_infer16.hip) from the t16-layout inference image
 hipError_t launch_infer16(const float* queries, float* out, int64_t n, const _Float16* wf16, hipStream_t s);

@@ -712,8 +712,13 @@ struct InferEpilogue {
     int64_t n_acc;
     float w;           // 1 / (iterationIndex + 1)
     uint64_t* stamps = nullptr;  // diagnostic build only (ABL & 256): per-wave phase cycle sums
-    uint32_t* wq = nullptr;      // ABL & 4096: the handle's work-queue counters {next tile, finished waves}, zero at launch
+    uint32_t* wq = nullptr;      // ABL & 16384: the handle's work-pool counters (kPoolSets sets of kPools)
+    int parity = 0;              // ABL & 16384: this launch's counter set; it zeroes the other one for the next launch
 };
+// ABL & 16384: the launch's tiles split into kPools contiguous pools, each a device-scope atomic counter; a block starts
+// on pool blockIdx % kPools and, once that pool is dry, steals from the others (a per-block LDS mask of the pools seen
+// dry keeps the walk short). Counters are 128 B apart; two sets alternate between launches on the stream.
+constexpr int kPools = 32, kPoolStride = 32, kPoolSetWords = kPools * kPoolStride;
 
 
 // ENC: 0 = Frequency composite (80-wide input), 1 = Hash composite (64-wide; grid = f16x2 table),
@@ -733,9 +738,16 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     // tiles at 36 us and the last at 82 us, the SIMDs running the tail at 1-2 waves. The block takes a contiguous
     // range of tiles and its waves draw the next tile from an LDS counter, so every SIMD stays loaded to the end.
     __shared__ uint32_t wq_next;
+    __shared__ uint32_t pool_dry;
     if constexpr ((ABL & 16) != 0) fp32_flush_output_denorms();
     if constexpr ((ABL & 2048) != 0) {
         if (threadIdx.x == 0) wq_next = 0;
+    }
+    if constexpr ((ABL & 16384) != 0) {
+        if (threadIdx.x == 0) pool_dry = 0;
+        // block 0 zeroes the other counter set: the launch before this one (same stream) used it and has completed
+        if (blockIdx.x == 0 && threadIdx.x < kPools)
+            epi.wq[(1 - epi.parity) * kPoolSetWords + threadIdx.x * kPoolStride] = 0u;
     }
     copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
@@ -776,6 +788,41 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         g = draw();
     }
     if constexpr ((ABL & 4096) != 0) g = draw();
+    // ABL & 16384: pooled draws (see kPools)
+    [[maybe_unused]] int cur = blockIdx.x % kPools;
+    [[maybe_unused]] uint32_t* const pools = epi.wq + epi.parity * kPoolSetWords;
+    auto pool_begin = [&](int k) -> int64_t { return (int64_t)k * ngroups_all / kPools; };
+    auto pool_issue = [&](int k) -> uint32_t {
+        uint32_t t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(pools + k * kPoolStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    };
+    // the tile of a draw from pool cur that returned t (wave-uniform); a dry pool sends the wave to the next pool not
+    // yet seen dry by its block (blocking draws; only at pool transitions); ngroups_all = nothing left anywhere
+    auto pool_resolve = [&](uint32_t t) -> int64_t {
+        int64_t idx = pool_begin(cur) + (int64_t)t;
+        if (idx < pool_begin(cur + 1)) return idx;
+        for (;;) {
+            if (lane == 0) atomicOr(&pool_dry, 1u << cur);
+            uint32_t m = 0;
+            if (lane == 0) m = __hip_atomic_load(&pool_dry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            m = __builtin_amdgcn_readfirstlane(m);
+            if (m == 0xFFFFFFFFu) return ngroups_all;
+            const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const uint32_t rot = (uint32_t)((cur + 1 + wv) % kPools);
+            const uint32_t free_rot = ~((m >> rot) | (m << ((32u - rot) & 31u)));  // bit i: pool (rot + i) % 32 free
+            cur = (int)((rot + (uint32_t)__builtin_ctz(free_rot)) % kPools);
+            uint32_t traw = pool_issue(cur), tt;
+            asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(tt) : "v"(traw));
+            idx = pool_begin(cur) + (int64_t)tt;
+            if (idx < pool_begin(cur + 1)) return idx;
+        }
+    };
+    if constexpr ((ABL & 16384) != 0) {
+        uint32_t traw = pool_issue(cur), tt;
+        asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(tt) : "v"(traw));
+        g = pool_resolve(tt);
+    }
     if (g >= ngroups) {
         finish();
         return;
@@ -820,13 +867,19 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     int64_t ng = 0;
     uint32_t nn_raw = 0;  // the pending draw: lane 0's atomic result, read (readfirstlane) one iteration later
     if constexpr ((ABL & (2048 | 4096)) != 0) ng = draw();
+    if constexpr ((ABL & 16384) != 0) {
+        uint32_t traw = pool_issue(cur), tt;
+        asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(tt) : "v"(traw));
+        ng = pool_resolve(tt);
+    }
     for (int64_t nn = 0; g < ngroups; g = ng, ng = nn) {
-        if constexpr ((ABL & (2048 | 4096)) != 0) {
+        if constexpr ((ABL & (2048 | 4096 | 16384)) != 0) {
             if (!first_iter) {
                 // an asm readfirstlane stays here; the builtin is hoisted to the atomic and the wave then waits for it
                 uint32_t t;
                 asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(t) : "v"(nn_raw));
-                ng = gbase + (int64_t)t;
+                if constexpr ((ABL & 16384) != 0) ng = pool_resolve(t);
+                else ng = gbase + (int64_t)t;
             }
         }
         if constexpr ((ABL & 256) != 0) {  // the previous iteration's epilogue (stores, loop overhead)
@@ -853,7 +906,10 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
                 encode_fast<(ABL & 16) != 0>(Q[t], h, x[t]);
             }
         }
-        if constexpr ((ABL & (2048 | 4096)) != 0) {
+        if constexpr ((ABL & 16384) != 0) {
+            nn_raw = ng < ngroups_all ? pool_issue(cur) : 0u;  // wave-uniform condition: no draw once everything is dry
+            first_iter = false;
+        } else if constexpr ((ABL & (2048 | 4096)) != 0) {
             if constexpr ((ABL & 4096) != 0) {
                 // every lane issues the buffer atomic; the descriptor covers lane 0's counter only, the other lanes'
                 // adds are dropped by the hardware (no branch around the atomic)
@@ -1058,6 +1114,14 @@ __global__ __launch_bounds__(THREADS, WAVES_PER_EU) void infer_kernel_v2(const f
 }
 
 #if NRC_DEBUG_KERNELS
+// variant 41 (A/B, rejected: 89.3 vs 81.0 us): variant 39's body with pooled cross-CU draws
+// (ABL & 16384) instead of the per-block LDS queue
+template <int ABL>
+__global__ __launch_bounds__(1024, 4) void infer_pooled_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                              int64_t n, const h8* __restrict__ wf, InferEpilogue epi) {
+    infer_v2_body<1, 1024, false, ABL, -1>(q, out, n, wf, epi);
+}
+
 // Diagnostic build of the default inference kernel (variant 23) with per-wave phase stamps (ABL & 256).
 __global__ __launch_bounds__(512, 4) void infer_stamp_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                              int64_t n, const h8* __restrict__ wf,
@@ -2570,10 +2634,21 @@ hipError_t read_infer_clock(uint64_t*, int64_t, int64_t*) { return hipErrorNotSu
 static int g_default_infer_variant = 39;
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
-                                hipStream_t s) {
+                                hipStream_t s, uint32_t* pools, int* parity) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
     static int bpc[kNumInferVariants] = {};
+#if NRC_DEBUG_KERNELS
+    if (variant == 41 || variant == 42) {  // 42: 41 with the in-kernel clock
+        if (!pools || !parity) return hipErrorInvalidValue;
+        InferEpilogue e{};
+        e.wq = pools;
+        e.parity = (*parity ^= 1);  // only pooled launches flip it: the set they skip is the one they zero
+        if (variant == 41)
+            return launch_persistent_infer(infer_pooled_kernel<48 | 1024 | 8192 | 16384>, 1024, bpc[41], ntiles, queries, out, n, wf, s, e);
+        return launch_clocked(infer_pooled_kernel<48 | 1024 | 8192 | 16384 | 512>, 1024, bpc[42], ntiles, queries, out, n, wf, s, e);
+    }
+#endif
     switch (variant) {
         // The kernels kept for in-process A/B (tools/ab_infer.py). The rejected ones of rounds 1-2 (register-resident
         // weights, explicit layer-ahead prefetch, ping-pong tiles, 2-tile waves, SIMD-staggered starts, launch-wide
@@ -2614,8 +2689,9 @@ hipError_t launch_infer_stamped(const float*, float*, int64_t, const _Float16*, 
 }
 #endif
 
-hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s) {
-    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s);
+hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s, uint32_t* pools,
+                        int* parity) {
+    return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, pools, parity);
 }
 
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,

@@ -87,7 +87,7 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40])
+@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40, 41, 42])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every kernel variant kept for A/B at sizes
     that exercise partial tiles / single blocks. The product library holds variant 39 only; the A/B variants are
@@ -390,3 +390,26 @@ def test_cpp_shim_end_to_end(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "replay ok" in r.stdout
+
+
+def test_pooled_variant_bitwise_and_reusable(nrc, torch, dev, net, golden):
+    """Debug library (A/B variant, rejected on speed). Variant 41 (pooled cross-CU tile draws) computes every tile exactly as 39 does, only the tile -> wave mapping
+    differs: outputs are bit-identical. Its two counter sets alternate between launches and each launch zeroes the
+    set it does not use, so back-to-back launches of different sizes, interleaved with non-pooled launches on the
+    same handle, must all see fresh counters (a stale set would skip tiles: the 777 sentinel would survive)."""
+    if not nrc._lib.is_debug_library():
+        pytest.skip("A/B variant of the debug library (libnrc_amd_debug.so)")
+    net.set_state(nrc.StateSlot.INFER, golden["params_b"])
+    L = nrc._lib.lib()
+    sp = int(torch.cuda.current_stream().cuda_stream)
+    sizes = [1 << 21, 31, 1 << 21, 100_003, 1, 1 << 20, 1 << 21]
+    for i, n in enumerate(sizes):
+        q = to_dev(torch, dev, nrc.synthetic.cornell_queries(n, seed=900 + i))
+        a = torch.full((n, 3), 777.0, device=dev)
+        b = torch.full((n, 3), 777.0, device=dev)
+        nrc._lib.check(L.nrc_debug_infer_variant(net._h, 39, q.data_ptr(), a.data_ptr(), n, sp))
+        nrc._lib.check(L.nrc_debug_infer_variant(net._h, 41, q.data_ptr(), b.data_ptr(), n, sp))
+        if i % 2:
+            net.infer(q, b, n)  # the handle's own launch (product default) in between
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), f"n={n}: {int((a != b).any(dim=1).sum())} rows differ"

@@ -19,8 +19,9 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import nrc_loader  # noqa: E402
 
-CLOCKED = {40}
-# 50: the rejected 16x16x32 inference kernel (nrc_infer16.hip)  # variants that record the in-kernel clock (nrc_debug_read_infer_clock)
+# variants that record the in-kernel clock (nrc_debug_read_infer_clock): 40 = 39 clocked, 42 = 41 (pooled) clocked.
+# 50: the rejected 16x16x32 inference kernel (nrc_infer16.hip)
+CLOCKED = {40, 42}
 
 
 def main() -> None:
@@ -110,9 +111,6 @@ def main() -> None:
             se = (c[:, 4].astype(np.int64) >> 13) & 7
             res[v]["end_us_by_xcd_mean_max"] = {int(x): [float(end[xcc == x].mean()), float(end[xcc == x].max())]
                                                 for x in sorted(set(xcc.tolist()))}
-            cu_end = {}
-            for x, e_, c_ in zip(xcc, se, cu):
-                pass
             keys = xcc * 256 + se * 16 + cu
             per_cu = np.array([end[keys == k].max() for k in sorted(set(keys.tolist()))])
             res[v]["cu_last_end_us_p0_10_50_90_100"] = pct(per_cu)
