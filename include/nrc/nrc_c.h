@@ -137,13 +137,28 @@ nrc_status nrc_get_grad_floats(const nrc_net* net, uint64_t* n);
 nrc_status nrc_train_grad(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
                           uint32_t global_b, float* grad_d);
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h);
+/* Hash only: the exact grid exchange (new capability). The grid-table gradient is an exact fixed-point sum per step
+ * (value x 2^24 of tcnn's f16 contributions); nrc_train_grad rounds each rank's sum to f16 before the exchange, so a
+ * world-N step differs from one GPU stepping the whole global minibatch. nrc_train_grad_fixed writes the MLP gradient
+ * and the loss into grad_d as nrc_train_grad does (its grid part is not written) and this rank's exact grid sums into
+ * grid_fixed_d[NRC_HASH_GRID_PARAMS] (int64, device) in an exchange encoding whose integer SUM over at most
+ * NRC_FIXED_MAX_RANKS ranks is the global sum (non-finite contributions included: +inf, -inf, NaN as tcnn's f16 atomics
+ * combine them). Sum grad_d (f32: [0, NRC_HASH_MLP_PARAMS) and the loss at [NRC_HASH_NUM_PARAMS]) and grid_fixed_d
+ * (int64) over ranks, then nrc_train_apply_fixed rounds each global grid sum to f16 once: every rank applies bitwise the
+ * grid gradient a single GPU forms over the global minibatch with the same weights. nrc_train_dp uses this exchange
+ * for Hash networks. */
+#define NRC_FIXED_MAX_RANKS 63
+nrc_status nrc_train_grad_fixed(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b,
+                                uint32_t global_b, float* grad_d, int64_t* grid_fixed_d);
+nrc_status nrc_train_apply_fixed(nrc_net* net, const float* grad_d, const int64_t* grid_fixed_d, float* loss_h);
 
 /* ---- data parallelism inside the library: RCCL over xGMI (new capability) ----
  * The reference's callers are C++ (Device::nrcTrainRadiance, Device.cpp:1503-1509): one process (or thread) per GPU
  * creates an RCCL communicator, attaches it to its handle, and calls nrc_train_dp where it called train(); the
  * gradient exchange then happens inside the library on the handle's stream:
  *     local fwd/bwd of b_local samples, normalised by 3 * global_b (nrc_train_grad)
- *  -> ncclAllReduce(sum) of the NRC_GRAD_FLOATS (Hash: NRC_HASH_GRAD_FLOATS) buffer incl. the loss
+ *  -> ncclAllReduce(sum) of the NRC_GRAD_FLOATS buffer incl. the loss (Hash: the f32 MLP gradient and loss plus
+ *     the int64 exact grid sums of nrc_train_grad_fixed, one RCCL group)
  *  -> the identical Adam + EMA step on every rank (nrc_train_apply), so the replicas stay bit-identical.
  * With world = 1 the step is bitwise the fused nrc_train step. C callers without rccl.h can create the
  * communicator through the nrc_comm_* helpers (one unique id made on rank 0 and shared by any means). */

@@ -21,6 +21,9 @@ NUM_PARAMS = 22528
 GRAD_FLOATS = NUM_PARAMS + 4
 HASH_NUM_PARAMS = 1012736
 HASH_GRAD_FLOATS = HASH_NUM_PARAMS + 4
+HASH_MLP_PARAMS = 21504                              # NRC_HASH_MLP_PARAMS
+HASH_GRID_PARAMS = HASH_NUM_PARAMS - HASH_MLP_PARAMS  # NRC_HASH_GRID_PARAMS: int64 sums of nrc_train_grad_fixed
+FIXED_MAX_RANKS = 63                                 # NRC_FIXED_MAX_RANKS
 WIDE_NUM_PARAMS = 77824  # width-128 network (BASELINE configs[4])
 PRECISION_F16, PRECISION_FP8 = 0, 1
 BATCH_SIZE = 16384
@@ -38,7 +41,7 @@ EXPORTS = [
     "nrc_version", "nrc_last_error", "nrc_default_config", "nrc_create", "nrc_free", "nrc_init", "nrc_destroy",
     "nrc_train", "nrc_train_stream", "nrc_train_batch", "nrc_train_async", "nrc_infer", "nrc_infer_stream", "nrc_set_stream",
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
-    "nrc_train_grad", "nrc_train_apply", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
+    "nrc_train_grad", "nrc_train_apply", "nrc_train_grad_fixed", "nrc_train_apply_fixed", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
     "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_hash_scatter_inputs", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
@@ -109,6 +112,8 @@ def lib() -> ctypes.CDLL:
         "nrc_get_config_json": (st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
         "nrc_train_grad": (st, [vp, fp, fp, u32, u32, fp]),
         "nrc_train_apply": (st, [vp, fp, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_train_grad_fixed": (st, [vp, fp, fp, u32, u32, fp, vp]),
+        "nrc_train_apply_fixed": (st, [vp, fp, vp, ctypes.POINTER(ctypes.c_float)]),
         "nrc_get_state": (st, [vp, ctypes.c_int, fp]),
         "nrc_set_state": (st, [vp, ctypes.c_int, fp]),
         "nrc_get_step": (st, [vp, ctypes.POINTER(u32)]),

@@ -335,6 +335,17 @@ struct nrc_net {
     _Float16 *table_train = nullptr, *table_infer = nullptr;
     HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
     int scatter_blocks = 0;
+    uint8_t* grid_nf = nullptr;       // [n_grid] non-finite contribution codes (GridNonFinite)
+    uint32_t* grid_nf_tag = nullptr;  // tag of the last scatter that recorded one
+    uint32_t nf_seq = 0;              // tag of the current step's scatter
+    GridNonFinite nonfinite() const { return GridNonFinite{grid_nf, grid_nf_tag, nf_seq}; }
+    // the scatter workspace for a new training step (a fresh non-finite tag)
+    const HashScatter* step_scatter(int blocks) {
+        ensure_scatter(blocks);
+        nf_seq = nf_seq + 1u ? nf_seq + 1u : 1u;
+        scatter.nf = nonfinite();
+        return &scatter;
+    }
 
     // width-128 network (BASELINE configs[4]): inference images (f16, FP8 + row scales), training images (f16
     // forward / backward from the master weights) and the training workspace
@@ -363,6 +374,9 @@ struct nrc_net {
         f(dp_grad);
         dp_grad = nullptr;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer);
+        f(grid_nf); f(grid_nf_tag);
+        grid_nf = nullptr;
+        grid_nf_tag = nullptr;
         f(scatter.pos); f(scatter.dy);
         scatter = HashScatter{};
         scatter_blocks = 0;
@@ -404,7 +418,8 @@ struct nrc_net {
     GridBuffers grid_buffers() const {
         GridBuffers g;
         g.params = params + n_mlp; g.m = m + n_mlp; g.v = v + n_mlp; g.ema = ema + n_mlp; g.infer = infer + n_mlp;
-        g.grad64 = grid_grad; g.grad32 = nullptr; g.steps = grid_steps;
+        g.grad64 = grid_grad; g.grad32 = nullptr; g.fixed = nullptr; g.steps = grid_steps;
+        g.nf = nonfinite();
         g.table_train = table_train; g.table_infer = table_infer;
         g.bias = grid_bias; g.bias_len = grid_bias ? kGridBiasLen : 0;
         g.n = n_grid;
@@ -546,7 +561,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     if (net->hash())
         HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                     net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                    net->ensure_scatter(blocks)));
+                                    net->step_scatter(blocks)));
     else
         train_partials(net, in, tgt, b, 3.0f * (float)b);
     net->step += 1;
@@ -758,6 +773,10 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->table_train, sizeof(_Float16) * ng));
             HIP_CHECK(hipMalloc(&net->table_infer, sizeof(_Float16) * ng));
             HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(int64_t) * ng));
+            HIP_CHECK(hipMalloc(&net->grid_nf, ng));
+            HIP_CHECK(hipMemset(net->grid_nf, 0, ng));
+            HIP_CHECK(hipMalloc(&net->grid_nf_tag, sizeof(uint32_t)));
+            HIP_CHECK(hipMemset(net->grid_nf_tag, 0, sizeof(uint32_t)));
             HIP_CHECK(hipMemset(net->grid_steps, 0, sizeof(uint32_t) * ng));
             std::vector<float2> bias(kGridBiasLen + 1, float2{0.0f, 0.0f});
             for (uint32_t st = 1; st <= kGridBiasLen; ++st)
@@ -964,8 +983,14 @@ nrc_status nrc_get_config_json(const nrc_net* net, char* buf, size_t cap, size_t
 }
 
 namespace {
-void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b, float* grad_d);
-void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* loss_d);
+void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b, float* grad_d,
+                   int64_t* grid_fixed = nullptr);
+void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* loss_d,
+                    const int64_t* grid_fixed = nullptr);
+void require_hash(const nrc_net* net, const char* what) {
+    check_live(net);
+    if (!net->hash()) throw ApiError(NRC_ERR_UNSUPPORTED, std::string(what) + ": InputEncoding::Hash only");
+}
 }  // namespace
 
 nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b,
@@ -975,6 +1000,23 @@ nrc_status nrc_train_grad(nrc_net* net, const float* in, const float* tgt, uint3
 
 nrc_status nrc_train_apply(nrc_net* net, const float* grad_d, float* loss_h) {
     return guarded([&] { do_train_apply(net, grad_d, loss_h, nullptr); });
+}
+
+nrc_status nrc_train_grad_fixed(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b,
+                                float* grad_d, int64_t* grid_fixed_d) {
+    return guarded([&] {
+        require_hash(net, "nrc_train_grad_fixed");
+        if (!grid_fixed_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null grid_fixed_d");
+        do_train_grad(net, in, tgt, b, global_b, grad_d, grid_fixed_d);
+    });
+}
+
+nrc_status nrc_train_apply_fixed(nrc_net* net, const float* grad_d, const int64_t* grid_fixed_d, float* loss_h) {
+    return guarded([&] {
+        require_hash(net, "nrc_train_apply_fixed");
+        if (!grid_fixed_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null grid_fixed_d");
+        do_train_apply(net, grad_d, loss_h, nullptr, grid_fixed_d);
+    });
 }
 
 namespace {
@@ -988,6 +1030,24 @@ void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_loc
     check_live(net);
     if (!net->comm) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm)");
     if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
+    if (net->hash()) {
+        // exact grid exchange: each rank's fixed-point sums, exchange-encoded in place in the handle's accumulator,
+        // summed as int64 beside the f32 MLP gradient and loss (one RCCL group on the handle's stream), then rounded
+        // to f16 once by the grid Adam -- every rank applies the sums a single GPU forms over the global minibatch
+        if (net->comm_world > kFixedMaxRanks)
+            throw ApiError(NRC_ERR_UNSUPPORTED, "Hash data parallelism: at most 63 ranks (exchange encoding)");
+        do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad, net->grid_grad);
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        nccl_check(ncclAllReduce(net->dp_grad, net->dp_grad, net->n_mlp, ncclFloat32, ncclSum, net->comm, net->stream),
+                   "ncclAllReduce");
+        nccl_check(ncclAllReduce(net->dp_grad + net->n_total(), net->dp_grad + net->n_total(), 4, ncclFloat32, ncclSum,
+                                 net->comm, net->stream), "ncclAllReduce");
+        nccl_check(ncclAllReduce(net->grid_grad, net->grid_grad, net->n_grid, ncclInt64, ncclSum, net->comm,
+                                 net->stream), "ncclAllReduce");
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        do_train_apply(net, net->dp_grad, loss_h, loss_d, net->grid_grad);
+        return;
+    }
     do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad);
     // one all-reduce of the gradient and the loss partial, on the handle's stream (stream-ordered with the kernels)
     nccl_check(ncclAllReduce(net->dp_grad, net->dp_grad, net->grad_floats(), ncclFloat32, ncclSum, net->comm,
@@ -995,13 +1055,15 @@ void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_loc
     do_train_apply(net, net->dp_grad, loss_h, loss_d);
 }
 
-void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b, float* grad_d) {
+void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, uint32_t global_b, float* grad_d,
+                   int64_t* grid_fixed) {
     {
         check_live(net);
         if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
         if (global_b < b || global_b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
         if (b == 0) {
             HIP_CHECK(hipMemsetAsync(grad_d, 0, sizeof(float) * net->grad_floats(), net->stream));
+            if (grid_fixed) HIP_CHECK(hipMemsetAsync(grid_fixed, 0, sizeof(int64_t) * net->n_grid, net->stream));
             return;
         }
         if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
@@ -1015,12 +1077,19 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
         const int blocks = train_block_count(net, b);
         net->ensure_slabs(blocks);
         if (net->hash()) {
-            // the grid-table gradient accumulates in the handle's f16 buffer (packed-half atomics) and is exported as
-            // f32 into the caller's buffer after the MLP part; the export zeroes the f16 buffer again
+            // the grid-table gradient accumulates in the handle's exact fixed-point buffer (grid_scatter_kernel) and is
+            // exported after the MLP part: rounded to f16, as f32, into the caller's gradient (nrc_train_grad), or
+            // exchange-encoded into grid_fixed (nrc_train_grad_fixed, nrc_train_dp); the export zeroes the buffer
+            // (unless grid_fixed is the buffer itself)
             HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
                                         net->wb_train, net->table_train, net->grid_grad, net->slabs, net->loss_partials,
-                                        net->stream, net->ensure_scatter(blocks)));
-            HIP_CHECK(launch_grid_grad_export(net->grid_grad, grad_d + net->n_mlp, net->n_grid, net->stream));
+                                        net->stream, net->step_scatter(blocks)));
+            if (grid_fixed)
+                HIP_CHECK(launch_grid_grad_export_fixed(net->grid_grad, grid_fixed, net->n_grid, net->nonfinite(),
+                                                        net->stream));
+            else
+                HIP_CHECK(launch_grid_grad_export(net->grid_grad, grad_d + net->n_mlp, net->n_grid, net->nonfinite(),
+                                                  net->stream));
         } else {
             train_partials(net, in, tgt, b, 3.0f * (float)global_b);
         }
@@ -1029,7 +1098,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
     }
 }
 
-void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* loss_d) {
+void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* loss_d, const int64_t* grid_fixed) {
     check_live(net);
     if (!grad_d) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null gradient buffer");
     net->step += 1;
@@ -1044,7 +1113,8 @@ void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* los
         if (net->hash()) {
             GridBuffers gb = net->grid_buffers();
             gb.grad32 = grad_d + net->n_mlp;  // read-only in kApplyOnly
-            HIP_CHECK(launch_grid_adam(kApplyOnly, gb, net->optim(net->step), net->stream));
+            gb.fixed = grid_fixed;            // kApplyFixed: read-only unless it is the handle's accumulator
+            HIP_CHECK(launch_grid_adam(grid_fixed ? kApplyFixed : kApplyOnly, gb, net->optim(net->step), net->stream));
         }
     }
     if (loss_h) {

@@ -217,7 +217,8 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
                                 const _Float16* wf, const _Float16* wb, float* slabs, float* loss_partials,
                                 uint64_t* stamps, hipStream_t s);
 
-enum ReduceMode { kReduceFused = 0, kReduceOnly = 1, kApplyOnly = 2, kPackOnly = 3 };
+// kApplyFixed (grid_adam_kernel only): the gradient is an all-reduced exchange-encoded fixed-point array (GridBuffers::fixed)
+enum ReduceMode { kReduceFused = 0, kReduceOnly = 1, kApplyOnly = 2, kPackOnly = 3, kApplyFixed = 4 };
 struct OptimArgs {
     float lr, beta1, beta2, eps, l2_reg, ema_decay, loss_scale;
     uint32_t step;
@@ -277,13 +278,24 @@ int knob(Knob k);
 
 // host-f32 Adam step-size and EMA debias of optimizer step oa.step (tcnn adam.h; identical to the oracle's)
 void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias);
+// Non-finite grid-gradient contributions: an f16 product w * dy that is inf or NaN cannot enter the fixed-point sum, so
+// grid_scatter_kernel ORs a code into codes[param] (1 = +inf, 2 = -inf, 3 = NaN; +inf and -inf together make NaN, as
+// in tcnn's f16 atomics) and stores the scatter's tag into *tag_dev. The kernels that round the step's sums read codes
+// only when *tag_dev equals their tag (a per-handle sequence number, never 0), and clear the codes they read.
+struct GridNonFinite {
+    uint8_t* codes = nullptr;   // [n] one byte per grid parameter, zero between steps
+    uint32_t* tag_dev = nullptr;
+    uint32_t tag = 0;
+};
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
     int64_t* grad64;      // [n] exact fixed-point sums (value x 2^24) of the f16 contributions, accumulated by
                           // grid_scatter_kernel, rounded to f16 and zeroed by grid_adam_kernel
     const float* grad32;  // kApplyOnly: the all-reduced data-parallel gradient (f32 [n], read-only)
+    const int64_t* fixed; // kApplyFixed: the all-reduced exchange-encoded sums [n] (may be grad64 itself)
     uint32_t* steps;  // per-entry Adam step counters
+    GridNonFinite nf;     // non-finite contributions of the step being consumed (kReduceFused)
     _Float16 *table_train, *table_infer;
     // Adam bias corrections per step count st = 1..bias_len: bias[st] = (sqrtf(1 - beta2^st), 1 - beta1^st), host
     // glibc powf as in the oracle (the kernel falls back to device powf past bias_len)
@@ -301,8 +313,18 @@ struct HashScatter {
     float4* pos;   // [bcap]
     uint32_t* dy;  // [NRC_HASH_LEVELS][bcap]
     int64_t bcap;
+    GridNonFinite nf;
 };
-hipError_t launch_grid_grad_export(int64_t* g64, float* g32, int n, hipStream_t s);
+// Data-parallel exports of the grid accumulator (both zero it for the next step and consume the non-finite codes):
+// f32 -- each sum rounded to f16 (nrc_train_grad); fixed -- the exact sum in the exchange encoding below, for an int64
+// sum over ranks (nrc_train_grad_fixed, nrc_train_dp; out may be g64 itself, which is then not zeroed).
+hipError_t launch_grid_grad_export(int64_t* g64, float* g32, int n, const GridNonFinite& nf, hipStream_t s);
+hipError_t launch_grid_grad_export_fixed(int64_t* g64, int64_t* out, int n, const GridNonFinite& nf, hipStream_t s);
+// Exchange encoding of a rank's exact sum v (value x 2^24) and its non-finite code c, such that the int64 SUM over up to
+// kFixedMaxRanks ranks decodes to the global sum and code: clamp(v, +-2^41) + 2^48 [c has +inf] + 2^55 [c has -inf].
+// |sum| >= 65520 x 2^24 rounds to f16 inf, so the clamp changes no result unless partial sums beyond 131072 cancel across
+// ranks (tcnn's f16 running sum is already inf there). The 7-bit marker counts bound the world size.
+constexpr int kFixedMaxRanks = 63;
 hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
                                 int64_t* waves, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,

@@ -2918,6 +2918,35 @@ __device__ __forceinline__ _Float16 fixed_to_f16(int64_t v) {
     return __builtin_bit_cast(_Float16, (uint16_t)(sign | ((uint32_t)be << 10) | (uint32_t)(mant - 1024u)));
 }
 
+// the value of a non-finite code (GridNonFinite)
+__device__ __forceinline__ float nonfinite_value(uint32_t code) {
+    return code == 1u ? __builtin_inff() : code == 2u ? -__builtin_inff() : __builtin_nanf("");
+}
+
+// parameter i's non-finite code of the step tagged nf.tag (0 if none), cleared for the next step
+__device__ __forceinline__ uint32_t take_nonfinite(const GridNonFinite& nf, int i) {
+    if (!nf.codes || __hip_atomic_load(nf.tag_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nf.tag) return 0u;
+    const uint32_t c = nf.codes[i];
+    if (c) nf.codes[i] = 0;
+    return c;
+}
+
+// the f16 gradient of an exact sum and its non-finite code
+__device__ __forceinline__ float fixed_gradient(int64_t v, uint32_t code) {
+    return code ? nonfinite_value(code) : (float)fixed_to_f16(v);
+}
+
+constexpr int64_t kFixedSat = 1ll << 41, kFixedOff = 1ll << 47;
+__device__ __forceinline__ int64_t fixed_encode(int64_t v, uint32_t code) {
+    v = v < -kFixedSat ? -kFixedSat : (v > kFixedSat ? kFixedSat : v);
+    return v + ((code & 1u) ? (1ll << 48) : 0ll) + ((code & 2u) ? (1ll << 55) : 0ll);
+}
+__device__ __forceinline__ float fixed_decode_gradient(int64_t e) {
+    const uint64_t u = (uint64_t)(e + kFixedOff);
+    const uint32_t code = (((u >> 48) & 127u) ? 1u : 0u) | (((u >> 55) & 127u) ? 2u : 0u);
+    return fixed_gradient((int64_t)(u & ((1ull << 48) - 1)) - kFixedOff, code);
+}
+
 __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -2929,8 +2958,11 @@ __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb
         float gradient;
         if (mode == kApplyOnly) {
             gradient = gb.grad32[i] / oa.loss_scale;
+        } else if (mode == kApplyFixed) {
+            gradient = fixed_decode_gradient(gb.fixed[i]) / oa.loss_scale;
+            if (gb.fixed == gb.grad64) gb.grad64[i] = 0;
         } else {
-            gradient = (float)fixed_to_f16(gb.grad64[i]) / oa.loss_scale;
+            gradient = fixed_gradient(gb.grad64[i], take_nonfinite(gb.nf, i)) / oa.loss_scale;
             gb.grad64[i] = 0;
         }
         if (gradient != 0.0f) {
@@ -2976,15 +3008,31 @@ hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa
 // Data-parallel export of the grid gradient: the f16-rounded exact sum as f32 into the exchange buffer, the fixed-point
 // accumulator zeroed for the next step.
 __global__ __launch_bounds__(256) void grid_grad_export_kernel(int64_t* __restrict__ g64, float* __restrict__ g32,
-                                                               int n) {
+                                                               int n, GridNonFinite nf) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    g32[i] = (float)fixed_to_f16(g64[i]);
+    g32[i] = fixed_gradient(g64[i], take_nonfinite(nf, i));
     g64[i] = 0;
 }
 
-hipError_t launch_grid_grad_export(int64_t* g64, float* g32, int n, hipStream_t s) {
-    hipLaunchKernelGGL(grid_grad_export_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g64, g32, n);
+hipError_t launch_grid_grad_export(int64_t* g64, float* g32, int n, const GridNonFinite& nf, hipStream_t s) {
+    hipLaunchKernelGGL(grid_grad_export_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g64, g32, n, nf);
+    return hipGetLastError();
+}
+
+// the exact sums in the exchange encoding (kFixedMaxRanks); in place when out == g64
+__global__ __launch_bounds__(256) void grid_grad_export_fixed_kernel(int64_t* g64, int64_t* out, int n,
+                                                                     GridNonFinite nf) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t v = g64[i];
+    out[i] = fixed_encode(v, take_nonfinite(nf, i));
+    if (out != g64) g64[i] = 0;
+}
+
+hipError_t launch_grid_grad_export_fixed(int64_t* g64, int64_t* out, int n, const GridNonFinite& nf, hipStream_t s) {
+    hipLaunchKernelGGL(grid_grad_export_fixed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g64, out, n,
+                       nf);
     return hipGetLastError();
 }
 
@@ -3010,7 +3058,7 @@ struct ScatterPlan {
 };
 constexpr int scatter_parts(int level) { return level == 0 ? 1 : NRC_HASH_T / kScatterPart; }
 
-// f16 value (bits) x 2^24 as an exact integer
+// finite f16 value (bits) x 2^24 as an exact integer (inf / NaN are routed to GridNonFinite by the caller)
 __device__ __forceinline__ int64_t f16_to_fixed(uint32_t h) {
     const uint32_t e = (h >> 10) & 31u, m = h & 1023u;
     const int64_t mag = e == 0 ? (int64_t)m : (int64_t)(m | 1024u) << (e - 1);
@@ -3020,7 +3068,8 @@ __device__ __forceinline__ int64_t f16_to_fixed(uint32_t h) {
 __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const float4* __restrict__ pos,
                                                                        const uint32_t* __restrict__ dy, int64_t bcap,
                                                                        ScatterPlan plan,
-                                                                       unsigned long long* __restrict__ grad) {
+                                                                       unsigned long long* __restrict__ grad,
+                                                                       GridNonFinite nf) {
     __shared__ unsigned long long acc[kScatterPart][2];  // 128 KiB: one block per CU
     int level = 0;
 #pragma unroll
@@ -3064,8 +3113,19 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
                 if (e < ne) {
                     const h2v c = {(_Float16)(C.w[cc] * dy0), (_Float16)(C.w[cc] * dy1)};
                     const uint32_t cb = __builtin_bit_cast(uint32_t, c);
-                    if (cb & 0x7FFFu) atomicAdd(&acc[e][0], (unsigned long long)f16_to_fixed(cb & 0xFFFFu));
-                    if (cb & 0x7FFF0000u) atomicAdd(&acc[e][1], (unsigned long long)f16_to_fixed(cb >> 16));
+#pragma unroll
+                    for (int f = 0; f < 2; ++f) {
+                        const uint32_t hb = (cb >> (16 * f)) & 0xFFFFu;
+                        if ((hb & 0x7C00u) == 0x7C00u) {
+                            // inf / NaN: no fixed-point value; recorded for the kernels that round the sums
+                            const uint32_t gi = 2u * (lbase + e0 + e) + (uint32_t)f;
+                            const uint32_t code = (hb & 0x3FFu) ? 3u : ((hb & 0x8000u) ? 2u : 1u);
+                            atomicOr(reinterpret_cast<uint32_t*>(nf.codes) + (gi >> 2), code << (8u * (gi & 3u)));
+                            __hip_atomic_store(nf.tag_dev, nf.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else if (hb & 0x7FFFu) {
+                            atomicAdd(&acc[e][f], (unsigned long long)f16_to_fixed(hb));
+                        }
+                    }
                 }
             }
         }
@@ -3086,7 +3146,8 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
     if (b <= 0) return hipSuccess;
     const int blocks = train_blocks(b);
     const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
-    if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap) return hipErrorInvalidValue;
+    if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap || !sc->nf.codes || !sc->nf.tag_dev || !sc->nf.tag)
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL((train_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
                        reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
@@ -3104,7 +3165,7 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
     }
     plan.first_block[NRC_HASH_LEVELS] = nb;
     hipLaunchKernelGGL(grid_scatter_kernel, dim3(nb), dim3(kScatterThreads), 0, s, sc->pos, sc->dy, bcap, plan,
-                       reinterpret_cast<unsigned long long*>(grid_grad));
+                       reinterpret_cast<unsigned long long*>(grid_grad), sc->nf);
     return hipGetLastError();
 }
 

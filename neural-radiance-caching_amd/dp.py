@@ -14,7 +14,9 @@ per device (/root/reference/nrc/src/Device.cpp:420, nrc/inc/Device.h:621) and ha
 
 ``backend`` is any object with ``train_grad(inputs, targets, b, global_b, grad)`` and
 ``train_apply(grad, loss)`` — ``network.Network`` on the GPU, an oracle-backed stand-in in the
-CPU tests.
+CPU tests. With a ``grid_fixed`` buffer (InputEncoding::Hash: int64 [HASH_GRID_PARAMS]) the trainer uses the exact
+grid exchange instead (``train_grad_fixed`` / ``train_apply_fixed``, nrc_c.h): the f32 all-reduce covers only the MLP
+gradient and the loss, the grid sums travel as int64 and are rounded to f16 once, after the sum over ranks.
 """
 from __future__ import annotations
 
@@ -30,12 +32,14 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
 
 
 class DataParallelTrainer:
-    def __init__(self, backend, grad_buffer, group=None):
+    def __init__(self, backend, grad_buffer, group=None, grid_fixed=None, mlp_params: int | None = None):
         import torch.distributed as dist
 
         self.backend = backend
         self.grad = grad_buffer  # torch tensor of backend.grad_floats f32 on the backend's device
         self.group = group
+        self.grid_fixed = grid_fixed  # Hash exact exchange: int64 [HASH_GRID_PARAMS] on the backend's device
+        self.mlp_params = mlp_params  # with grid_fixed: the MLP part of grad (loss at grad[-4])
         self._dist = dist
 
     def broadcast_state(self, net, device) -> None:
@@ -58,6 +62,13 @@ class DataParallelTrainer:
         net.step = int(step.item())
 
     def step(self, inputs, targets, b_local: int, global_b: int, loss: bool = False):
+        if self.grid_fixed is not None:
+            self.backend.train_grad_fixed(inputs, targets, b_local, global_b, self.grad, self.grid_fixed)
+            sum_ = self._dist.ReduceOp.SUM
+            self._dist.all_reduce(self.grad[:self.mlp_params], op=sum_, group=self.group)
+            self._dist.all_reduce(self.grad[-4:], op=sum_, group=self.group)
+            self._dist.all_reduce(self.grid_fixed, op=sum_, group=self.group)
+            return self.backend.train_apply_fixed(self.grad, self.grid_fixed, loss)
         self.backend.train_grad(inputs, targets, b_local, global_b, self.grad)
         self._dist.all_reduce(self.grad, op=self._dist.ReduceOp.SUM, group=self.group)
         return self.backend.train_apply(self.grad, loss)

@@ -31,7 +31,8 @@ from enum import IntEnum
 import numpy as np
 
 from . import _lib
-from ._lib import BATCH_SIZE, GRAD_FLOATS, NUM_PARAMS, NrcConfig, NrcError, NrcHyperParams, check, lib
+from ._lib import (BATCH_SIZE, GRAD_FLOATS, HASH_GRID_PARAMS, NUM_PARAMS, NrcConfig, NrcError, NrcHyperParams, check,
+                   lib)
 
 NRC_ERR_DESTROYED = 2
 
@@ -57,7 +58,7 @@ class HyperParams:
     learningRate: float
 
 
-def _dev_ptr(x, what: str, min_elems: int | None = None) -> int:
+def _dev_ptr(x, what: str, min_elems: int | None = None, dtype: str = "torch.float32") -> int:
     if x is None:
         raise ValueError(f"{what}: null buffer")
     if isinstance(x, int):
@@ -66,12 +67,12 @@ def _dev_ptr(x, what: str, min_elems: int | None = None) -> int:
     if hasattr(x, "data_ptr"):
         if not x.is_cuda:
             raise ValueError(f"{what}: tensor must live on the GPU")
-        if str(x.dtype) != "torch.float32":
-            raise ValueError(f"{what}: tensor must be float32")
+        if str(x.dtype) != dtype:
+            raise ValueError(f"{what}: tensor must be {dtype.split('.')[-1]}")
         if not x.is_contiguous():
             raise ValueError(f"{what}: tensor must be contiguous")
         if min_elems is not None and x.numel() < min_elems:
-            raise ValueError(f"{what}: needs at least {min_elems} floats, got {x.numel()}")
+            raise ValueError(f"{what}: needs at least {min_elems} elements, got {x.numel()}")
         return int(x.data_ptr())
     raise TypeError(f"{what}: expected a CUDA tensor or an integer device address, got {type(x)}")
 
@@ -207,6 +208,28 @@ class Network:
         lh = ctypes.c_float(float("nan"))
         check(self._lib.nrc_train_apply(self._h, _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None),
                                         ctypes.byref(lh) if loss else None))
+        return lh.value if loss else None
+
+    def train_grad_fixed(self, inputs, targets, b: int, global_b: int, grad, grid_fixed) -> None:
+        """Hash only: nrc_train_grad with this rank's exact grid sums exchange-encoded into grid_fixed (int64,
+        HASH_GRID_PARAMS; sum it over ranks as int64) and the grid part of grad left unwritten."""
+        b = int(b)
+        check(self._lib.nrc_train_grad_fixed(
+            self._h, _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None) if b else None,
+            _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None, b, int(global_b),
+            _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None),
+            _dev_ptr(grid_fixed, "grid_fixed", HASH_GRID_PARAMS if hasattr(grid_fixed, "numel") else None,
+                     "torch.int64")))
+
+    def train_apply_fixed(self, grad, grid_fixed, loss: bool = False):
+        """Hash only: the Adam + EMA step from the summed MLP gradient / loss in grad and the summed exact grid sums
+        in grid_fixed (each rounded to f16 once)."""
+        lh = ctypes.c_float(float("nan"))
+        check(self._lib.nrc_train_apply_fixed(
+            self._h, _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None),
+            _dev_ptr(grid_fixed, "grid_fixed", HASH_GRID_PARAMS if hasattr(grid_fixed, "numel") else None,
+                     "torch.int64"),
+            ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
     # ---- data parallelism inside the library (nrc_c.h: RCCL communicator + nrc_train_dp) ------------------

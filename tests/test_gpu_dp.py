@@ -32,13 +32,17 @@ def to_dev(torch, dev, a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
 
-def test_world1_rccl_step_is_bitwise_nrc_train(nrc, torch, dev, golden):
+@pytest.mark.parametrize("encoding", ["Frequency", "Hash"])
+def test_world1_rccl_step_is_bitwise_nrc_train(nrc, torch, dev, golden, encoding):
+    """Hash: nrc_train_dp runs the exact grid exchange (int64 sums in the exchange encoding, one RCCL group with the
+    f32 MLP gradient), which at world 1 must reproduce the fused step's grid update bit for bit."""
     comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
     nets = []
     for _ in range(2):
         n = nrc.Network()
-        n.init(stream=torch.cuda.current_stream())
-        n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+        n.init(stream=torch.cuda.current_stream(), encoding=getattr(nrc.InputEncoding, encoding))
+        if encoding == "Frequency":
+            n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
         nets.append(n)
     nets[1].set_comm(comm)
     assert nets[1].comm_rank() == (0, 1)
