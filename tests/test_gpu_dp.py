@@ -171,3 +171,32 @@ def test_two_ranks_on_one_gpu_gloo(tmp_path, nrc, torch, dev, golden, B):
     assert np.linalg.norm(p - r) <= 1e-4 * np.linalg.norm(r)
     np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
     ref.destroy()
+
+
+def test_two_ranks_on_one_gpu_gloo_hash_exact(tmp_path, nrc, torch, dev):
+    """Hash over gloo with the exact grid exchange (int64 all-reduce of the exchange-encoded fixed-point sums): the
+    replicas are bit-identical and their grid update is bitwise the single-process step over the whole minibatch (the
+    MLP part: summation-order tolerance). One step: afterwards the MLP weights differ by f32 rounding, and so would
+    the next step's grid gradient."""
+    B = 16384
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    procs = [subprocess.Popen([sys.executable, str(ROOT / "tools" / "dp_rank_worker.py"), str(tmp_path), str(B), "Hash",
+                               "1"], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), logs
+    ref = nrc.Network()
+    ref.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+    p0 = ref.get_state(nrc.StateSlot.PARAMS)
+    q_np, t_np = nrc.synthetic.cornell_batch(B, seed=80)
+    ref_loss = ref.train_batch(to_dev(torch, dev, q_np), to_dev(torch, dev, t_np), B, loss=True)
+    for slot in ("params", "infer"):
+        np.testing.assert_array_equal(np.load(tmp_path / f"{slot}_0.npy"), np.load(tmp_path / f"{slot}_1.npy"))
+    M = nrc.HASH_MLP_PARAMS
+    p, r = np.load(tmp_path / "params_0.npy"), ref.get_state(nrc.StateSlot.PARAMS)
+    assert (r[M:] != p0[M:]).sum() > 10_000
+    np.testing.assert_array_equal(p[M:], r[M:])
+    assert np.linalg.norm(p[:M] - r[:M]) <= 3e-3 * np.linalg.norm(r[:M])
+    np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), [ref_loss], rtol=1e-5)
+    ref.destroy()

@@ -2,8 +2,10 @@
 nrc_train_grad / nrc_train_apply through nrc_amd.dp.DataParallelTrainer, every rank on cuda:0.
 
     RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tools/dp_rank_worker.py <out_dir> [global_batch]
+        [encoding] [steps]
 
 global_batch (default 16,384) is split over the ranks; 4,096 gives configs[3]'s per-rank slice of 2,048 samples.
+encoding Hash: the exact grid exchange (DataParallelTrainer with an int64 grid_fixed buffer).
 """
 import os
 import sys
@@ -22,19 +24,26 @@ def main() -> None:
 
     out = Path(sys.argv[1])
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
+    encoding = sys.argv[3] if len(sys.argv) > 3 else "Frequency"
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     nrc = nrc_loader.load()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     net = nrc.Network()
-    net.init(stream=torch.cuda.current_stream())
-    net.set_state(nrc.StateSlot.PARAMS, np.load(out / "params.npy"))
-    grad = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
-    trainer = nrc.dp.DataParallelTrainer(net, grad)
+    net.init(stream=torch.cuda.current_stream(), encoding=getattr(nrc.InputEncoding, encoding))
+    if (out / "params.npy").exists():
+        net.set_state(nrc.StateSlot.PARAMS, np.load(out / "params.npy"))
+    grad = torch.zeros(net.grad_floats, dtype=torch.float32, device=dev)
+    if encoding == "Hash":
+        fixed = torch.zeros(nrc.HASH_GRID_PARAMS, dtype=torch.int64, device=dev)
+        trainer = nrc.dp.DataParallelTrainer(net, grad, grid_fixed=fixed, mlp_params=nrc.HASH_MLP_PARAMS)
+    else:
+        trainer = nrc.dp.DataParallelTrainer(net, grad)
     trainer.broadcast_state(net, dev)
     losses = []
-    for it in range(3):
+    for it in range(steps):
         q, t = nrc.synthetic.cornell_batch(B, seed=80 + it)
         s, c = nrc.dp.shard_range(B, rank, world)
         qd = torch.from_numpy(np.ascontiguousarray(q[s:s + c])).to(dev)
