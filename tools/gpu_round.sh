@@ -21,7 +21,7 @@ tests)
   tail -2 gpurun_out/smoke.log
   ;;
 bench)
-  bash tools/gpu_pmc.sh pmc_bench python3 "$ROOT/bench.py" --steps 10 --warmup 2 --train-frames 2 --no-cpu --sustained 0 --frame-iters 2 || exit 6
+  bash tools/gpu_pmc.sh pmc_bench python3 "$ROOT/bench.py" --steps 10 --warmup 2 --train-frames 2 --no-cpu --sustained 0 --frame-iters 2 --no-wide --no-hash --no-c4 || exit 6
   python tools/pmc_to_json.py gpurun_out/pmc_bench infer_kernel gpurun_out/pmc_infer.json > /dev/null || exit 7
   python tools/pmc_summary.py gpurun_out/pmc_bench > gpurun_out/pmc_bench_summary.txt || exit 8
   cp gpurun_out/pmc_infer.json "profiles/pmc_infer_$ROUND.json"
