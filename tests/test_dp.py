@@ -51,6 +51,25 @@ class OracleBackend:
         self.st.apply(grad[: self.st.params.size].numpy().astype(np.float32))
         return float(grad[self.st.params.size]) if loss else None
 
+    # Hash exact exchange (nrc_train_grad_fixed / nrc_train_apply_fixed contract): the grid part travels as int64
+    # fixed-point sums (value x 2^24; the stand-in quantises the oracle's f32 gradient), the f32 grid part of grad is
+    # not written
+    def train_grad_fixed(self, q, t, b, global_b, grad, grid_fixed):
+        import torch
+
+        M = self.orc.HASH_MLP_PARAMS
+        g, loss = self.orc.hash_grad(self.st.params, q[:b], t[:b], n_total=3.0 * global_b, mode=self.orc.FP32,
+                                     threads=2)
+        grad[:M] = torch.from_numpy(g[:M])
+        grad[g.size] = loss
+        grid_fixed[:] = torch.from_numpy(np.rint(g[M:].astype(np.float64) * 2.0 ** 24).astype(np.int64))
+
+    def train_apply_fixed(self, grad, grid_fixed, loss=False):
+        M = self.orc.HASH_MLP_PARAMS
+        g = np.concatenate([grad[:M].numpy(), (grid_fixed.numpy() / 2.0 ** 24).astype(np.float32)])
+        self.st.apply(g.astype(np.float32))
+        return float(grad[self.st.params.size]) if loss else None
+
     # state access with nrc_amd.Network's names (StateSlot order: PARAMS, INFER, EMA, ADAM_M, ADAM_V)
     _SLOTS = ("params", "infer", "ema", "m", "v")
 
@@ -83,7 +102,7 @@ def _init_params(orc, hash_grid):
     return orc.init_params(1337) * np.float32(1.5)
 
 
-def _worker(rank, world, port, B, steps, out_dir, hash_grid=False):
+def _worker(rank, world, port, B, steps, out_dir, hash_grid=False, fixed=False):
     import torch
     import torch.distributed as dist
 
@@ -94,8 +113,13 @@ def _worker(rank, world, port, B, steps, out_dir, hash_grid=False):
     orc = nrc_loader.load_oracle()
     params = _init_params(orc, hash_grid)
     backend = OracleBackend(params, hash_grid)
-    grad = torch.zeros(backend.grad_floats, dtype=torch.float32)
-    trainer = nrc.dp.DataParallelTrainer(backend, grad)
+    grad = torch.full((backend.grad_floats,), 9.0, dtype=torch.float32)  # the grid part must play no role (fixed)
+    if fixed:
+        grid_fixed = torch.zeros(orc.HASH_GRID_PARAMS, dtype=torch.int64)
+        trainer = nrc.dp.DataParallelTrainer(backend, grad, grid_fixed=grid_fixed, mlp_params=orc.HASH_MLP_PARAMS)
+    else:
+        grad.zero_()
+        trainer = nrc.dp.DataParallelTrainer(backend, grad)
     losses = []
     for it in range(steps):
         q, t = nrc.synthetic.cornell_batch(B, seed=40 + it)
@@ -191,3 +215,34 @@ def test_broadcast_state_syncs_every_slot_and_the_step(tmp_path):
     for slot in range(5):
         np.testing.assert_array_equal(np.load(tmp_path / f"slot{slot}_0.npy"), np.load(tmp_path / f"slot{slot}_1.npy"))
     assert int(np.load(tmp_path / "step_0.npy")[0]) == int(np.load(tmp_path / "step_1.npy")[0]) == 2
+
+
+def test_dp_trainer_fixed_grid_exchange(tmp_path):
+    """DataParallelTrainer with an int64 grid_fixed buffer (the Hash exact exchange): the f32 all-reduce covers the
+    MLP gradient and the loss slots only, the grid sums are summed as int64 — the replicas equal a single process
+    that sums the two shards' fixed-point grid gradients as integers."""
+    import torch.multiprocessing as mp
+
+    world, B, steps = 2, 256, 2
+    mp.spawn(_worker, args=(world, _free_port(), B, steps, str(tmp_path), True, True), nprocs=world, join=True)
+    orc = nrc_loader.load_oracle()
+    nrc = nrc_loader.load()
+    M = orc.HASH_MLP_PARAMS
+    st = orc.HashAdamEmaState(_init_params(orc, True))
+    ref_losses = []
+    for it in range(steps):
+        q, t = nrc.synthetic.cornell_batch(B, seed=40 + it)
+        g_mlp, fixed, loss = np.zeros(M, np.float32), np.zeros(orc.HASH_GRID_PARAMS, np.int64), 0.0
+        for r in range(world):
+            s, c = nrc.dp.shard_range(B, r, world)
+            g, lr = orc.hash_grad(st.params, q[s:s + c], t[s:s + c], n_total=3.0 * B, mode=orc.FP32, threads=2)
+            g_mlp += g[:M]
+            fixed += np.rint(g[M:].astype(np.float64) * 2.0 ** 24).astype(np.int64)
+            loss += lr
+        st.apply(np.concatenate([g_mlp, (fixed / 2.0 ** 24).astype(np.float32)]))
+        ref_losses.append(loss)
+    p0, p1 = np.load(tmp_path / "params_0.npy"), np.load(tmp_path / "params_1.npy")
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_array_equal(p0[M:], st.params[M:])
+    assert np.linalg.norm(p0[:M] - st.params[:M]) <= 1e-5 * np.linalg.norm(st.params[:M])
+    np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
