@@ -488,11 +488,14 @@ void upload_all(nrc_net* net, const std::vector<float>& params, const std::vecto
     HIP_CHECK(hipMemcpy(net->infer, infer.data(), sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
 }
 
+WideImages wide_images(const nrc_net* net) {
+    return WideImages{reinterpret_cast<_Float16*>(net->wide_img16), net->wide_img8, net->wide_scales, net->wide_fwd_train,
+                      net->wide_bwd_train, net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0};
+}
+
 void repack(nrc_net* net, hipStream_t s) {
     if (net->wide()) {
-        const int enc = net->encoding == NRC_ENCODING_FREQUENCY_SH ? 2 : 0;
-        HIP_CHECK(launch_wide_pack(net->infer, net->params, enc, reinterpret_cast<_Float16*>(net->wide_img16),
-                                   net->wide_img8, net->wide_scales, net->wide_fwd_train, net->wide_bwd_train, s));
+        HIP_CHECK(launch_wide_pack(net->infer, net->params, wide_images(net), s));
         return;
     }
     HIP_CHECK(launch_reduce_adam(kPackOnly, nullptr, 0, nullptr, nullptr, nullptr, net->buffers(), net->optim(1), s));
@@ -549,8 +552,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
         net->step += 1;
         HIP_CHECK(launch_wide_adam(kReduceFused, net->wide_slabs, wide_chunks(b), net->wide_loss_partials,
                                    (int)(wide_bpad(b) / 32), nullptr, loss_d ? loss_d : net->loss_dev, net->buffers(),
-                                   net->optim(net->step), net->stream));
-        repack(net, net->stream);
+                                   net->optim(net->step), wide_images(net), net->stream));
         if (loss_h) {
             *loss_h = net->read_loss();
         }
@@ -1071,7 +1073,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
             wide_grad_partials(net, in, tgt, b, 3.0f * (float)global_b);
             HIP_CHECK(launch_wide_adam(kReduceOnly, net->wide_slabs, wide_chunks(b), net->wide_loss_partials,
                                        (int)(wide_bpad(b) / 32), grad_d, nullptr, net->buffers(),
-                                       net->optim(net->step + 1), net->stream));
+                                       net->optim(net->step + 1), wide_images(net), net->stream));
             return;
         }
         const int blocks = train_block_count(net, b);
@@ -1105,8 +1107,7 @@ void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* los
     float* ld = loss_d ? loss_d : net->loss_dev;
     if (net->wide()) {
         HIP_CHECK(launch_wide_adam(kApplyOnly, nullptr, 0, nullptr, 0, const_cast<float*>(grad_d), ld, net->buffers(),
-                                   net->optim(net->step), net->stream));
-        repack(net, net->stream);
+                                   net->optim(net->step), wide_images(net), net->stream));
     } else {
         HIP_CHECK(launch_reduce_adam(kApplyOnly, nullptr, 0, nullptr, const_cast<float*>(grad_d), ld, net->buffers(),
                                      net->optim(net->step), net->stream));

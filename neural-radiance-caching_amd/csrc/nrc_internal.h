@@ -154,9 +154,17 @@ __host__ __device__ constexpr int wide8_frag(int layer, int mb, int s) {
 __host__ __device__ constexpr int f8_row(int s, int h, int j) {
     return 64 * s + 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
 }
+// the width-128 weight images a step rewrites: f16 inference (img16; img8 = FP8 image whose first 20 KiB are the f16
+// layer-0 fragments, scales = per-row E8M0 words) and the training forward / backward images; enc 0 Frequency, 2 SH
+struct WideImages {
+    _Float16* img16;
+    uint8_t* img8;
+    uint32_t* scales;
+    _Float16 *fwd16, *bwd16;
+    int enc;
+};
 // every width-128 image: inference f16 + FP8 (+ row scales) from w_infer, training fwd/bwd from w_train
-hipError_t launch_wide_pack(const float* w_infer, const float* w_train, int enc, _Float16* img16, uint8_t* img8,
-                            uint32_t* scales, _Float16* fwd16, _Float16* bwd16, hipStream_t s);
+hipError_t launch_wide_pack(const float* w_infer, const float* w_train, const WideImages& im, hipStream_t s);
 // prec 0 = f16, 1 = fp8; enc 0 = Frequency, 2 = FrequencySH; mode -1 plain, 0 / 2 fused accumulation
 hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out, int64_t n, const void* img,
                              const uint32_t* scales, const float* thr, float* rgba, int64_t n_acc, int mode, float w,
@@ -172,9 +180,10 @@ int wide_chunks(int64_t b);
 hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float* targets, int64_t b, float n_total,
                                      float loss_scale, const _Float16* fwd16, const _Float16* bwd16, _Float16* ws_in,
                                      _Float16* ws_d, float* slabs, float* loss_partials, hipStream_t s);
+// the optimizer step and (modes other than kReduceOnly) every image of im, in one launch
 hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const float* loss_partials, int nlp,
                             float* grad_io, float* loss_out, const struct ModelBuffers& mb, const struct OptimArgs& oa,
-                            hipStream_t s);
+                            const WideImages& im, hipStream_t s);
 // diagnostic: e4m3 conversion exactly as the FP8 kernels do it (clamp to [lo, 448], v_cvt_pk_fp8_f32)
 hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, hipStream_t s);
 

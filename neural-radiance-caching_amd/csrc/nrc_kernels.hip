@@ -1429,15 +1429,6 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
     }
 }
 
-// All width-128 weight images in one launch, after every optimizer step (or set_state):
-//   fp8 part, one wave per (layer 1..5, row block mb): lane (r, h) loads the 64 weights of row 32 mb + r that its
-//     e4m3 bytes carry (lanes h = 0 / 1 hold complementary halves of the row), so the row's E8M0 exponent (oracle
-//     orc_fp8_row_exponent: max |w| of the row) is a lane max and one xor-32 shuffle; the wave then converts and
-//     stores its 4 16-byte units and byte mb of the row's scale word (W5: the whole word);
-//   f16 inference image (img16, and its 20 layer-0 fragments into img8) from the EMA weights;
-//   training images fwd16 / bwd16 (W_l^T) from the master weights.
-// One thread per 16-byte unit in the f16 parts. (It replaced three launches -- row exponents, inference images,
-// training images -- of ~5 us each.)
 // width-128 training layout helpers: backward-image fragment, workspace rows, parameter offsets
 __host__ __device__ constexpr int wide_bwd_frag(int layer, int mb, int kk) {
     return layer == 5 ? mb : 4 + (layer - 1) * 32 + mb * 8 + kk;
@@ -1446,123 +1437,6 @@ __host__ __device__ constexpr int64_t wide_in_row(int layer) { return layer == 0
 __host__ __device__ constexpr int64_t wide_d_row(int layer) { return (int64_t)layer * 128; }
 __host__ __device__ constexpr int wide_off(int layer) {
     return layer == 0 ? NRC_WIDE_W0_OFFSET : layer <= 4 ? NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 : NRC_WIDE_W5_OFFSET;
-}
-
-// training images from the f32 master weights: forward (as the inference img16) and backward W_l^T fragments
-__device__ __forceinline__ void wide_pack_train_unit(const float* __restrict__ w, int enc,
-                                                     _Float16* __restrict__ fwd16, _Float16* __restrict__ bwd16, int u) {
-    constexpr int UF = kWideF16Frags * 64, UB = kWideBwdFrags * 64;
-    if (u < UF) {
-        const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
-        int layer, mb, kk;
-        if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
-        else if (f < 148) { layer = 1 + (f - 20) / 32; mb = ((f - 20) % 32) / 8; kk = (f - 20) % 8; }
-        else { layer = 5; mb = 0; kk = f - 148; }
-        const int row = 32 * mb + r;
-        h8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float x = 0.0f;
-            if (layer == 0) x = w[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
-            else if (layer < 5 || row < NRC_OUT_PADDED) x = w[wide_off(layer) + row * 128 + acc_row(kk, h, j)];
-            v[j] = (_Float16)x;
-        }
-        reinterpret_cast<h8*>(fwd16)[u] = v;
-    } else if (u < UF + UB) {
-        const int v8 = u - UF, f = v8 / 64, lane = v8 % 64, r = lane & 31, h = lane >> 5;
-        const int layer = f < 4 ? 5 : 1 + (f - 4) / 32, mb = f < 4 ? f : ((f - 4) % 32) / 8, kk = f < 4 ? 0 : (f - 4) % 8;
-        const int col = 32 * mb + r;  // row of W_l^T = input feature of layer l
-        h8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int row = acc_row(kk, h, j);  // output neuron of layer l
-            v[j] = (_Float16)w[wide_off(layer) + row * 128 + col];
-        }
-        reinterpret_cast<h8*>(bwd16)[v8] = v;
-    }
-}
-
-constexpr int kPackFp8Waves = 4 * 4 + 1;
-__global__ __launch_bounds__(256) void wide_pack_all_kernel(const float* __restrict__ wi, const float* __restrict__ wt,
-                                                            int enc, _Float16* __restrict__ img16,
-                                                            uint8_t* __restrict__ img8, uint32_t* __restrict__ scales,
-                                                            _Float16* __restrict__ fwd16, _Float16* __restrict__ bwd16) {
-    constexpr int UC = kPackFp8Waves * 64, U16 = kWideF16Bytes / 16, UF = kWideF16Frags * 64, UB = kWideBwdFrags * 64;
-    int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u < UC) {
-        const int t = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
-        const int layer = t < 16 ? 1 + t / 4 : 5, mb = t < 16 ? t % 4 : 0;
-        const int row = 32 * mb + r;
-        const bool live = layer < 5 || row < NRC_OUT_PADDED;
-        const float* wr = wi + NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128;  // W5 rows follow W4's
-        float v[2][2][16];
-        float amax = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int plane = 0; plane < 2; ++plane)
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const float x = live ? wr[f8_row(s, h, 16 * plane + k)] : 0.0f;
-                    v[s][plane][k] = x;
-                    amax = fmaxf(amax, fabsf(x));
-                }
-        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
-        int e = 0;
-        if (amax > 0.0f) {
-            int E = 0;
-            const float M = frexpf(amax, &E);
-            e = M <= 0.875f ? E - 9 : E - 8;
-            e = max(-127, min(127, e));
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int plane = 0; plane < 2; ++plane) {
-                uint32_t wd[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    float a[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        a[i] = live ? __builtin_amdgcn_fmed3f(ldexpf(v[s][plane][4 * d + i], -e), -448.0f, 448.0f)
-                                    : 0.0f;
-                    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
-                    wd[d] = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], lo, true);
-                }
-                const int f = wide8_frag(layer, mb, s);
-                reinterpret_cast<u4*>(img8 + 20 * 1024)[f * 128 + plane * 64 + lane] = u4{wd[0], wd[1], wd[2], wd[3]};
-            }
-        // scale word of (layer, r): byte mb = E8M0 of row 32 mb + r (rows past W5's 16 outputs: exponent 0)
-        if (h == 0) {
-            if (layer < 5) reinterpret_cast<uint8_t*>(scales)[((layer - 1) * 32 + r) * 4 + mb] = (uint8_t)(e + 127);
-            else scales[4 * 32 + r] = (uint32_t)(e + 127) | (127u << 8) | (127u << 16) | (127u << 24);
-        }
-        return;
-    }
-    u -= UC;
-    if (u < U16) {
-        const int f = u / 64, lane = u % 64, r = lane & 31, h = lane >> 5;
-        int layer, mb, kk;
-        if (f < 20) { layer = 0; mb = f / 5; kk = f % 5; }
-        else if (f < 148) { layer = 1 + (f - 20) / 32; mb = ((f - 20) % 32) / 8; kk = (f - 20) % 8; }
-        else { layer = 5; mb = 0; kk = f - 148; }
-        const int row = 32 * mb + r;
-        h8 v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float x = 0.0f;
-            if (layer == 0) x = wi[NRC_WIDE_W0_OFFSET + row * NRC_ENC_WIDTH + enc_k0_feature(enc, 16 * kk + 8 * h + j)];
-            else if (layer < 5 || row < NRC_OUT_PADDED)
-                x = wi[NRC_WIDE_W1_OFFSET + (layer - 1) * 16384 + row * 128 + acc_row(kk, h, j)];
-            v[j] = (_Float16)x;
-        }
-        reinterpret_cast<h8*>(img16)[u] = v;
-        if (f < 20) reinterpret_cast<h8*>(img8)[u] = v;
-        return;
-    }
-    u -= U16;
-    if (u < UF + UB) wide_pack_train_unit(wt, enc, fwd16, bwd16, u);
 }
 
 // e4m3 conversion as the FP8 kernels do it (diagnostic entry for the exhaustive conversion test)
@@ -2244,8 +2118,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
 //                        layer's input and delta as f16 [feature][sample] rows of a workspace (row stride wide_ld);
 //   wide_dw_kernel       dW_l = sum_s delta_l in_l^T as 32x32 tiles x 512-sample chunks (A and B fragments are
 //                        16-byte loads of those rows), partial sums per chunk in canonical parameter order;
-//   wide_adam_kernel     fixed-order chunk sum + tcnn Adam + EMA per parameter (same float operations as
-//                        adam_pack_one), then the f16 / FP8 images are repacked (wide_pack_all_kernel).
+//   wide_adam_pack_kernel fixed-order chunk sum + tcnn Adam + EMA per parameter (same float operations as
+//                        adam_pack_one) and, in the same launch, every f16 / FP8 weight image.
 // ------------------------------------------------------------------------------------------------
 // f16 B fragments (rows acc_row(kk, h, j), sample s) -> ws[row * ld + s] with 4-byte stores: adjacent lanes
 // (samples 2p, 2p + 1) swap half of their 8 rows (one DPP quad_perm [1,0,3,2] per dword), so each lane holds 4 rows x
@@ -2503,12 +2377,35 @@ __global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict
     }
 }
 
-// fixed-order chunk sum + Adam + EMA (modes as reduce_adam_kernel); loss partials summed by wave 0 of block 0
-__global__ __launch_bounds__(256) void wide_adam_kernel(int mode, const float* __restrict__ slabs, int nchunks,
-                                                        const float* __restrict__ loss_partials, int nlp,
-                                                        float* __restrict__ grad_io, float* __restrict__ loss_out,
-                                                        ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+// Width-128 optimizer step with every weight image packed in the same launch (round 3; replaced wide_adam_kernel +
+// wide_pack_all_kernel, 6.3 + 9.5 us per step: the pack's FP8 part was 17 waves each gathering 64 scattered weights).
+// One row of one layer per 32 lanes, 4 consecutive parameters per lane (16-byte loads / stores of the f32 arrays):
+//   modes kReduceFused / kReduceOnly: the chunk partials summed in chunk order (as the oracle's f32 loop); kApplyOnly: the
+//   all-reduced gradient; then tcnn Adam + EMA, the same float operations as adam_pack_one (kReduceOnly stops at the sum);
+//   kPackOnly: no step, the images from the current params / infer;
+//   images: f16 inference image (img16, and img8's f16 layer-0 fragments) from the debiased EMA weights, training
+//   forward (fwd16) and backward W_l^T (bwd16) images from the master weights, and the FP8 image with its per-row E8M0
+//   exponent: max |w| of the row is a max over the row's 32 lanes (orc_fp8_row_exponent).
+// The loss partials are summed by wave 0 of block 0.
+struct K0Inverse {
+    int8_t k[2][NRC_ENC_WIDTH];  // [FrequencySH][canonical feature] -> layer-0 K slot
+};
+constexpr K0Inverse make_k0_inverse() {
+    K0Inverse t{};
+    for (int e = 0; e < 2; ++e)
+        for (int K = 0; K < NRC_ENC_WIDTH; ++K) t.k[e][enc_k0_feature(e ? 2 : 0, K)] = (int8_t)K;
+    return t;
+}
+__constant__ K0Inverse kK0Inv = make_k0_inverse();
+constexpr int kWideRowUnits = 128 + 4 * 128 + 32;  // layer 0, layers 1-4, layer 5 incl. the 16 zero rows of its images
+
+__global__ __launch_bounds__(256) void wide_adam_pack_kernel(int mode, const float* __restrict__ slabs, int nchunks,
+                                                             const float* __restrict__ loss_partials, int nlp,
+                                                             float* __restrict__ grad_io, float* __restrict__ loss_out,
+                                                             ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias,
+                                                             WideImages im) {
 #pragma clang fp contract(off)
+    typedef float f4 __attribute__((ext_vector_type(4)));
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
@@ -2523,40 +2420,124 @@ __global__ __launch_bounds__(256) void wide_adam_kernel(int mode, const float* _
             loss_out[0] = grad_io[mb.n_total];
         }
     }
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= NRC_WIDE_NUM_PARAMS) return;
-    float gsum = 0.0f;
-    if (mode == kApplyOnly) {
-        gsum = grad_io[p];
-    } else {
-        // 16 chunk loads in flight, summed in chunk order (adding +0 for absent chunks leaves the sum unchanged)
-        for (int c0 = 0; c0 < nchunks; c0 += 16) {
-            float v[16];
+    const int unit = (int)((blockIdx.x * 256u + threadIdx.x) >> 5), c4 = threadIdx.x & 31;
+    if (unit >= kWideRowUnits) return;  // whole half-waves
+    const int layer = unit < 128 ? 0 : unit < 640 ? 1 + (unit - 128) / 128 : 5;
+    const int row = unit < 128 ? unit : unit < 640 ? (unit - 128) % 128 : unit - 640;
+    const int in_dim = layer == 0 ? NRC_ENC_WIDTH : 128, c = 4 * c4;
+    const bool live = (layer < 5 || row < NRC_OUT_PADDED) && c < in_dim;
+    const int p = wide_off(layer) + row * in_dim + c;  // this lane's first parameter
+    f4 w = {0.f, 0.f, 0.f, 0.f}, inf = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+        if (mode == kPackOnly) {
+            w = *(const f4*)(mb.params + p);
+            inf = *(const f4*)(mb.infer + p);
+        } else {
+            const f4 w0 = *(const f4*)(mb.params + p);
+            f4 g = {0.f, 0.f, 0.f, 0.f}, m0 = {}, v0 = {}, e0 = {};
+            if (mode != kReduceOnly) {
+                m0 = *(const f4*)(mb.m + p);
+                v0 = *(const f4*)(mb.v + p);
+                e0 = *(const f4*)(mb.ema + p);
+            }
+            if (mode == kApplyOnly) {
+                // the caller's all-reduced buffer: 4-byte aligned only
+                for (int i = 0; i < 4; ++i) g[i] = grad_io[p + i];
+            } else {
+                // 16 chunk loads in flight per batch, summed in chunk order (+0 for absent chunks leaves the sum unchanged)
+                for (int c0 = 0; c0 < nchunks; c0 += 16) {
+                    f4 v[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                v[j] = c0 + j < nchunks ? slabs[(int64_t)(c0 + j) * NRC_WIDE_NUM_PARAMS + p] : 0.0f;
+                    for (int j = 0; j < 16; ++j)
+                        v[j] = c0 + j < nchunks ? *(const f4*)(slabs + (int64_t)(c0 + j) * NRC_WIDE_NUM_PARAMS + p)
+                                                : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < 16; ++j) gsum += v[j];
+                    for (int j = 0; j < 16; ++j) g += v[j];
+                }
+                if (mode == kReduceOnly) {
+                    for (int i = 0; i < 4; ++i) grad_io[p + i] = g[i];
+                    return;
+                }
+            }
+            f4 m1, v1, e1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float gradient = g[i] / oa.loss_scale;
+                float wi = w0[i];
+                gradient += oa.l2_reg * wi;
+                const float gsq = gradient * gradient;
+                m1[i] = oa.beta1 * m0[i] + (1.0f - oa.beta1) * gradient;
+                v1[i] = oa.beta2 * v0[i] + (1.0f - oa.beta2) * gsq;
+                const float eff = lr_t / (sqrtf(v1[i]) + oa.eps);
+                wi = wi - eff * m1[i];
+                w[i] = wi;
+                e1[i] = e0[i] * oa.ema_decay + wi * (1.0f - oa.ema_decay);
+                inf[i] = e1[i] / ema_debias;
+            }
+            *(f4*)(mb.m + p) = m1;
+            *(f4*)(mb.v + p) = v1;
+            *(f4*)(mb.params + p) = w;
+            *(f4*)(mb.ema + p) = e1;
+            *(f4*)(mb.infer + p) = inf;
         }
-        if (mode == kReduceOnly) {
-            grad_io[p] = gsum;
-            return;
+    } else if (mode == kReduceOnly) {
+        return;
+    }
+    // ---- images
+    const int mbk = row >> 5, r = row & 31;
+    if (layer == 0) {
+        if (c >= in_dim) return;
+        for (int i = 0; i < 4; ++i) {
+            const int K = kK0Inv.k[im.enc == 2][c + i];
+            const int idx = (wide_frag(0, mbk, K >> 4) * 64 + r + 32 * ((K >> 3) & 1)) * 8 + (K & 7);
+            im.img16[idx] = (_Float16)inf[i];
+            reinterpret_cast<_Float16*>(im.img8)[idx] = (_Float16)inf[i];
+            im.fwd16[idx] = (_Float16)w[i];
+        }
+        return;
+    }
+    {
+        // forward layout: column c -> (k-step kk, lane half h, element j) of acc_row; 4 columns = 4 consecutive halves
+        const int kk = ((c >> 5) << 1) | ((c >> 4) & 1), h = (c >> 2) & 1, j = ((c >> 3) & 1) * 4;
+        const int idx = (wide_frag(layer, mbk, kk) * 64 + r + 32 * h) * 8 + j;
+        const h4 hi = {(_Float16)inf[0], (_Float16)inf[1], (_Float16)inf[2], (_Float16)inf[3]};
+        const h4 hw = {(_Float16)w[0], (_Float16)w[1], (_Float16)w[2], (_Float16)w[3]};
+        *(h4*)(im.img16 + idx) = hi;
+        *(h4*)(im.fwd16 + idx) = hw;
+    }
+    if (layer < 5 || row < NRC_OUT_PADDED) {
+        // backward image W_l^T: element (row, col) at lane (col % 32, half (row >> 2) & 1) of fragment (col / 32, kk(row))
+        const int kk = ((row >> 5) << 1) | ((row >> 4) & 1), h = (row >> 2) & 1, j = ((row >> 3) & 1) * 4 + (row & 3);
+        for (int i = 0; i < 4; ++i) {
+            const int col = c + i;
+            im.bwd16[(wide_bwd_frag(layer, col >> 5, kk) * 64 + (col & 31) + 32 * h) * 8 + j] = (_Float16)w[i];
         }
     }
-    float gradient = gsum / oa.loss_scale;
-    float w = mb.params[p];
-    gradient += oa.l2_reg * w;
-    const float gsq = gradient * gradient;
-    const float m1 = oa.beta1 * mb.m[p] + (1.0f - oa.beta1) * gradient;
-    const float v1 = oa.beta2 * mb.v[p] + (1.0f - oa.beta2) * gsq;
-    mb.m[p] = m1;
-    mb.v[p] = v1;
-    const float eff = lr_t / (sqrtf(v1) + oa.eps);
-    w = w - eff * m1;
-    mb.params[p] = w;
-    const float e = mb.ema[p] * oa.ema_decay + w * (1.0f - oa.ema_decay);
-    mb.ema[p] = e;
-    mb.infer[p] = e / ema_debias;
+    // FP8 image: the row's exponent, then bytes k .. k + 3 of (k-step s, plane, lane r + 32 h)
+    float amax = fmaxf(fmaxf(fabsf(inf[0]), fabsf(inf[1])), fmaxf(fabsf(inf[2]), fabsf(inf[3])));
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, 64));
+    int e = 0;
+    if (amax > 0.0f) {
+        int E = 0;
+        const float M = frexpf(amax, &E);
+        e = M <= 0.875f ? E - 9 : E - 8;
+        e = max(-127, min(127, e));
+    }
+    float a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = __builtin_amdgcn_fmed3f(ldexpf(inf[i], -e), -448.0f, 448.0f);
+    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
+    const uint32_t wd = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], lo, true);
+    {
+        const int s = c >> 6, plane = (c >> 5) & 1, h = (c >> 2) & 1, k = 4 * ((c >> 3) & 3);
+        const int f = wide8_frag(layer, mbk, s);
+        *reinterpret_cast<uint32_t*>(im.img8 + 20 * 1024 + (f * 128 + plane * 64 + r + 32 * h) * 16 + k) = wd;
+    }
+    if (c4 == 0) {
+        if (layer < 5) reinterpret_cast<uint8_t*>(im.scales)[((layer - 1) * 32 + r) * 4 + mbk] = (uint8_t)(e + 127);
+        else im.scales[4 * 32 + r] = (uint32_t)(e + 127) | (127u << 8) | (127u << 16) | (127u << 24);
+    }
 }
 
 
@@ -2723,11 +2704,13 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
     }
 }
 
-hipError_t launch_wide_pack(const float* w_infer, const float* w_train, int enc, _Float16* img16, uint8_t* img8,
-                            uint32_t* scales, _Float16* fwd16, _Float16* bwd16, hipStream_t s) {
-    constexpr int units = kPackFp8Waves * 64 + kWideF16Bytes / 16 + (kWideF16Frags + kWideBwdFrags) * 64;
-    hipLaunchKernelGGL(wide_pack_all_kernel, dim3((units + 255) / 256), dim3(256), 0, s, w_infer, w_train, enc, img16,
-                       img8, scales, fwd16, bwd16);
+hipError_t launch_wide_pack(const float* w_infer, const float* w_train, const WideImages& im, hipStream_t s) {
+    ModelBuffers mb{};
+    mb.params = const_cast<float*>(w_train);
+    mb.infer = const_cast<float*>(w_infer);
+    hipLaunchKernelGGL(wide_adam_pack_kernel, dim3(kWideRowUnits * 32 / 256), dim3(256), 0, s, (int)kPackOnly,
+                       (const float*)nullptr, 0, (const float*)nullptr, 0, (float*)nullptr, (float*)nullptr, mb,
+                       OptimArgs{}, 0.0f, 1.0f, im);
     return hipGetLastError();
 }
 
@@ -2808,12 +2791,13 @@ hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float*
 }
 
 hipError_t launch_wide_adam(int mode, const float* slabs, int nchunks, const float* loss_partials, int nlp,
-                            float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+                            float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
+                            const WideImages& im, hipStream_t s) {
     const float step = (float)(oa.step ? oa.step : 1);
     const float lr_t = oa.lr * sqrtf(1.0f - powf(oa.beta2, step)) / (1.0f - powf(oa.beta1, step));
     const float ema_debias = 1.0f - powf(oa.ema_decay, step);
-    hipLaunchKernelGGL(wide_adam_kernel, dim3((NRC_WIDE_NUM_PARAMS + 255) / 256), dim3(256), 0, s, mode, slabs, nchunks,
-                       loss_partials, nlp, grad_io, loss_out, mb, oa, lr_t, ema_debias);
+    hipLaunchKernelGGL(wide_adam_pack_kernel, dim3(kWideRowUnits * 32 / 256), dim3(256), 0, s, mode, slabs, nchunks,
+                       loss_partials, nlp, grad_io, loss_out, mb, oa, lr_t, ema_debias, im);
     return hipGetLastError();
 }
 
