@@ -2297,83 +2297,61 @@ __global__ __launch_bounds__(128, 1) void wide_fwd_bwd_lds_kernel(const float* _
     }
 }
 
-// One wave per (32x32 tile of dW_l, chunk of kWideChunk samples). Tiles: layer 0 4 x 3 (80 inputs), layers 1-4
-// 4 x 4, layer 5 1 x 4 (16 outputs) = 80.
-constexpr int kWideTiles = 12 + 64 + 4;
-constexpr int kWideChunk = 512;  // 1,024: 85.5 us per step, 512: 81.3, 256: 84.0 (latency vs Adam's chunk sums)
-__global__ __launch_bounds__(256) void wide_dw_kernel(const _Float16* __restrict__ ws_in, const _Float16* __restrict__ ws_d,
-                                                      int64_t bpad, int64_t ld, int nchunks, float* __restrict__ slabs) {
-    // Blocks are dealt to the 8 XCDs round-robin (physical block p runs on XCD p % 8): 4 consecutive logical blocks
-    // -- the 4 row blocks of one (layer, chunk), which read the same input rows -- go to one XCD's L2 (L2 hit rate
-    // 30 -> 68 %, HBM/Infinity-Cache fetch 103 -> 45 MB per step). A chunk is 20 blocks (W0 = blocks 0-2, W1..W4 =
-    // 4 blocks each from block 3, W5 = block 19): rotated by 3 so that every aligned group of 4 is one hidden
-    // layer's 4 row blocks. The grid is rounded up to whole groups of 32 (the extra blocks return).
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int logical = ((slot >> 2) * 8 + xcd) * 4 + (slot & 3);
-    const int blk = logical / 20 * 20 + (logical % 20 + 3) % 20;
-    const int task = blk * 4 + (threadIdx.x >> 6);
-    if (task >= kWideTiles * nchunks) return;
-    const int tile = task % kWideTiles, chunk = task / kWideTiles;
-    int layer, mb, nb;
-    if (tile < 12) { layer = 0; mb = tile / 3; nb = tile % 3; }
-    else if (tile < 76) { layer = 1 + (tile - 12) / 16; mb = ((tile - 12) % 16) / 4; nb = (tile - 12) % 4; }
-    else { layer = 5; mb = 0; nb = tile - 76; }
+// dW_l = sum_s delta_l in_l^T per (layer, chunk of kWideChunk samples): one block of 4 waves per pair, 6 layers x
+// nchunks blocks. The chunk's input rows (<= 128 rows x 512 samples f16 = 128 KiB) are staged in LDS by LDS-DMA, each
+// 1-KiB row's 16-byte slots XOR-swizzled by the row (slot s of row i at s ^ (i & 31): the 32 lanes of a B-fragment read
+// hit 32 distinct slots); wave w holds the delta rows 32 w .. 32 w + 31 of the chunk in registers (A operands, all 32
+// k steps loaded at once) and computes the row block's 32x32 tiles against every 32-row block of the inputs (layer 5:
+// 16 delta rows, wave w takes input block w). Every load of the block is in flight at once: one memory round trip per
+// block instead of one per 8 k steps (round 2's wave-per-tile kernel: 23.9 us per 16,384-sample step, every input row
+// read from L2 by 4 waves). Partial sums per chunk in canonical parameter order, written through (sc1).
+constexpr int kWideChunk = 512;
+__global__ __launch_bounds__(256, 1) void wide_dw_kernel(const _Float16* __restrict__ ws_in, const _Float16* __restrict__ ws_d,
+                                                         int64_t bpad, int64_t ld, int nchunks, float* __restrict__ slabs) {
+    constexpr int KS = kWideChunk / 16;  // k steps per chunk
+    __shared__ __attribute__((aligned(16))) h8 lb[128 * (kWideChunk / 8)];
+    const int layer = blockIdx.x % 6, chunk = blockIdx.x / 6;
+    if (chunk >= nchunks) return;
     const int in_dim = layer == 0 ? NRC_ENC_WIDTH : 128, out_dim = layer == 5 ? NRC_OUT_PADDED : 128;
-    const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
-    const int o = 32 * mb + r, i = 32 * nb + r;  // this lane's A row / B column
-    const bool oa = o < out_dim, ib = i < in_dim;
-    const h8* pa = reinterpret_cast<const h8*>(ws_d + (wide_d_row(layer) + (oa ? o : 0)) * ld + 8 * h);
-    const h8* pb = reinterpret_cast<const h8*>(ws_in + (wide_in_row(layer) + (ib ? i : 0)) * ld + 8 * h);
-    const int64_t k0 = (int64_t)chunk * kWideChunk, k1 = min<int64_t>(bpad, k0 + kWideChunk);
-    f16v acc[2] = {zero16(), zero16()};
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    const int64_t k0 = (int64_t)chunk * kWideChunk;
+    const int nk = (int)min<int64_t>(KS, (bpad - k0) / 16);  // bpad % 32 == 0
+    // input rows -> LDS: one DMA instruction per row (64 lanes x 16 B), lane L fetches the slot that lands at L
+    for (int i = wave; i < in_dim; i += 4) {
+        const int src_slot = lane ^ (i & 31);
+        if (src_slot < 2 * nk)
+            __builtin_amdgcn_global_load_lds((const void*)(ws_in + (wide_in_row(layer) + i) * ld + k0 + 8 * src_slot),
+                                             (__attribute__((address_space(3))) void*)(lb + i * (kWideChunk / 8)), 16, 0, 0);
+    }
+    // delta rows -> registers
+    const int mb = layer == 5 ? 0 : wave;
+    const int o = 32 * mb + r;
+    const bool oa = o < out_dim;
+    const h8* pa = reinterpret_cast<const h8*>(ws_d + (wide_d_row(layer) + (oa ? o : 0)) * ld + k0 + 8 * h);
     const h8 z = {};
-    // batches of 8 k steps with the next batch's 16 loads in flight during this batch's MFMAs (the operands come
-    // from L2: a load -> MFMA chain one k step at a time waited a full L2 round trip per step; 16-step batches
-    // measured slower)
-    constexpr int KB = 8;
-    int64_t k = k0;
-    const int64_t kfull = k0 + (k1 - k0) / (16 * KB) * (16 * KB);
-    if (k < kfull) {
-        h8 A[KB], B[KB];
+    h8 A[KS];
 #pragma unroll
-        for (int j = 0; j < KB; ++j) {
-            A[j] = oa ? pa[(k >> 3) + 2 * j] : z;
-            B[j] = ib ? pb[(k >> 3) + 2 * j] : z;
+    for (int ks = 0; ks < KS; ++ks) A[ks] = (oa && ks < nk) ? pa[2 * ks] : z;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nb0 = layer == 5 ? wave : 0, nb1 = layer == 5 ? wave + 1 : (in_dim + 31) / 32;
+    lds_h8* lbl = launder((lds_h8*)lb);
+    for (int nb = nb0; nb < nb1; ++nb) {
+        f16v acc = zero16();
+        const int i = 32 * nb + r;  // this lane's B column (input row); rows past in_dim read stale LDS, never stored
+        lds_h8* row = lbl + i * (kWideChunk / 8);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            if (ks < nk) acc = mfma(A[ks], row[(2 * ks + h) ^ r], acc);
+        if (i >= in_dim) continue;
+        float* slab = slabs + (int64_t)chunk * NRC_WIDE_NUM_PARAMS + wide_off(layer);
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int orow = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            // sc1: written through, not left dirty in this XCD's L2 (wide_adam_pack_kernel reads the chunks on every XCD)
+            if (orow < out_dim)
+                __hip_atomic_store(&slab[orow * in_dim + i], acc[reg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        for (; k < kfull; k += 16 * KB) {
-            h8 An[KB], Bn[KB];
-            const int64_t kn = k + 16 * KB < kfull ? k + 16 * KB : k;  // clamped: the last batch re-reads itself
-#pragma unroll
-            for (int j = 0; j < KB; ++j) {
-                An[j] = oa ? pa[(kn >> 3) + 2 * j] : z;
-                Bn[j] = ib ? pb[(kn >> 3) + 2 * j] : z;
-            }
-#pragma unroll
-            for (int j = 0; j < KB; ++j) acc[j & 1] = mfma(A[j], B[j], acc[j & 1]);
-#pragma unroll
-            for (int j = 0; j < KB; ++j) {
-                A[j] = An[j];
-                B[j] = Bn[j];
-            }
-        }
-    }
-    for (int u = 0; k < k1; k += 16, u ^= 1) {
-        const h8 av = oa ? pa[k >> 3] : z;
-        const h8 bv = ib ? pb[k >> 3] : z;
-        acc[u] = mfma(av, bv, acc[u]);
-    }
-    const f16v sum = acc[0] + acc[1];
-    float* slab = slabs + (int64_t)chunk * NRC_WIDE_NUM_PARAMS + wide_off(layer);
-    if (!ib) return;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = 32 * mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-#if defined(NRC_WIDE_PLAIN_STORES)
-        if (row < out_dim) slab[row * in_dim + i] = sum[reg];
-#else
-        // sc1: written through, not left dirty in this XCD's L2 (wide_adam_kernel reads the chunks on every XCD)
-        if (row < out_dim) __hip_atomic_store(&slab[row * in_dim + i], sum[reg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     }
 }
 
@@ -2785,8 +2763,7 @@ hipError_t launch_wide_train_fwd_bwd(int enc, const float* queries, const float*
         hipLaunchKernelGGL(wide_fwd_bwd_lds_kernel<0>, dim3(blocks), dim3(128), 0, s, queries, targets, b, bpad, ld,
                            n_total, loss_scale, (const h8*)fwd16, (const h8*)bwd16, ws_in, ws_d, loss_partials);
     const int nch = wide_chunks(b);
-    const int nblk = (kWideTiles * nch + 3) / 4;
-    hipLaunchKernelGGL(wide_dw_kernel, dim3((nblk + 31) / 32 * 32), dim3(256), 0, s, ws_in, ws_d, bpad, ld, nch, slabs);
+    hipLaunchKernelGGL(wide_dw_kernel, dim3(6 * nch), dim3(256), 0, s, ws_in, ws_d, bpad, ld, nch, slabs);
     return hipGetLastError();
 }
 
