@@ -247,6 +247,34 @@ def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
     return res
 
 
+def graph_ms_per_call(net, stream, fn, k: int, reps: int) -> float:
+    """k calls of fn captured into a HIP graph (the handle launches on the capture stream meanwhile), replayed reps
+    times: event-timed ms per call on the GPU, host launch cost excluded."""
+    import torch
+
+    cs = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    net.set_stream(cs)
+    try:
+        with torch.cuda.graph(g, stream=cs):
+            for i in range(k):
+                fn(i)
+    finally:
+        net.set_stream(stream)
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        g.replay()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    del g
+    return e0.elapsed_time(e1) / (k * reps)
+
+
 def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_ms: float, step16k_ms: float) -> dict:
     """configs[3] (C4) per-rank work, measured on ONE GPU: what each of the 8 ranks runs.
     Inference: its 2^19-query shard (no collective). Training: one 2,048-sample slice of a 16,384-sample global
@@ -282,12 +310,16 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
     tq, tt = frames_q[0], frames_t[0]
     k = 4 * iters
     dp_ms = timed(lambda i: net.train_dp(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B), k)
+    dp_graph_ms = graph_ms_per_call(net, stream, lambda i: net.train_dp(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B),
+                                    16, 10)
     net.set_comm(None)
     comm.destroy()
     grad = torch.zeros(net.grad_floats, dtype=torch.float32, device=dev)
     grad_ms = timed(lambda i: net.train_grad(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B, grad), k)
     apply_ms = timed(lambda i: net.train_apply(grad), k)
     local_ms = timed(lambda i: net.train_batch(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local), k)
+    local_graph_ms = graph_ms_per_call(net, stream, lambda i: net.train_batch(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local),
+                                       16, 10)
     for s, v in zip((nrc.StateSlot.PARAMS, nrc.StateSlot.INFER, nrc.StateSlot.EMA, nrc.StateSlot.ADAM_M,
                      nrc.StateSlot.ADAM_V), state):
         net.set_state(s, v)
@@ -299,6 +331,9 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
             "train_b_local": b_local, "train_global_b": B,
             "train_dp_step_ms": dp_ms, "train_grad_ms": grad_ms, "train_apply_ms": apply_ms,
             "train_local_fused_step_ms": local_ms,
+            "graph_replayed": {"train_dp_step_ms": dp_graph_ms, "train_local_fused_step_ms": local_graph_ms,
+                               "what": "the same calls replayed from a HIP graph: GPU time per step without the "
+                                       "per-call host cost (Python, ctypes, one hipLaunchKernel per kernel)"},
             "prediction_8gpu": {
                 "infer_speedup": (t_full_ms / infer_ms) if infer_ms > 0 else None,
                 "infer_what": "1-GPU kernel time of the whole 2^22-query frame / per-rank 2^19-query kernel time "
@@ -470,6 +505,12 @@ def main() -> None:
     barrier()
     train_frame_ms = max_over_ranks(time.perf_counter() - t0) / args.train_frames * 1e3
     train_step_ms = train_frame_ms / 4
+    # the same training frames replayed from a HIP graph (N = 1): the GPU's own step time, without the per-call host
+    # cost (Python + ctypes + one hipLaunchKernel per kernel) that the eager figure above includes
+    train_step_graph_ms = None
+    if world == 1:
+        train_step_graph_ms = graph_ms_per_call(net, stream, lambda i: net.train(frames_q[(i // 4) % 4][(i % 4) * nrc.BATCH_SIZE:],
+                                                                                frames_t[(i // 4) % 4][(i % 4) * nrc.BATCH_SIZE:]), 16, 10)
 
     # ---- sustained inference: the clock the chip holds under a long run of back-to-back
     # launches is lower than in a short burst; the average of the last `sustained` of 2 x `sustained` launches
@@ -531,6 +572,7 @@ def main() -> None:
                    "train_batch_global": nrc.BATCH_SIZE, "train_batch_per_gpu": bn if distributed else nrc.BATCH_SIZE,
                    "parallelism": f"dp{world}" if world > 1 else "single"},
         "train_step_ms": train_step_ms,
+        "train_step_graph_ms": train_step_graph_ms,
         "train_frame_ms": train_frame_ms,
         "infer_kernel_ms": kernel_ms,
         "weak": weak,

@@ -2039,6 +2039,21 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
     __shared__ f4 part[kRedGroups][kRedParams];
     const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
     const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;  // slab position (reduce modes) / parameter (apply, pack)
+    // diagnostic build: per-block s_memrealtime stamps of thread 0 (entry, slab sums done, after the combine barrier,
+    // Adam issued) in g_infer_clock, read back by nrc_debug_read_infer_clock (tools/reduce_stamps.py)
+    auto stamp = [&](int k) {
+#if NRC_DEBUG_KERNELS
+        if (threadIdx.x == 0 && mode == kReduceFused && blockIdx.x < kInferClockWavesMax)
+            g_infer_clock[6 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+        if (k == 0 && threadIdx.x == 0 && mode == kReduceFused && blockIdx.x < kInferClockWavesMax) {
+            g_infer_clock[6 * blockIdx.x + 4] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+            g_infer_clock[6 * blockIdx.x + 5] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
+        }
+#else
+        (void)k;
+#endif
+    };
+    stamp(0);
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
@@ -2089,7 +2104,9 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             else a0 += v;
         }
         part[grp][pl] = a0 + a1;
+        stamp(1);
         __syncthreads();
+        stamp(2);
         // one parameter per thread for the combine + Adam (threads 0..63 of the block)
         if (threadIdx.x >= kRedParams * kRedVec) return;
         const int lp = threadIdx.x / kRedVec, comp = threadIdx.x % kRedVec;
@@ -2104,6 +2121,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
             return;
         }
         adam_pack_pre(p, g1, ain, mb, oa, lr_t, ema_debias);
+        stamp(3);
         return;
     }
     if (threadIdx.x >= kRedParams * kRedVec) return;
@@ -3143,6 +3161,9 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
     adam_host_factors(oa, lr_t, ema_debias);
     // reduce modes walk the slab positions, apply / pack modes the parameters
     const int grid = (mode == kReduceFused || mode == kReduceOnly ? mb.n_slab : mb.n_mlp) / (kRedParams * kRedVec);
+#if NRC_DEBUG_KERNELS
+    if (mode == kReduceFused) g_last_clock_waves = std::min<int64_t>(grid, kInferClockWavesMax);
+#endif
     if (mb.slab_f16)
         hipLaunchKernelGGL(reduce_adam_kernel<true>, dim3(grid), dim3(kRedThreads), 0, s, mode, slabs, nslabs, loss_partials,
                            grad_io, loss_out, mb, oa, lr_t, ema_debias);
