@@ -281,7 +281,8 @@ enum Knob : int {
     kKnobTrainShape = 1,   // dc shape (0..5), -1 = dc_auto_shape(b)
     kKnobScatterMin = 2,   // Hash grid scatter slice plan (samples per block at level 0 / cap), -1 = 1024 / 2048
     kKnobScatterMax = 3,
-    kKnobCount = 4
+    kKnobDcDw0Delay = 4,  // debug library: s_sleep(127) rounds dW wave 0 of the dc kernel spends after its step 5
+    kKnobCount = 5
 };
 int knob(Knob k);
 

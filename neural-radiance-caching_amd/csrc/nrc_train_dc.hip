@@ -37,8 +37,13 @@ struct DcLayout {
 };
 static_assert(DcLayout<4, 2>::BYTES <= 160 * 1024, "LDS budget at 128 samples per block");
 
-// flags: ready[0..5] (chain waves that published delta_L), dwdone (dW-wave steps finished), red[0..3] (loss partials)
-constexpr int kFlagDwDone = 6, kFlagRed = 8;
+// flags: ready[0..5] (chain waves that published delta_L), red[0..3] (loss partials), dwdone[L] (dW waves that finished
+// their step L, for the steps L = 2..4 whose delta buffer the chain reuses).
+// Round 3 fix: one counter of ALL dW-wave steps let a dW wave that ran ahead into step L - 1 stand in for a slow one still
+// reading delta_L, and the chain overwrote that buffer under it (nondeterministic dW_2..dW_4 in 5 of 6 trials once a
+// slower loss-partial store delayed dW wave 0); the chain now waits for every dW wave's step L + 1 exactly.
+constexpr int kFlagRed = 8;
+constexpr int flag_dwdone(int L) { return 12 + (L - 2); }  // L = 2, 3, 4 -> 12, 13, 14
 
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -257,7 +262,7 @@ __device__ __forceinline__ void dc_chain(const float* __restrict__ q, const floa
             W[mb][1] = w[2 * mb + 1];
         }
         chain_groups<GPW>(W, d, a[L - 1], dn);
-        if (L <= 3) lds_wait_ge(flags + kFlagDwDone, (uint32_t)(DWW * (5 - L)));
+        if (L <= 3) lds_wait_ge(flags + flag_dwdone(L + 1), (uint32_t)DWW);  // buffer (L - 1) & 1 held delta_{L+1}
         char* const buf = smem + Lay::OFF_D + ((L - 1) & 1) * Lay::IMG;
 #pragma unroll
         for (int u = 0; u < GPW; ++u) {
@@ -370,17 +375,27 @@ __device__ __forceinline__ void dc_dw_step(char* smem, int dw, int lane, _Float1
         acc[k][1] = dw_mfma<S>(A[k], Bo[k]);
     }
     // every read of delta_L by this wave has returned (the MFMAs consumed them): release the buffer, then store
-    lds_publish(flags + kFlagDwDone, lane);
+    if (L >= 2 && L <= 4) lds_publish(flags + flag_dwdone(L), lane);
 #pragma unroll
     for (int k = 0; k < PER; ++k)
         if (own[k]) slab_pair_b<16>(slab, L, tm[k], 2 * tp[k], lane, pack_pair(acc[k][0], acc[k][1]));
     stamp(2 + 2 * (5 - L));
 }
 
+#if NRC_DEBUG_KERNELS
+// debug knob dc_dw0_delay: dW wave 0 idles this many s_sleep(127) rounds after its step 5, so that the other dW waves run
+// ahead of it (the stress case of the round-3 ring-buffer race, tests/test_gpu_train_dc.py)
+__device__ int g_dc_dw0_delay = 0;
+#endif
+
 template <int CW, int GPW, int DWW, bool STAMP>
 __device__ __forceinline__ void dc_dw(char* smem, int dw, int lane, _Float16* __restrict__ slab,
                                       float* __restrict__ loss_partials, const Stamper<STAMP>& stamp) {
     dc_dw_step<CW, GPW, DWW, 5, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
+#if NRC_DEBUG_KERNELS
+    if (dw == 0)
+        for (int i = 0; i < g_dc_dw0_delay; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
     dc_dw_step<CW, GPW, DWW, 4, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
     dc_dw_step<CW, GPW, DWW, 3, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
     dc_dw_step<CW, GPW, DWW, 2, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
@@ -467,6 +482,15 @@ hipError_t launch_train_dc(int shape, const float* queries, const float* targets
                            float loss_scale, const _Float16* wf, const _Float16* wb, _Float16* slabs,
                            float* loss_partials, hipStream_t s, uint64_t* stamps) {
     if (b <= 0) return hipSuccess;
+#if NRC_DEBUG_KERNELS
+    static int applied = 0;
+    const int delay = std::max(knob(kKnobDcDw0Delay), 0);
+    if (delay != applied) {
+        const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_dc_dw0_delay), &delay, sizeof(int));
+        if (e != hipSuccess) return e;
+        applied = delay;
+    }
+#endif
     switch (shape) {
         case 0: return launch_dc<1, 1, 1>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
         case 1: return launch_dc<1, 2, 1>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);

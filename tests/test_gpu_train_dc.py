@@ -36,6 +36,8 @@ def knobs(nrc):
     yield nrc._lib
     nrc._lib.set_knob("train_kernel", -1)
     nrc._lib.set_knob("train_shape", -1)
+    if nrc._lib.is_debug_library():
+        nrc._lib.set_knob("dc_dw0_delay", -1)
 
 
 def make_net(nrc, torch, params):
@@ -110,3 +112,41 @@ def test_c4_rank_slice_train_dp(nrc, orc, torch, dev, golden):
     a.destroy()
     c.destroy()
     comm.destroy()
+
+
+@pytest.mark.parametrize("shape", [7, 3])
+def test_dc_gradient_is_deterministic(nrc, torch, dev, knobs, shape):
+    """The decoupled-chain kernel's gradient, three passes over the same samples, bitwise equal, on several streams of
+    untrained weights. Round 3 found a ring-buffer race here (a dW wave that ran ahead counted for a slow one, and the
+    chain overwrote a delta buffer still being read): nondeterministic dW_2..dW_4 in 5 of 6 such trials once a slower
+    loss-partial store delayed dW wave 0."""
+    knobs.set_knob("train_shape", shape)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    B = 2048
+    for trial in range(6):
+        q_np, t_np = nrc.synthetic.cornell_batch(B, seed=100 + trial)
+        gs = [grad_of(nrc, torch, dev, net, q_np, t_np, B, B) for _ in range(3)]
+        np.testing.assert_array_equal(gs[1], gs[0])
+        np.testing.assert_array_equal(gs[2], gs[0])
+    net.destroy()
+
+
+def test_dc_gradient_is_deterministic_with_a_slow_dw_wave(nrc, torch, dev, knobs):
+    """The stress case of the ring-buffer race: dW wave 0 idles after its step 5 (debug knob dc_dw0_delay, ~4 us per
+    round) so that the other dW waves run ahead of it; the gradient must stay bitwise reproducible and equal to the
+    undelayed one. Debug library only (tests/test_gpu_debug_lib.py runs it there)."""
+    if not nrc._lib.is_debug_library():
+        pytest.skip("needs libnrc_amd_debug.so (NRC_LIB_PATH)")
+    knobs.set_knob("train_shape", 7)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    B = 2048
+    for trial in range(4):
+        q_np, t_np = nrc.synthetic.cornell_batch(B, seed=200 + trial)
+        knobs.set_knob("dc_dw0_delay", 0)
+        ref = grad_of(nrc, torch, dev, net, q_np, t_np, B, B)
+        for delay in (1, 4):
+            knobs.set_knob("dc_dw0_delay", delay)
+            np.testing.assert_array_equal(grad_of(nrc, torch, dev, net, q_np, t_np, B, B), ref)
+    net.destroy()

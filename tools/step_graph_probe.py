@@ -25,10 +25,14 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="run only the cases whose name contains this")
+    ap.add_argument("--knob", action="append", default=[], help="name=value A/B knob of the library (repeatable)")
     args = ap.parse_args()
     import torch
 
     nrc = nrc_loader.load()
+    for kv in args.knob:
+        k, v = kv.split("=")
+        nrc._lib.set_knob(k, int(v))
     dev = torch.device("cuda:0")
     main_stream = torch.cuda.current_stream()
     B = nrc.BATCH_SIZE
