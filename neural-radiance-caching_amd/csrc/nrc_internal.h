@@ -190,7 +190,10 @@ hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, h
 // ---- kernel launchers (nrc_kernels.hip). All are stream-ordered and capture-safe.
 // pools / parity: the handle's work-pool counters (kInferPoolBytes, zeroed at allocation) and its launch parity, which
 // the pooled variants flip (see ABL & 16384 in nrc_kernels.hip); variants that do not pool ignore both
-constexpr int kInferPoolBytes = 2 * 32 * 32 * 4;
+// [0, 8 KiB): the pooled variant's two sets of 32 counters; then the steal variant's two sets of kStealMaxBlocks
+// per-block range counters, 64 B apart (ABL & 32768 in nrc_kernels.hip)
+constexpr int kStealMaxBlocks = 1024, kStealStride = 16, kStealSetWords = kStealMaxBlocks * kStealStride;
+constexpr int kInferPoolBytes = 2 * 32 * 32 * 4 + 2 * kStealSetWords * 4;
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s,
                         uint32_t* pools = nullptr, int* parity = nullptr);
 // the product kernel is variant 39; the debug library (NRC_DEBUG_KERNELS) also has the A/B variants 0, 23, 30 and 40

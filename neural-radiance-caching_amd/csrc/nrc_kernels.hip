@@ -749,6 +749,16 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         if (blockIdx.x == 0 && threadIdx.x < kPools)
             epi.wq[(1 - epi.parity) * kPoolSetWords + threadIdx.x * kPoolStride] = 0u;
     }
+    // ABL & 32768: the block's tile range as with the LDS queue (2048), but its counter in global memory (one per block,
+    // 64 B apart, two sets alternating by launch parity), so that waves whose block has drained its range steal tiles
+    // from other blocks' ranges. Every tile of a range is taken by exactly one atomic add on that range's counter and
+    // every block drains its own counter, so stealing only moves work; each launch zeroes the other set for the next.
+    [[maybe_unused]] uint32_t* const scnt = epi.wq + (ABL & 32768 ? 2 * kPoolSetWords + epi.parity * kStealSetWords : 0);
+    if constexpr ((ABL & 32768) != 0) {
+        uint32_t* const other = epi.wq + 2 * kPoolSetWords + (1 - epi.parity) * kStealSetWords;
+        for (int b = blockIdx.x + gridDim.x * (int)threadIdx.x; b < kStealMaxBlocks; b += gridDim.x * THREADS)
+            __hip_atomic_store(other + b * kStealStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
@@ -786,6 +796,65 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         gbase = (int64_t)blockIdx.x * ngroups_all / gridDim.x;
         ngroups = (int64_t)(blockIdx.x + 1) * ngroups_all / gridDim.x;  // end of this block's range
         g = draw();
+    }
+    // steal state (ABL & 32768): the range the wave draws from (own block first)
+    [[maybe_unused]] int scur = blockIdx.x;
+    __shared__ uint32_t steal_dry;  // some wave of this block found every range drained
+    if constexpr ((ABL & 32768) != 0) {
+        if (threadIdx.x == 0) steal_dry = 0;
+        __syncthreads();
+    }
+    auto rbeg = [&](int v) -> int64_t { return (int64_t)v * ngroups_all / gridDim.x; };
+    auto sissue = [&]() -> uint32_t {
+        uint32_t t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(scnt + scur * kStealStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return t;
+    };
+    // the tile of a draw from range scur that returned t; a drained range sends the wave looking for a range with tiles
+    // left: every other block's counter read at once (lane i: candidates i, i + 64, ..., sc1 loads; the blocks of this
+    // block's XCD first under round-robin placement), atomic claims on those that showed tiles left, in order;
+    // ngroups_all = nothing left
+    auto sresolve = [&](uint32_t t) -> int64_t {
+        int64_t idx = rbeg(scur) + (int64_t)t;
+        if (idx < rbeg(scur + 1)) return idx;
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&steal_dry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)))
+            return ngroups_all;
+        const int G = gridDim.x;
+        constexpr int kProbe = kStealMaxBlocks / 64;
+        int vs[kProbe];
+        uint32_t cs[kProbe];
+#pragma unroll
+        for (int k = 0; k < kProbe; ++k) {
+            const int i = 1 + lane + 64 * k;
+            vs[k] = i < G ? (int)(((int64_t)blockIdx.x + 8 * (int64_t)i + (8 * (int64_t)i) / G) % G) : -1;
+            cs[k] = vs[k] >= 0 ? __hip_atomic_load(scnt + vs[k] * kStealStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kProbe; ++k) {
+            uint64_t m = __ballot(vs[k] >= 0 && (int64_t)cs[k] < rbeg(vs[k] + 1) - rbeg(vs[k]));
+            while (m) {
+                const int src = __builtin_ctzll(m);
+                m &= m - 1;
+                const int cand = __builtin_amdgcn_readlane(vs[k], src);
+                uint32_t tt = 0;
+                if (lane == 0)
+                    tt = __hip_atomic_fetch_add(scnt + cand * kStealStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                tt = __builtin_amdgcn_readfirstlane(tt);
+                if (rbeg(cand) + (int64_t)tt < rbeg(cand + 1)) {
+                    scur = cand;
+                    return rbeg(cand) + tt;
+                }
+            }
+        }
+        if (lane == 0) __hip_atomic_store(&steal_dry, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return ngroups_all;
+    };
+    if constexpr ((ABL & 32768) != 0) {
+        uint32_t traw = sissue(), tt;
+        asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(tt) : "v"(traw));
+        g = sresolve(tt);
+        ngroups = ngroups_all;
     }
     if constexpr ((ABL & 4096) != 0) g = draw();
     // ABL & 16384: pooled draws (see kPools)
@@ -866,19 +935,25 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     // prefetch loads, so its (atomic) latency hides under a whole tile and the prefetch never waits for it
     int64_t ng = 0;
     uint32_t nn_raw = 0;  // the pending draw: lane 0's atomic result, read (readfirstlane) one iteration later
-    if constexpr ((ABL & (2048 | 4096)) != 0) ng = draw();
+    if constexpr ((ABL & (2048 | 4096)) != 0 && (ABL & 32768) == 0) ng = draw();
+    if constexpr ((ABL & 32768) != 0) {
+        uint32_t traw = g < ngroups_all ? sissue() : 0u, tt;
+        asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(tt) : "v"(traw));
+        ng = g < ngroups_all ? sresolve(tt) : ngroups_all;
+    }
     if constexpr ((ABL & 16384) != 0) {
         uint32_t traw = pool_issue(cur), tt;
         asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(tt) : "v"(traw));
         ng = pool_resolve(tt);
     }
     for (int64_t nn = 0; g < ngroups; g = ng, ng = nn) {
-        if constexpr ((ABL & (2048 | 4096 | 16384)) != 0) {
+        if constexpr ((ABL & (2048 | 4096 | 16384 | 32768)) != 0) {
             if (!first_iter) {
                 // an asm readfirstlane stays here; the builtin is hoisted to the atomic and the wave then waits for it
                 uint32_t t;
                 asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(t) : "v"(nn_raw));
                 if constexpr ((ABL & 16384) != 0) ng = pool_resolve(t);
+                else if constexpr ((ABL & 32768) != 0) ng = sresolve(t);
                 else ng = gbase + (int64_t)t;
             }
         }
@@ -908,6 +983,9 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         }
         if constexpr ((ABL & 16384) != 0) {
             nn_raw = ng < ngroups_all ? pool_issue(cur) : 0u;  // wave-uniform condition: no draw once everything is dry
+            first_iter = false;
+        } else if constexpr ((ABL & 32768) != 0) {
+            nn_raw = ng < ngroups_all ? sissue() : 0u;
             first_iter = false;
         } else if constexpr ((ABL & (2048 | 4096)) != 0) {
             if constexpr ((ABL & 4096) != 0) {
@@ -2620,10 +2698,20 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         if (!pools || !parity) return hipErrorInvalidValue;
         InferEpilogue e{};
         e.wq = pools;
-        e.parity = (*parity ^= 1);  // only pooled launches flip it: the set they skip is the one they zero
+        e.parity = (*parity ^= 1) & 1;  // only pooled launches flip it: the set they skip is the one they zero
         if (variant == 41)
             return launch_persistent_infer(infer_pooled_kernel<48 | 1024 | 8192 | 16384>, 1024, bpc[41], ntiles, queries, out, n, wf, s, e);
         return launch_clocked(infer_pooled_kernel<48 | 1024 | 8192 | 16384 | 512>, 1024, bpc[42], ntiles, queries, out, n, wf, s, e);
+    }
+    if (variant == 45 || variant == 46) {  // 46: 45 with the in-kernel clock
+        if (!pools || !parity) return hipErrorInvalidValue;
+        InferEpilogue e{};
+        e.wq = pools;
+        *parity ^= 2;  // the steal sets' own parity bit (the pooled variants flip bit 0)
+        e.parity = (*parity >> 1) & 1;
+        if (variant == 45)
+            return launch_persistent_infer(infer_pooled_kernel<48 | 1024 | 8192 | 32768>, 1024, bpc[45], ntiles, queries, out, n, wf, s, e);
+        return launch_clocked(infer_pooled_kernel<48 | 1024 | 8192 | 32768 | 512>, 1024, bpc[46], ntiles, queries, out, n, wf, s, e);
     }
 #endif
     switch (variant) {
