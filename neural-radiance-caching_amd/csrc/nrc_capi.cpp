@@ -819,6 +819,10 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         {
             const std::vector<int> sm = net->t16 ? build_t16_slab_map() : build_slab_map(net->encoding);
+            if (net->t16)  // the reduction maps t16 slab positions in closed form (t16_slab_param): same map
+                for (size_t i = 0; i < sm.size(); ++i)
+                    if (sm[i] != t16_slab_param((int)i))
+                        throw ApiError(NRC_ERR_INTERNAL, "t16_slab_param disagrees with the slab map at " + std::to_string(i));
             net->n_slab = (int)sm.size();
             HIP_CHECK(hipMalloc(&net->slab_param, sizeof(int) * sm.size()));
             HIP_CHECK(hipMemcpy(net->slab_param, sm.data(), sizeof(int) * sm.size(), hipMemcpyHostToDevice));

@@ -68,6 +68,22 @@ __host__ __device__ constexpr int t16_slab_pos(int L, int tm, int tn, int lane, 
     return t16_slab_base(L, tm, tn & ~1) + lane * 8 + 4 * (tn & 1) + i;
 }
 static_assert(t16_slab_base(5, 0, 4) == 23552, "t16 slab size");
+// Inverse of t16_slab_pos (Frequency layer offsets of layout.h): the canonical parameter of slab position pos, -1 for the
+// dummy layer-0 K slots. Closed form so the reduction needs no map load before the parameter's Adam state
+// (checked against build_t16_slab_map at nrc_init).
+__host__ __device__ constexpr int t16_slab_param(int pos) {
+    const int L = pos < 6144 ? 0 : pos < 22528 ? 1 + (pos - 6144) / 4096 : 5;
+    const int off = pos - (L == 0 ? 0 : L <= 4 ? 6144 + (L - 1) * 4096 : 22528);
+    const int ntn = t16_ntn(L), rec = off >> 9, q = off & 511, lane = q >> 3, e = q & 7;
+    const int tm = rec / (ntn >> 1), tn = 2 * (rec % (ntn >> 1)) + (e >> 2);
+    const int row = 16 * tm + 4 * (lane >> 4) + (e & 3), col = 16 * tn + (lane & 15);
+    const int f = L == 0 ? t16_slot_feature(col) : col;
+    const int in_dim = L == 0 ? NRC_ENC_WIDTH : 64;
+    const int loff = L == 0 ? NRC_W0_OFFSET : L <= 4 ? NRC_W1_OFFSET + (L - 1) * 4096 : NRC_W5_OFFSET;
+    return f < 0 ? -1 : loff + row * in_dim + f;
+}
+static_assert(t16_slab_param(t16_slab_pos(3, 2, 1, 37, 2)) == NRC_W1_OFFSET + 2 * 4096 + (32 + 4 * 2 + 2) * 64 + 16 + 5,
+              "t16 slab inverse");
 
 // Gradient exchange buffer: loss-scaled dL/dW (NRC_NUM_PARAMS f32) followed by the minibatch loss.
 

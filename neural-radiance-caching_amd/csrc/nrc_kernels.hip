@@ -2147,14 +2147,16 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         }
     }
     if (mode == kReduceFused || mode == kReduceOnly) {
-        // the combining threads fetch their parameter's optimizer state before the slab loads, so Adam does not
-        // wait for a second round trip after the reduction
-        int pp = -1;
-        AdamIn ain{};
-        if (threadIdx.x < kRedParams * kRedVec) {
-            pp = mb.slab_param[blockIdx.x * kRedParams * kRedVec + threadIdx.x];
-            if (mode == kReduceFused && pp >= 0) ain = adam_load(pp, mb);
-        }
+        // Load order (round 3): the parameter-map load, then the first batch of up to 8 slab loads, then the Adam
+        // state of the mapped parameter -- so that the slab loads do not wait a round trip for the map (the in-order
+        // vmcnt lets the map's value be used with the slab loads still in flight), and a short last batch is issued
+        // in one go (the remainder used to be a serial loop: 4 round trips for the 64 slabs of a 2,048-sample step).
+        // the slab position this thread combines (threads < 64): t16 slabs map it in closed form, the 32x32 slabs
+        // through the map (one branch-free load, every thread)
+        const int mypos = blockIdx.x * kRedParams * kRedVec + (threadIdx.x & (kRedParams * kRedVec - 1));
+        int pp_raw;
+        if constexpr (H) pp_raw = t16_slab_param(mypos);
+        else pp_raw = mb.slab_param[mypos];
         f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         auto ld = [&](int slab) -> f4 {
             if constexpr (H) {
@@ -2164,22 +2166,34 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
                 return *(const f4*)&slabs[(int64_t)slab * mb.n_slab + p0];
             }
         };
-        int i = grp;
-        for (; i + 7 * kRedGroups < nslabs; i += 8 * kRedGroups) {
-            f4 v[8];
+        // slabs grp, grp + G, ... (G = kRedGroups), in batches of 8 loads; element k of the sequence goes to a0 for
+        // even k, a1 for odd k (the same float sums as the round-2 loop)
+        // loads are branch-free (a slab index past the last is clamped to it and its value not added): a load under a
+        // branch made the compiler wait for it at the join
+        const int nmine = grp < nslabs ? (nslabs - grp + kRedGroups - 1) / kRedGroups : 0;
+        auto ldc = [&](int k) -> f4 { return ld(min(grp + k * kRedGroups, nslabs - 1)); };
+        // the combining threads' Adam state first (t16: its address needs no load), then the slabs: all in flight at once
+        const int pp = threadIdx.x < kRedParams * kRedVec ? pp_raw : -1;
+        AdamIn ain{};
+        if (mode == kReduceFused && pp >= 0) ain = adam_load(pp, mb);
+        f4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ldc(u);
+        // the image positions are first used here: otherwise the compiler computes the 64-bit store addresses right
+        // after their loads and waits for them before issuing the slab loads
+        asm volatile("" : "+v"(ain.fp), "+v"(ain.ft), "+v"(ain.bp));
+        for (int base = 0;;) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const bool in = base + u < nmine;
+                if (u & 1) a1 += in ? v[u] : f4{0.f, 0.f, 0.f, 0.f};
+                else a0 += in ? v[u] : f4{0.f, 0.f, 0.f, 0.f};
+            }
+            base += 8;
+            if (base >= nmine) break;
             // plain loads (0.4 us per step faster than nontemporal ones here)
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = ld(i + u * kRedGroups);
-#pragma unroll
-            for (int u = 0; u < 8; u += 2) {
-                a0 += v[u];
-                a1 += v[u + 1];
-            }
-        }
-        for (int u = 0; i < nslabs; i += kRedGroups, ++u) {
-            const f4 v = ld(i);
-            if (u & 1) a1 += v;
-            else a0 += v;
+            for (int u = 0; u < 8; ++u) v[u] = ldc(base + u);
         }
         part[grp][pl] = a0 + a1;
         stamp(1);
