@@ -2104,6 +2104,20 @@ __device__ __forceinline__ void adam_pack_one(int mode, int p, float gsum, const
     if (bp >= 0) mb.wb_train[bp] = (_Float16)w;
 }
 
+// Sum of the loss partials p[lane], p[lane + 64], ... (in that order) for one wave: the loads of each batch of 8 issue
+// together (branch-free: clamped index, masked add), instead of one round trip per partial
+__device__ __forceinline__ float lane_partial_sum(const float* __restrict__ p, int n, int lane) {
+    float L = 0.0f;
+    for (int base = lane; base < n; base += 8 * 64) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[min(base + 64 * u, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) L += base + 64 * u < n ? v[u] : 0.0f;
+    }
+    return L;
+}
+
 // The per-slab loss partials are summed by wave 0 of block 0: a strided per-lane sum and a fixed xor
 // butterfly (one load latency instead of a serial chain of nslabs loads).
 // H: f16 slabs (the t16 training kernel's), converted to f32 before the same fixed-order f32 sums
@@ -2135,7 +2149,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
-            for (int i = threadIdx.x; i < nslabs; i += 64) L += loss_partials[i];
+            L = lane_partial_sum(loss_partials, nslabs, threadIdx.x);
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
             if (threadIdx.x == 0) {
@@ -2497,7 +2511,7 @@ __global__ __launch_bounds__(256) void wide_adam_pack_kernel(int mode, const flo
     if (blockIdx.x == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
-            for (int i = threadIdx.x; i < nlp; i += 64) L += loss_partials[i];
+            L = lane_partial_sum(loss_partials, nlp, threadIdx.x);
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
             if (threadIdx.x == 0) {
