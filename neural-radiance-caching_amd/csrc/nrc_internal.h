@@ -298,7 +298,7 @@ enum Knob : int {
     kKnobTrainKernel = 0,  // Frequency training: -1 / 0 decoupled chain (dc), 1 round-2 t16 role split, 2 round-2 t16
                            // 4-wave, 32 round-1 32x32x16 (read at nrc_init)
     kKnobTrainShape = 1,   // dc shape (0..5), -1 = dc_auto_shape(b)
-    kKnobScatterMin = 2,   // Hash grid scatter slice plan (samples per block at level 0 / cap), -1 = 1024 / 2048
+    kKnobScatterMin = 2,   // Hash grid scatter slice plan (samples per block at level 0 / cap), -1 = 2048 / 4096
     kKnobScatterMax = 3,
     kKnobDcDw0Delay = 4,  // debug library: s_sleep(127) rounds dW wave 0 of the dc kernel spends after its step 5
     kKnobCount = 5

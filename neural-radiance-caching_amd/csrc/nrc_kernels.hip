@@ -3247,9 +3247,10 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
                        loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
                        reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
                        bcap);
-    // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep in profiles/r01_hash/README.md
+    // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep of the exact 64-bit scatter,
+    // profiles/r03_hash/scatter_plan_sweep.txt (round 1's f16 scatter: profiles/r01_hash/README.md)
     const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);
-    const int smin = kmin > 0 ? kmin : 1024, smax = kmax > 0 ? kmax : 2048;
+    const int smin = kmin > 0 ? kmin : 2048, smax = kmax > 0 ? kmax : 4096;
     ScatterPlan plan;
     int nb = 0;
     for (int l = 0; l < NRC_HASH_LEVELS; ++l) {

@@ -17,10 +17,14 @@ def main():
     ap.add_argument("--width", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--knob", action="append", default=[], help="name=value A/B knob of the library (repeatable)")
     args = ap.parse_args()
     import torch
 
     nrc = nrc_loader.load()
+    for kv in args.knob:
+        k, v = kv.split("=")
+        nrc._lib.set_knob(k, int(v))
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     e = getattr(nrc.InputEncoding, args.encoding)
@@ -41,7 +45,7 @@ def main():
         ts.append(e0.elapsed_time(e1) / args.iters * 1e3)
     loss = net.train(q, t, loss=True)
     net.destroy()
-    print(f"{args.encoding} w{args.width} step_us {np.median(ts):.2f} loss {loss:.6g}")
+    print(f"{args.encoding} w{args.width} {' '.join(args.knob)} step_us {np.median(ts):.2f} loss {loss:.6g}")
 
 
 if __name__ == "__main__":
