@@ -192,11 +192,12 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 nrc_status nrc_debug_set_knob(const char* name, int value);
 nrc_status nrc_debug_get_knob(const char* name, int* value);
 /* Inference through a specific kernel variant for in-process A/B timing; results are identical in meaning to
- * nrc_infer_stream. The product library has variant 39 (the production kernel) only; the debug library
- * (libnrc_amd_debug.so) also has 0, 23, 30, 40 (39 + in-kernel clock) and 50 / 51 (the 16x16x32 kernel). */
+ * nrc_infer_stream. The product library has variant 47 (the production kernel) only; the debug library
+ * (libnrc_amd_debug.so) also has 0, 23, 30, 39 (47 with the 32x32x16 output layer), 40 / 48 (39 / 47 + in-kernel
+ * clock) and 50 / 51 (the 16x16x32 kernel). */
 nrc_status nrc_debug_infer_variant(nrc_net* net, int variant, const float* inputs_d, float* outputs_d, uint32_t n,
                                    hipStream_t stream);
-/* Diagnostic (debug library): after a launch of the clocked inference variant 40, per wave 6 uint64: s_memtime cycles
+/* Diagnostic (debug library): after a launch of a clocked inference variant (40, 48), per wave 6 uint64: s_memtime cycles
  * of its persistent loop, s_memrealtime (100 MHz) at loop start, at loop end and at wave start, HW_ID, XCC_ID:
  * 6 * *waves values into host_dst (at most cap_waves waves). */
 nrc_status nrc_debug_read_infer_clock(uint64_t* host_dst, uint32_t cap_waves, uint32_t* waves);

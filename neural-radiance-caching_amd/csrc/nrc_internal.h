@@ -212,9 +212,9 @@ constexpr int kStealMaxBlocks = 1024, kStealStride = 16, kStealSetWords = kSteal
 constexpr int kInferPoolBytes = 2 * 32 * 32 * 4 + 2 * kStealSetWords * 4;
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s,
                         uint32_t* pools = nullptr, int* parity = nullptr);
-// the product kernel is variant 39; the debug library (NRC_DEBUG_KERNELS) also has the A/B variants 0, 23, 30 and 40
-// (39 + in-kernel clock)
-constexpr int kProductInferVariant = 39;
+// the product kernel is variant 47; the debug library (NRC_DEBUG_KERNELS) also has the A/B variants 0, 23, 30, 39 (round
+// 2's product: 47 with the 32x32x16 output layer), 40 (39 + in-kernel clock) and 48 (47 + in-kernel clock)
+constexpr int kProductInferVariant = 47;
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s, uint32_t* pools = nullptr, int* parity = nullptr);
 constexpr int kNumInferVariants = 52;  // 50: launch_infer16 (the t16 image)

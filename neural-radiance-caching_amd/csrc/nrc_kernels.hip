@@ -680,14 +680,46 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
                 for (int kk = 0; kk < 4; ++kk) y[t][kk] = z[t][kk];
             mark(1 + l);
         }
-        lds_h8* wl = launder(lw_lane);
+        if constexpr ((ABL & 65536) != 0) {
+            // Output layer on v_mfma_f32_4x4x4_16b_f16 (16 independent 4x4x4 blocks): block b = lane / 4 takes the
+            // samples of lanes 4b..4b+3 and the hidden half (lane / 32) those lanes hold, so the h8 activations feed
+            // the B operand as they are; the A operand of lane l is output row l % 4 of that half's weights, i.e. the
+            // 32x32x16 fragment of lane (l & 3) | (l & 32). 8 of these (4 rows, 3 used) replace 4 32x32x16 (32 rows);
+            // o[t][0..3] = rows 0..3 of sample lane % 32 summed over hidden half lane / 32 (the epilogue adds halves).
+            const int ln = threadIdx.x & 63;
+            lds_h8* w4 = launder(lw_lane + (((ln & 3) | (ln & 32)) - ln));
+            f4v c4[TILES];
 #pragma unroll
-        for (int t = 0; t < TILES; ++t) o[t] = zero16();
+            for (int t = 0; t < TILES; ++t) c4[t] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const h8 a = wl[fwd_frag(5, 0, kk) * 64];
+            for (int kk = 0; kk < 4; ++kk) {
+                const h8 a = w4[fwd_frag(5, 0, kk) * 64];
 #pragma unroll
-            for (int t = 0; t < TILES; ++t) o[t] = mfma(a, y[t][kk], o[t]);
+                for (int t = 0; t < TILES; ++t) {
+                    c4[t] = __builtin_amdgcn_mfma_f32_4x4x4f16(__builtin_shufflevector(a, a, 0, 1, 2, 3),
+                                                                __builtin_shufflevector(y[t][kk], y[t][kk], 0, 1, 2, 3),
+                                                                c4[t], 0, 0, 0);
+                    c4[t] = __builtin_amdgcn_mfma_f32_4x4x4f16(__builtin_shufflevector(a, a, 4, 5, 6, 7),
+                                                                __builtin_shufflevector(y[t][kk], y[t][kk], 4, 5, 6, 7),
+                                                                c4[t], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                o[t] = zero16();
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[t][i] = c4[t][i];
+            }
+        } else {
+            lds_h8* wl = launder(lw_lane);
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) o[t] = zero16();
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const h8 a = wl[fwd_frag(5, 0, kk) * 64];
+#pragma unroll
+                for (int t = 0; t < TILES; ++t) o[t] = mfma(a, y[t][kk], o[t]);
+            }
         }
         if constexpr ((ABL & 256) != 0) {
             // make the output MFMAs complete inside their own phase
@@ -1058,7 +1090,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             ph[0] += tn - tprev;
             tprev = tn;
         }
-        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
+        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256 | 65536), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
         if constexpr ((ABL & 8) && EPI < 0) {
             const int64_t s0 = g * TILES * 32;
             if (out16 && s0 + TILES * 32 <= n) {
@@ -1088,7 +1120,34 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             for (int t = 0; t < TILES; ++t) {
                 const int64_t s0 = (g * TILES + t) * 32, sq = s0 + r;
                 float L0, L1, L2;
-                if constexpr ((ABL & 8192) != 0) {
+                if constexpr ((ABL & 65536) != 0) {
+                    // halves of the 4x4x4 output layer: swapping lanes 32..63 of rows 0 / 2 with lanes 0..31 of rows
+                    // 1 / 3 lines up both halves of a row in one lane pair; the sums are row 0 (lanes 0..31), row 1
+                    // (lanes 32..63), row 2 (lanes 0..31) of sample lane % 32
+                    // (a whole-vector bit_cast: clang 22 turns __builtin_bit_cast(uint32_t, v[i]) into element 0, §8)
+                    typedef uint32_t u16v __attribute__((ext_vector_type(16)));
+                    const u16v ob = __builtin_bit_cast(u16v, o[t]);
+                    const auto s01 = __builtin_amdgcn_permlane32_swap(ob[0], ob[1], false, false);
+                    const auto s23 = __builtin_amdgcn_permlane32_swap(ob[2], ob[3], false, false);
+                    const f2 p01 = __builtin_bit_cast(f2, s01), p23 = __builtin_bit_cast(f2, s23);
+                    const float A = p01[0] + p01[1];
+                    const float B = p23[0] + p23[1];
+                    const h2 z = {};
+                    const h2 ab = __builtin_elementwise_max(__builtin_bit_cast(h2, pk2(A, B)), z);
+                    const float LA = (float)ab[0], LB = (float)ab[1];
+                    if constexpr (EPI < 0) {
+                        const auto rs = buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, LA), rs, r * 12 + h * 4, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, LB), rs,
+                                                              h ? kBufferOff : r * 12 + 8, 0, 0);
+                        continue;
+                    }
+                    const uint32_t la = __builtin_bit_cast(uint32_t, LA);
+                    const auto s11 = __builtin_amdgcn_permlane32_swap(la, la, false, false);
+                    L0 = LA;
+                    L1 = __builtin_bit_cast(f2, s11)[1];
+                    L2 = LB;
+                } else if constexpr ((ABL & 8192) != 0) {
                     // f16(max(x, 0)) == max(f16(x), 0): two packed converts + two packed maxes + three widenings
                     const h2 z = {};
                     const h2 a = __builtin_elementwise_max(__builtin_bit_cast(h2, pk2(o[t][0], o[t][1])), z);
@@ -1218,6 +1277,7 @@ __global__ __launch_bounds__(THREADS, 4) void infer_accumulate_kernel(const floa
                                                                       int64_t n, const h8* __restrict__ wf,
                                                                       InferEpilogue epi) {
     infer_v2_body<1, THREADS, false, kDefaultAbl | 1024 | 8192 | XABL, EPI>(q, out, n, wf, epi);  // encoder v3, buffer-load prefetch
+    // (XABL 2048 | 65536: the product inference kernel's shape and output layer, so the fused frame is bit-identical)
 }
 
 // InputEncoding::Hash inference (EPI -1: plain infer; 0 / 2: fused accumulation as above)
@@ -2713,8 +2773,8 @@ hipError_t read_infer_clock(uint64_t*, int64_t, int64_t*) { return hipErrorNotSu
 //   21: variant 3 + LDS-staged 16-B result stores;  22: variant 3 + omod doubling-chain encoder
 //   23: variant 22 + branch-free prefetch and buffer-store epilogue (default)
 // round 2: variant 39 (encoder v3, per-CU LDS work queue on 1024-thread blocks, buffer-load prefetch, packed epilogue);
-// in-process A/B at 2^21 queries: 75.1 vs 86.5 us for variant 23 (profiles/r02_infer/)
-static int g_default_infer_variant = 39;
+// in-process A/B at 2^21 queries: 75.1 vs 86.5 us for variant 23 (profiles/r02_infer/). round 3: variant 47 (below)
+static int g_default_infer_variant = 47;
 
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s, uint32_t* pools, int* parity) {
@@ -2756,8 +2816,13 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         // 39 (default): 30 with 1024-thread blocks (one per CU) drawing tiles from an LDS work queue, buffer-load query
         // prefetch and the packed output epilogue; 40: 39 with the in-kernel clock (nrc_debug_read_infer_clock)
         case 40: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 512>, 1024, bpc[40], ntiles, queries, out, n, wf, s);
-#endif
         case 39: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192>, 1024, bpc[39], ntiles, queries, out, n, wf, s);
+        // 48: 47 with the in-kernel clock
+        case 48: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | 512>, 1024, bpc[48], ntiles, queries, out, n, wf, s);
+#endif
+        // 47 (default, round 3): 39 with the output layer on 4x4x4 16-block MFMAs (65536); in-process A/B at 2^21
+        // queries 82.3-82.6 vs 82.7-83.4 us (profiles/r03_infer/ab_out4x4_v47.json)
+        case 47: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536>, 1024, bpc[47], ntiles, queries, out, n, wf, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -2941,8 +3006,8 @@ hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, 
     // one 1024-thread block per CU drawing tiles from an LDS work queue (round 2: 82.6 vs 86.7 us per 1080p frame for
     // the round-1 512-thread shape, bit-identical, profiles/r02_frame/; the round-1 shape was removed in round 3)
     switch (mode) {
-        case 0: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, 2048>, 1024, bpc[0], ntiles, queries, out, n, wf, s, epi);
-        case 2: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, 2048>, 1024, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        case 0: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, 2048 | 65536>, 1024, bpc[0], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, 2048 | 65536>, 1024, bpc[1], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }

@@ -47,8 +47,8 @@ def test_debug_entry_points(nrc, dev):
         if nrc._lib.is_debug_library():
             s = stamps.cpu().numpy()[:64 * 6 * 16].reshape(64, 6, 16)  # dc shape 7: 64 blocks x 6 waves
             assert (np.diff(s[:, 0, :14], axis=1) >= 0).all(), "chain-wave stamps must be monotone"
-        # variant 39 (the product kernel) is available in both
-        nrc._lib.check(lib.nrc_debug_infer_variant(net._h, 39, q.data_ptr(), out.data_ptr(), 2048, None))
+        # variant 47 (the product kernel) is available in both
+        nrc._lib.check(lib.nrc_debug_infer_variant(net._h, 47, q.data_ptr(), out.data_ptr(), 2048, None))
     finally:
         net.destroy()
 

@@ -21,7 +21,7 @@ import nrc_loader  # noqa: E402
 
 # variants that record the in-kernel clock (nrc_debug_read_infer_clock): 40 = 39 clocked, 42 = 41 (pooled) clocked.
 # 50: the rejected 16x16x32 inference kernel (nrc_infer16.hip)
-CLOCKED = {40, 42, 46}
+CLOCKED = {40, 42, 46, 48}
 
 
 def main() -> None:

@@ -56,7 +56,7 @@ def main() -> None:
             elif how == "nrc_infer(int ptrs)":
                 L.nrc_infer(net._h, qp, op, args.n)
             else:
-                L.nrc_debug_infer_variant(net._h, 39, qp, op, args.n, sp)
+                L.nrc_debug_infer_variant(net._h, 47, qp, op, args.n, sp)
         t_host = time.perf_counter() - t0
         e1.record(stream)
         torch.cuda.synchronize()
@@ -64,7 +64,7 @@ def main() -> None:
         return {"event_us": e0.elapsed_time(e1) / args.iters * 1e3, "host_enqueue_us": t_host / args.iters * 1e6,
                 "wall_us": wall / args.iters * 1e6}
 
-    hows = ["net.infer", "nrc_infer(int ptrs)", "debug variant 39"]
+    hows = ["net.infer", "nrc_infer(int ptrs)", "debug variant 47"]
     res = {h: [] for h in hows}
     for _ in range(args.rounds):
         for h in hows:

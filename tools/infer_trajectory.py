@@ -2,7 +2,7 @@
 --chunk launches, on bench.py's weights (4 frames of self-training) and on more-trained weights, to separate the chip's
 clock ramp from the effect of the weights' activation statistics on the power-limited clock.
 
-    python tools/infer_trajectory.py [--variant 39] [--chunks 30] [--chunk 100]
+    python tools/infer_trajectory.py [--variant 47] [--chunks 30] [--chunk 100]
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ import nrc_loader  # noqa: E402
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 21)
-    ap.add_argument("--variant", type=int, default=39)
+    ap.add_argument("--variant", type=int, default=47)
     ap.add_argument("--chunks", type=int, default=30)
     ap.add_argument("--chunk", type=int, default=100)
     ap.add_argument("--frames", default="4,26,100", help="self-training frames before each trajectory")
