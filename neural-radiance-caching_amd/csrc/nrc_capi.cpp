@@ -234,8 +234,9 @@ std::vector<int> build_t16_slab_map() {
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
 bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1};
-const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay"};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1};
+const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
+                                            "hash_infer"};
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -333,6 +334,8 @@ struct nrc_net {
     uint32_t* grid_steps = nullptr;
     float2* grid_bias = nullptr;  // Adam bias-correction table of the grid parameters (GridBuffers::bias)
     _Float16 *table_train = nullptr, *table_infer = nullptr;
+    uint32_t* hash_feat = nullptr;  // [NRC_HASH_LEVELS][kHashFeatStride] level features of an inference pass
+    uint32_t* hash_feat_arg() const { return knob(kKnobHashInfer) == 1 ? nullptr : hash_feat; }
     HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
     int scatter_blocks = 0;
     uint8_t* grid_nf = nullptr;       // [n_grid] non-finite contribution codes (GridNonFinite)
@@ -373,7 +376,8 @@ struct nrc_net {
         work_queue = nullptr;
         f(dp_grad);
         dp_grad = nullptr;
-        f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer);
+        f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer); f(hash_feat);
+        hash_feat = nullptr;
         f(grid_nf); f(grid_nf_tag);
         grid_nf = nullptr;
         grid_nf_tag = nullptr;
@@ -587,7 +591,8 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
     if (net->wide())
         return infer_wide(net, (int)net->cfg.infer_precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     if (net->hash())
-        return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
+        return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream,
+                                 net->hash_feat_arg());
     if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
         return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     return launch_infer(in, out, n, net->wf_infer, net->stream, net->work_queue, &net->pool_parity);
@@ -774,6 +779,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             HIP_CHECK(hipMalloc(&net->grid_steps, sizeof(uint32_t) * ng));
             HIP_CHECK(hipMalloc(&net->table_train, sizeof(_Float16) * ng));
             HIP_CHECK(hipMalloc(&net->table_infer, sizeof(_Float16) * ng));
+            HIP_CHECK(hipMalloc(&net->hash_feat, sizeof(uint32_t) * NRC_HASH_LEVELS * (size_t)kHashFeatStride));
             HIP_CHECK(hipMemset(net->grid_grad, 0, sizeof(int64_t) * ng));
             HIP_CHECK(hipMalloc(&net->grid_nf, ng));
             HIP_CHECK(hipMemset(net->grid_nf, 0, ng));
@@ -893,7 +899,7 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
                                  rgba, num_pixels, mode, w, net->stream));
         else if (net->hash())
             HIP_CHECK(launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, reinterpret_cast<const float*>(thr),
-                                        rgba, num_pixels, mode, w, net->stream));
+                                        rgba, num_pixels, mode, w, net->stream, net->hash_feat_arg()));
         else if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
             HIP_CHECK(launch_infer_sh(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba, num_pixels,
                                       mode, w, net->stream));

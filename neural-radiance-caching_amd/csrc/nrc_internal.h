@@ -226,8 +226,12 @@ hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves);
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                                    float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
 // InputEncoding::Hash inference (mode -1: plain; 0 / 2: fused accumulation for queries [0, n_acc))
+// feat: the handle's [NRC_HASH_LEVELS][kHashFeatStride] level-feature workspace (hash_feature_kernel, round 3), or
+// nullptr for the round-2 gather kernel (also knob "hash_infer" = 1)
+constexpr int64_t kHashFeatStride = (int64_t)1 << 21;  // queries per feature pass (128 MiB of features)
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
-                             const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
+                             const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s,
+                             uint32_t* feat = nullptr);
 hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float* enc, int64_t n, hipStream_t s);
 // FrequencySH extension
 hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
@@ -301,7 +305,8 @@ enum Knob : int {
     kKnobScatterMin = 2,   // Hash grid scatter slice plan (samples per block at level 0 / cap), -1 = 2048 / 4096
     kKnobScatterMax = 3,
     kKnobDcDw0Delay = 4,  // debug library: s_sleep(127) rounds dW wave 0 of the dc kernel spends after its step 5
-    kKnobCount = 5
+    kKnobHashInfer = 5,   // Hash inference: -1 / 0 LDS-table feature pass + MLP kernel (round 3), 1 the gather kernel
+    kKnobCount = 6
 };
 int knob(Knob k);
 

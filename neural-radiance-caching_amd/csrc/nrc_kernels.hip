@@ -429,6 +429,20 @@ __device__ __forceinline__ void hash_corners(float px, float py, float pz, int l
     }
 }
 
+// tcnn kernel_grid's interpolation of one level: result = fma((half)w, value, result) over corners 0..7, packed half2
+__device__ __forceinline__ uint32_t hash_interp(const HashCorners& C, const uint32_t (&v)[8]) {
+    h2v acc = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        // (half)weight must be rounded before the FMA: the launder stops the compiler from folding the f32->f16
+        // conversion into a mixed-precision v_fma_mix (which would skip that rounding)
+        uint32_t w2 = pk2(C.w[c], C.w[c]);
+        asm volatile("" : "+v"(w2));
+        acc = __builtin_elementwise_fma(__builtin_bit_cast(h2v, w2), __builtin_bit_cast(h2v, v[c]), acc);
+    }
+    return __builtin_bit_cast(uint32_t, acc);
+}
+
 // One level's two features as a packed half2: tcnn kernel_grid result = fma((half)w, value, result), corners 0..7.
 template <bool DENSE_OK>
 __device__ __forceinline__ uint32_t hash_level_feature(float px, float py, float pz, int l,
@@ -451,16 +465,7 @@ __device__ __forceinline__ uint32_t hash_level_feature(float px, float py, float
         v[2 * p] = pick4(quad, e0 & 3u);
         v[2 * p + 1] = same ? pick4(quad, e1 & 3u) : far;
     }
-    h2v acc = {(_Float16)0.0f, (_Float16)0.0f};
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        // (half)weight must be rounded before the FMA: the launder stops the compiler from folding the f32->f16
-        // conversion into a mixed-precision v_fma_mix (which would skip that rounding)
-        uint32_t w2 = pk2(C.w[c], C.w[c]);
-        asm volatile("" : "+v"(w2));
-        acc = __builtin_elementwise_fma(__builtin_bit_cast(h2v, w2), __builtin_bit_cast(h2v, v[c]), acc);
-    }
-    return __builtin_bit_cast(uint32_t, acc);
+    return hash_interp(C, v);
 }
 
 // 32 K slots of lane half h (see hash_slot_feature): 8 hash levels (16 features), 3 OneBlob dims, 3 identity,
@@ -493,6 +498,79 @@ __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
         u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
         x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
+// encode_hash with the 8 level features of lane half h already computed (hash_feature_kernel): F[i] = level 8h + i
+__device__ __forceinline__ void encode_hashf(const QLane& Q, const uint32_t (&F)[8], h8 (&x)[4]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = F[i];
+    {
+        const float xb[3] = {Q.b0, Q.b1, Q.b2};
+        uint32_t lo[3], hi[3];
+        blob_many<3>(xb, lo, hi);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            w[8 + 2 * i] = lo[i];
+            w[8 + 2 * i + 1] = hi[i];
+        }
+    }
+    w[14] = pk2(Q.i0, Q.i1);
+    w[15] = pk2(Q.i2, 1.0f);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        u4 t4 = {w[4 * kk], w[4 * kk + 1], w[4 * kk + 2], w[4 * kk + 3]};
+        x[kk] = __builtin_bit_cast(h8, t4);
+    }
+}
+
+// HashGrid features of a chunk of queries, one level per block with the level's table in LDS (round 3). The gather
+// kernel above reads 128 random 4-byte table entries per query from L1/L2 -- one cache line each, the L1 line rate
+// bounds it -- while one level's table (32,768 entries x 4 B = 128 KiB, level 0: 16 KiB) fits a CU's LDS, where a
+// random 4-byte read costs a bank access instead of a line. Block b: level (b / 8) % 16, query range sub = b % 8 +
+// 8 * (b / 128) of P: the 16 level blocks of a range are dispatched to the same XCD (round-robin b % 8), so they share
+// its L2 for the positions. feat[level * kHashFeatStride + s] = the same half2 as hash_level_feature (same corners,
+// same interpolation), for s in [0, n).
+__global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __restrict__ q, int64_t n, int P,
+                                                               const uint32_t* __restrict__ table,
+                                                               uint32_t* __restrict__ feat) {
+    __shared__ __attribute__((aligned(16))) uint32_t lt[NRC_HASH_T];
+    const int b = blockIdx.x;
+    const int level = (b >> 3) & 15, sub = (b & 7) + 8 * (b >> 7);
+    if (sub >= P) return;
+    const uint32_t entries = level == 0 ? 4096u : (uint32_t)NRC_HASH_T;
+    const uint32_t off = level == 0 ? 0u : 4096u + (uint32_t)(level - 1) * (uint32_t)NRC_HASH_T;
+    {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const u4* src = reinterpret_cast<const u4*>(table + off);
+        for (int c = wave; c < (int)(entries / 256u); c += 16)
+            __builtin_amdgcn_global_load_lds((const void*)(src + c * 64 + lane),
+                                             (__attribute__((address_space(3))) void*)(lt + c * 256), 16, 0, 0);
+    }
+    const int64_t s0 = (int64_t)sub * n / P, s1 = (int64_t)(sub + 1) * n / P;
+    int64_t s = s0 + threadIdx.x;
+    typedef float f3 __attribute__((ext_vector_type(3)));
+    auto load_pos = [&](int64_t i) -> f3 {
+        const int64_t ic = i < s1 ? i : (s1 > s0 ? s1 - 1 : 0);
+        return *reinterpret_cast<const f3*>(q + ic * NRC_INPUT_DIMS);
+    };
+    f3 p = load_pos(s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t* const dst = feat + (int64_t)level * kHashFeatStride;
+    for (; s0 + (s - s0 - (int64_t)threadIdx.x) < s1; s += 1024) {  // block-uniform trip count
+        const f3 pn = load_pos(s + 1024);
+        HashCorners C;
+        if (level <= 1) hash_corners<true>(p.x, p.y, p.z, level, C);
+        else hash_corners<false>(p.x, p.y, p.z, level, C);
+        uint32_t v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = lt[C.entry[c] - off];
+        const uint32_t f = hash_interp(C, v);
+        if (s < s1) dst[s] = f;
+        p = pn;
     }
 }
 
@@ -759,7 +837,7 @@ template <int TILES, int THREADS, bool PREFETCH, int ABL, int EPI, int ENC = 0>
 __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float* __restrict__ out, int64_t n,
                                               const h8* __restrict__ wf, const InferEpilogue& epi,
                                               const uint32_t* __restrict__ grid = nullptr) {
-    constexpr int KK0 = ENC == 1 ? 4 : 5;
+    constexpr int KK0 = ENC == 1 || ENC == 3 ? 4 : 5;  // ENC 3: Hash from hash_feature_kernel's features (grid = feat)
     [[maybe_unused]] uint64_t rstart = 0;
     if constexpr ((ABL & 512) != 0) rstart = __builtin_amdgcn_s_memrealtime();
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
@@ -931,9 +1009,20 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     const int64_t last = n - 1;
 
     QLane Q[TILES];
-    // ABL & 8192 (ENC 0, TILES 1): queries through raw buffer loads (load_q_tile)
-    constexpr bool kBufQ = (ABL & 8192) != 0 && ENC == 0 && TILES == 1;
+    // ABL & 8192 (ENC 0 / 3, TILES 1): queries through raw buffer loads (load_q_tile)
+    constexpr bool kBufQ = (ABL & 8192) != 0 && (ENC == 0 || ENC == 3) && TILES == 1;
     const QOffsets vo{r * 60, r * 60 + 12 + 12 * h, r * 60 + 36 + 12 * h};
+    // ENC 3: the lane's 8 level features of the tile's query (levels 8h .. 8h + 7), prefetched with the query
+    [[maybe_unused]] uint32_t F[8];
+    auto load_f = [&](int64_t tile) {
+        if constexpr (ENC == 3) {
+            const int64_t sq = min(tile * 32 + r, last);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) F[i] = grid[(int64_t)(8 * h + i) * kHashFeatStride + sq];
+        }
+    };
+    static_assert(ENC != 3 || TILES == 1, "ENC 3 prefetches one tile");
+    load_f(g);
     if constexpr (kBufQ) {
         Q[0] = load_q_tile(q, n, g, vo);
     } else {
@@ -1000,6 +1089,8 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         for (int t = 0; t < TILES; ++t) {
             if constexpr (ENC == 1) {
                 encode_hash(Q[t], h, grid, x[t]);
+            } else if constexpr (ENC == 3) {
+                encode_hashf(Q[t], F, x[t]);
             } else if constexpr (ENC == 2) {
                 encode_sh<(ABL & 16) != 0>(Q[t], h, x[t]);
             } else if constexpr ((ABL & 1) != 0) {
@@ -1032,6 +1123,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             ng = g + wstride;
             nn = ng;
         }
+        load_f(ng);  // ENC 3 (after the encoder has consumed F)
         if constexpr (kBufQ) {
             Q[0] = load_q_tile(q, n, ng, vo);
         } else if constexpr ((ABL & 32) != 0) {
@@ -1287,6 +1379,14 @@ __global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restr
                                                             const uint32_t* __restrict__ grid) {
     // ABL 0: the buffer-store epilogue (32) measured 2 % slower here (536 vs 524 us; gather-bound kernel)
     infer_v2_body<1, 512, false, XABL, EPI, 1>(q, out, n, wf, epi, grid);
+}
+
+// InputEncoding::Hash inference from hash_feature_kernel's level features (round 3): variant 39's shape and queue
+template <int EPI>
+__global__ __launch_bounds__(1024, 4) void infer_hashf_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                              int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
+                                                              const uint32_t* __restrict__ feat) {
+    infer_v2_body<1, 1024, false, 32 | 2048 | 8192, EPI, 3>(q, out, n, wf, epi, feat);
 }
 
 // FrequencySH extension inference (EPI -1 plain; 0 / 2 fused accumulation)
@@ -2853,11 +2953,34 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
 }
 
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
-                             const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
+                             const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s,
+                             uint32_t* feat) {
     if (n <= 0) return hipSuccess;
+    if (mode != -1 && mode != 0 && mode != 2) return hipErrorInvalidValue;
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
+    if (feat) {
+        // round 3: per pass of <= kHashFeatStride queries, the LDS-table feature kernel, then the MLP kernel reading them
+        static int bpf[3] = {};
+        for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
+            const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
+            const int P = cnt > ((int64_t)1 << 19) ? 16 : 8;  // query ranges per level (multiple of the 8 XCDs)
+            hipLaunchKernelGGL(hash_feature_kernel, dim3(16 * P), dim3(1024), 0, s, queries + c0 * NRC_INPUT_DIMS, cnt,
+                               P, g, feat);
+            const int64_t acc = std::min<int64_t>(std::max<int64_t>(n_acc - c0, 0), cnt);
+            const InferEpilogue e{thr ? thr + c0 * 3 : nullptr, rgba ? reinterpret_cast<float4*>(rgba) + c0 : nullptr, acc, w};
+            const float* qc = queries + c0 * NRC_INPUT_DIMS;
+            float* oc = out ? out + c0 * NRC_OUTPUT_DIMS : nullptr;
+            const int64_t nt = (cnt + 31) / 32;
+            hipError_t err;
+            if (mode == -1) err = launch_persistent_infer(infer_hashf_kernel<-1>, 1024, bpf[0], nt, qc, oc, cnt, wf, s, e, (const uint32_t*)feat);
+            else if (mode == 0) err = launch_persistent_infer(infer_hashf_kernel<0>, 1024, bpf[1], nt, qc, oc, cnt, wf, s, e, (const uint32_t*)feat);
+            else err = launch_persistent_infer(infer_hashf_kernel<2>, 1024, bpf[2], nt, qc, oc, cnt, wf, s, e, (const uint32_t*)feat);
+            if (err != hipSuccess) return err;
+        }
+        return hipGetLastError();
+    }
     const int64_t ntiles = (n + 31) / 32;
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
     static int bpq[3] = {};
     switch (mode) {
         case -1: return launch_persistent_infer(infer_hash_kernel<-1, 2048 | 32>, 512, bpq[0], ntiles, queries, out, n, wf, s, epi, g);

@@ -105,6 +105,51 @@ def test_hash_infer_accumulate_fused_bitwise(nrc, dev, hnet, orc):
     assert torch.equal(rgba, ref_rgba) and torch.equal(res[n_acc:], ref[n_acc:])
 
 
+@pytest.mark.parametrize("n", [1, 33, 70001, (1 << 21) + 77])
+def test_hash_feature_pass_bitwise_gather_kernel(nrc, dev, hnet, orc, n):
+    """The round-3 inference (hash_feature_kernel: one level's table in LDS per block, then the MLP kernel reading the
+    level features) computes the same half2 features as the round-2 gather kernel (knob hash_infer = 1) and runs the
+    same MLP body: outputs bitwise equal, including a second feature pass (n > 2^21) and its tail."""
+    import torch
+    hnet.set_state(nrc.StateSlot.INFER, _trained_like(orc))
+    q = _t(nrc.synthetic.cornell_queries(n, seed=7 + n), dev)
+    a = torch.full((n + 8, 3), 777.0, device=dev)
+    b = torch.full((n + 8, 3), 777.0, device=dev)
+    hnet.infer(q, a, n)
+    try:
+        nrc._lib.set_knob("hash_infer", 1)
+        hnet.infer(q, b, n)
+    finally:
+        nrc._lib.set_knob("hash_infer", -1)
+    torch.cuda.synchronize()
+    assert (a[n:] == 777.0).all()
+    assert torch.equal(a, b), f"{int((a != b).any(dim=1).sum())} rows differ"
+
+
+def test_hash_feature_pass_fused_across_passes(nrc, dev, hnet, orc):
+    """Fused accumulation over two feature passes, the render/train boundary inside the second: bitwise the gather
+    kernel's frame buffer and train-suffix radiance."""
+    import torch
+    F = nrc.frame
+    hnet.set_state(nrc.StateSlot.INFER, _trained_like(orc))
+    n, n_acc = (1 << 21) + 9000, (1 << 21) + 3000
+    q = _t(nrc.synthetic.cornell_queries(n, seed=12), dev)
+    thr = torch.rand((n_acc, 3), device=dev)
+    rgba0 = torch.rand((n_acc, 4), device=dev)
+    res = []
+    for k in (-1, 1):
+        out = torch.full((n, 3), -1.0, device=dev)
+        rgba = rgba0.clone()
+        try:
+            nrc._lib.set_knob("hash_infer", k)
+            F.infer_accumulate(hnet, q, out, n, thr, rgba, n_acc, F.RenderMode.Full, 2)
+        finally:
+            nrc._lib.set_knob("hash_infer", -1)
+        res.append((out, rgba))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][0][n_acc:], res[1][0][n_acc:])
+
+
 def test_hash_train_step_matches_oracle(nrc, orc, dev, hnet):
     params = _trained_like(orc, seed=9)
     for slot in (nrc.StateSlot.PARAMS, nrc.StateSlot.INFER):

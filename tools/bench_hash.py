@@ -1,7 +1,7 @@
 """Timing of the InputEncoding::Hash model on one MI355X: inference over 2^21 synthetic
 Cornell queries and the 16,384-sample training step, HIP events on the network's stream.
 
-    python tools/bench_hash.py [--iters 50]
+    python tools/bench_hash.py [--iters 50] [--knob hash_infer=1]
 """
 from __future__ import annotations
 
@@ -21,10 +21,14 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--queries", type=int, default=1 << 21)
+    ap.add_argument("--knob", action="append", default=[], help="name=value A/B knob of the library (repeatable)")
     args = ap.parse_args()
     import torch
 
     nrc = nrc_loader.load()
+    for kv in args.knob:
+        k, v = kv.split("=")
+        nrc._lib.set_knob(k, int(v))
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream()
     net = nrc.Network()
@@ -52,7 +56,7 @@ def main() -> None:
     train_us = timed(lambda i=0: net.train(tq[(i % 4) * nrc.BATCH_SIZE:], tt[(i % 4) * nrc.BATCH_SIZE:]), 40)
     net.destroy()
     flop_q = 2 * (62 * 64 + 4 * 64 * 64 + 64 * 3)
-    print(json.dumps({"encoding": "Hash", "queries": n, "infer_us": infer_us, "Gq_per_s": n / infer_us / 1e3,
+    print(json.dumps({"encoding": "Hash", "knobs": args.knob, "queries": n, "infer_us": infer_us, "Gq_per_s": n / infer_us / 1e3,
                       "mlp_tflops_alg": flop_q * n / (infer_us * 1e-6) / 1e12,
                       "gathers_per_query": 16 * 8, "train_step_us": train_us}, indent=1))
 
