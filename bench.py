@@ -189,7 +189,7 @@ def hash_bench(nrc, dev, iters: int) -> dict:
     net.destroy()
     return {"workload": "SURVEY 8(f) row 3: InputEncoding::Hash, 2^21-query inference + 16384-sample train step",
             "M_queries_per_s": n / (infer_ms * 1e-3) / 1e6, "infer_kernel_ms": infer_ms, "train_step_ms": train_ms,
-            "bound": "L1/TA gather rate (128 random table reads per query), DESIGN.md section 10"}
+            "bound": "feature pass (one level table per CU in LDS: random LDS gathers + VALU) + MLP pass, DESIGN.md section 10"}
 
 
 def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:

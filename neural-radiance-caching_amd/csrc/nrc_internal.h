@@ -306,7 +306,8 @@ enum Knob : int {
     kKnobScatterMax = 3,
     kKnobDcDw0Delay = 4,  // debug library: s_sleep(127) rounds dW wave 0 of the dc kernel spends after its step 5
     kKnobHashInfer = 5,   // Hash inference: -1 / 0 LDS-table feature pass + MLP kernel (round 3), 1 the gather kernel
-    kKnobCount = 6
+    kKnobHashFeatAbl = 6,  // debug library: hash_feature_kernel ablation (1 no gathers, 2 no position loads, 4 no stores)
+    kKnobCount = 7
 };
 int knob(Knob k);
 

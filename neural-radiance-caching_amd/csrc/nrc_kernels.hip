@@ -14,6 +14,7 @@
 // reduce_adam_kernel after every optimizer step. Weight gradients (a contraction over samples) go
 // through a per-block LDS transpose read with ds_read_b64_tr_b16.
 #include <cstdlib>
+#include <type_traits>
 
 #include "nrc_device.h"
 
@@ -481,16 +482,11 @@ __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_
         if (i == 4) asm volatile("" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
         w[i] = hash_level_feature<false>(Q.p0, Q.p1, Q.p2, 8 * h + i, table);
     }
-    {
-        const float xb[3] = {Q.b0, Q.b1, Q.b2};
-        uint32_t lo[3], hi[3];
-        blob_many<3>(xb, lo, hi);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            w[8 + 2 * i] = lo[i];
-            w[8 + 2 * i + 1] = hi[i];
-        }
-    }
+    // OneBlob as encoder v3 (clamped wrap, one path): the reference's raw-angle inputs send every Cornell wave down
+    // blob_many's wrap branch (~25 VALU more per input)
+    blob_v3(Q.b0, w[8], w[9]);
+    blob_v3(Q.b1, w[10], w[11]);
+    blob_v3(Q.b2, w[12], w[13]);
     w[14] = pk2(Q.i0, Q.i1);
     w[15] = pk2(Q.i2, 1.0f);
 #pragma unroll
@@ -506,16 +502,11 @@ __device__ __forceinline__ void encode_hashf(const QLane& Q, const uint32_t (&F)
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = F[i];
-    {
-        const float xb[3] = {Q.b0, Q.b1, Q.b2};
-        uint32_t lo[3], hi[3];
-        blob_many<3>(xb, lo, hi);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            w[8 + 2 * i] = lo[i];
-            w[8 + 2 * i + 1] = hi[i];
-        }
-    }
+    // OneBlob as encoder v3 (clamped wrap, one path): the reference's raw-angle inputs send every Cornell wave down
+    // blob_many's wrap branch (~25 VALU more per input)
+    blob_v3(Q.b0, w[8], w[9]);
+    blob_v3(Q.b1, w[10], w[11]);
+    blob_v3(Q.b2, w[12], w[13]);
     w[14] = pk2(Q.i0, Q.i1);
     w[15] = pk2(Q.i2, 1.0f);
 #pragma unroll
@@ -533,6 +524,44 @@ __device__ __forceinline__ void encode_hashf(const QLane& Q, const uint32_t (&F)
 // 8 * (b / 128) of P: the 16 level blocks of a range are dispatched to the same XCD (round-robin b % 8), so they share
 // its L2 for the positions. feat[level * kHashFeatStride + s] = the same half2 as hash_level_feature (same corners,
 // same interpolation), for s in [0, n).
+// hash_corners for one level whose table sits alone in LDS: the corners' LDS byte offsets instead of global entries.
+// (index & mask) * 4 == (4 index) & (4 mask) for the hashed x ^ y P1 ^ z P2 and the dense x + y res + z res^2 alike
+// (uint32 wrap-around), so the cell coordinates and multipliers carry the factor 4 and one v_bitop3 per corner
+// ((x ^ yz) & mask) gives the offset; positions, fractions and weights are hash_corners' float operations.
+struct LdsCorners {
+    uint32_t off[8];
+    float w[8];
+};
+template <bool DENSE>
+__device__ __forceinline__ void hash_corners_lds(float px, float py, float pz, int l, LdsCorners& C) {
+    const float scale = (float)(16 << l) - 1.0f;
+    const uint32_t res = 16u << l;
+    const float xs[3] = {px, py, pz};
+    float fr[3];
+    uint32_t cell[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float pos = __builtin_fmaf(scale, xs[d], 0.5f);
+        const float fl = floorf(pos);
+        cell[d] = (uint32_t)(int)fl;
+        fr[d] = pos - fl;
+    }
+    const uint32_t mask4 = (l == 0 ? 4095u : 32767u) << 2;
+    const uint32_t ym = 4u * (DENSE ? res : NRC_HASH_PRIME1), zm = 4u * (DENSE ? res * res : NRC_HASH_PRIME2);
+    const uint32_t X[2] = {4u * cell[0], 4u * cell[0] + 4u};
+    const uint32_t Y[2] = {cell[1] * ym, cell[1] * ym + ym};
+    const uint32_t Z[2] = {cell[2] * zm, cell[2] * zm + zm};
+    const float wx[2] = {1.0f - fr[0], fr[0]}, wy[2] = {1.0f - fr[1], fr[1]}, wz[2] = {1.0f - fr[2], fr[2]};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+        const uint32_t i = DENSE ? X[bx] + (Y[by] + Z[bz]) : X[bx] ^ (Y[by] ^ Z[bz]);
+        C.off[c] = i & mask4;
+        C.w[c] = (wx[bx] * wy[by]) * wz[bz];
+    }
+}
+
+template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores
 __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __restrict__ q, int64_t n, int P,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ feat) {
@@ -550,28 +579,83 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
                                              (__attribute__((address_space(3))) void*)(lt + c * 256), 16, 0, 0);
     }
     const int64_t s0 = (int64_t)sub * n / P, s1 = (int64_t)(sub + 1) * n / P;
-    int64_t s = s0 + threadIdx.x;
+    const int cnt = (int)(s1 - s0);  // <= kHashFeatStride: 32-bit byte offsets below
+    uint32_t* const fb = feat + (int64_t)level * kHashFeatStride + s0;
     typedef float f3 __attribute__((ext_vector_type(3)));
-    auto load_pos = [&](int64_t i) -> f3 {
-        const int64_t ic = i < s1 ? i : (s1 > s0 ? s1 - 1 : 0);
-        return *reinterpret_cast<const f3*>(q + ic * NRC_INPUT_DIMS);
+    // Position loads and feature stores as inline asm: the compiler neither moves them nor waits for them (it sank
+    // compiler-visible loads issued two steps ahead to the loop latch, right before their use; a conditional store made
+    // it wait for the store's acknowledgement); the waits are explicit. vmcnt counts loads and stores in issue order;
+    // every step issues 2 loads then 2 stores, so the positions loaded two steps earlier are complete once at most 6
+    // operations are outstanding (the prologue pads the count with 2 x 2 extra loads). Lanes past the range load the
+    // range's last position and store its feature -- the same value to the same word as the lane that owns it.
+    const int64_t last = cnt > 0 ? cnt - 1 : 0;
+    const float* const qb = q + s0 * NRC_INPUT_DIMS;
+    auto load_pos = [&](int k, f3& dst) {
+        if constexpr ((ABL & 2) != 0) {
+            const float u = (float)(k & 1023) * (1.0f / 1024.0f);
+            dst = f3{u, 1.0f - u, u * u};
+        } else {
+            const float* src = qb + (int64_t)(k < last ? k : last) * NRC_INPUT_DIMS;
+            asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(dst) : "v"(src) : "memory");
+        }
     };
-    f3 p = load_pos(s);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    uint32_t* const dst = feat + (int64_t)level * kHashFeatStride;
-    for (; s0 + (s - s0 - (int64_t)threadIdx.x) < s1; s += 1024) {  // block-uniform trip count
-        const f3 pn = load_pos(s + 1024);
-        HashCorners C;
-        if (level <= 1) hash_corners<true>(p.x, p.y, p.z, level, C);
-        else hash_corners<false>(p.x, p.y, p.z, level, C);
-        uint32_t v[8];
+    auto store_feature = [&](int k, uint32_t f) {
+        if constexpr ((ABL & 4) == 0) {
+            uint32_t* dst = fb + (k < last ? k : last);
+            asm volatile("global_store_dword %0, %1, off" : : "v"(dst), "v"(f) : "memory");
+        } else {
+            f3 dummy;  // ablation: a load in place of the store keeps the vmcnt arithmetic
+            load_pos(k, dummy);
+            asm volatile("" : : "v"(dummy.x));
+        }
+    };
+    int i = threadIdx.x;
+    f3 PB[2][2], pad[4];
+    load_pos(i, PB[0][0]);
+    load_pos(i + 1024, PB[0][1]);
+    load_pos(i, pad[0]);
+    load_pos(i, pad[1]);
+    load_pos(i + 2048, PB[1][0]);
+    load_pos(i + 3072, PB[1][1]);
+    load_pos(i, pad[2]);
+    load_pos(i, pad[3]);
+    asm volatile("s_waitcnt vmcnt(8)" : "+v"(pad[0]), "+v"(pad[1]), "+v"(pad[2]), "+v"(pad[3]) : : "memory");
+    __syncthreads();  // the table DMA (issued before these 8 loads) has landed
+    const char* const ltb = reinterpret_cast<const char*>(lt);
+    auto body = [&](auto dense_c) {
+        constexpr bool kDense = decltype(dense_c)::value;
+        auto step = [&](auto cur_c) -> bool {
+            constexpr int cur = decltype(cur_c)::value;
+            if (i - (int)threadIdx.x >= cnt) return false;  // block-uniform
+            if constexpr ((ABL & 2) == 0)
+                asm volatile("s_waitcnt vmcnt(6)" : "+v"(PB[cur][0]), "+v"(PB[cur][1]) : : "memory");
+            LdsCorners C[2];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = lt[C.entry[c] - off];
-        const uint32_t f = hash_interp(C, v);
-        if (s < s1) dst[s] = f;
-        p = pn;
-    }
+            for (int u = 0; u < 2; ++u) hash_corners_lds<kDense>(PB[cur][u].x, PB[cur][u].y, PB[cur][u].z, level, C[u]);
+            load_pos(i + 4096, PB[cur][0]);
+            load_pos(i + 5120, PB[cur][1]);
+            uint32_t v[2][8];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    v[u][c] = (ABL & 1) ? C[u].off[c] : *reinterpret_cast<const uint32_t*>(ltb + C[u].off[c]);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                HashCorners W;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) W.w[c] = C[u].w[c];
+                const uint32_t f = hash_interp(W, v[u]);
+                store_feature(i + 1024 * u, f);
+            }
+            i += 2048;
+            return true;
+        };
+        while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{})) {
+        }
+    };
+    if (level <= 1) body(std::integral_constant<bool, true>{});
+    else body(std::integral_constant<bool, false>{});
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2964,8 +3048,16 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
         for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
             const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
             const int P = cnt > ((int64_t)1 << 19) ? 16 : 8;  // query ranges per level (multiple of the 8 XCDs)
-            hipLaunchKernelGGL(hash_feature_kernel, dim3(16 * P), dim3(1024), 0, s, queries + c0 * NRC_INPUT_DIMS, cnt,
-                               P, g, feat);
+            const float* qc0 = queries + c0 * NRC_INPUT_DIMS;
+#if NRC_DEBUG_KERNELS
+            const int fa = knob(kKnobHashFeatAbl);
+            if (fa > 0) {
+                auto k = fa == 1 ? hash_feature_kernel<1> : fa == 2 ? hash_feature_kernel<2> : fa == 4 ? hash_feature_kernel<4>
+                                                                                                   : hash_feature_kernel<7>;
+                hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+            } else
+#endif
+                hipLaunchKernelGGL(hash_feature_kernel<0>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
             const int64_t acc = std::min<int64_t>(std::max<int64_t>(n_acc - c0, 0), cnt);
             const InferEpilogue e{thr ? thr + c0 * 3 : nullptr, rgba ? reinterpret_cast<float4*>(rgba) + c0 : nullptr, acc, w};
             const float* qc = queries + c0 * NRC_INPUT_DIMS;
