@@ -1465,12 +1465,13 @@ __global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restr
     infer_v2_body<1, 512, false, XABL, EPI, 1>(q, out, n, wf, epi, grid);
 }
 
-// InputEncoding::Hash inference from hash_feature_kernel's level features (round 3): variant 39's shape and queue
+// InputEncoding::Hash inference from hash_feature_kernel's level features (round 3): variant 47's shape, queue and
+// 4x4x4 output layer (the gather kernel below takes the same output layer, so the two stay bitwise equal)
 template <int EPI>
 __global__ __launch_bounds__(1024, 4) void infer_hashf_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                               int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
                                                               const uint32_t* __restrict__ feat) {
-    infer_v2_body<1, 1024, false, 32 | 2048 | 8192, EPI, 3>(q, out, n, wf, epi, feat);
+    infer_v2_body<1, 1024, false, 32 | 2048 | 8192 | 65536, EPI, 3>(q, out, n, wf, epi, feat);
 }
 
 // FrequencySH extension inference (EPI -1 plain; 0 / 2 fused accumulation)
@@ -3075,9 +3076,9 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     static int bpq[3] = {};
     switch (mode) {
-        case -1: return launch_persistent_infer(infer_hash_kernel<-1, 2048 | 32>, 512, bpq[0], ntiles, queries, out, n, wf, s, epi, g);
-        case 0: return launch_persistent_infer(infer_hash_kernel<0, 2048 | 32>, 512, bpq[1], ntiles, queries, out, n, wf, s, epi, g);
-        case 2: return launch_persistent_infer(infer_hash_kernel<2, 2048 | 32>, 512, bpq[2], ntiles, queries, out, n, wf, s, epi, g);
+        case -1: return launch_persistent_infer(infer_hash_kernel<-1, 2048 | 32 | 65536>, 512, bpq[0], ntiles, queries, out, n, wf, s, epi, g);
+        case 0: return launch_persistent_infer(infer_hash_kernel<0, 2048 | 32 | 65536>, 512, bpq[1], ntiles, queries, out, n, wf, s, epi, g);
+        case 2: return launch_persistent_infer(infer_hash_kernel<2, 2048 | 32 | 65536>, 512, bpq[2], ntiles, queries, out, n, wf, s, epi, g);
         default: return hipErrorInvalidValue;
     }
 }
