@@ -234,9 +234,9 @@ std::vector<int> build_t16_slab_map() {
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
 bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
-                                            "hash_infer", "hash_feat_abl"};
+                                            "hash_infer", "hash_feat_abl", "t16_groups"};
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -514,6 +514,8 @@ void wide_grad_partials(nrc_net* net, const float* in, const float* tgt, uint32_
                                         net->wide_ws_d, net->wide_slabs, net->wide_loss_partials, net->stream));
 }
 
+int t16_groups() { return knob(kKnobT16Groups) == 1 ? 1 : 2; }
+
 // dc shape of a b-sample step (train_shape knob, else by batch size)
 int dc_shape(uint32_t b) {
     const int k = knob(kKnobTrainShape);
@@ -525,6 +527,10 @@ int train_block_count(const nrc_net* net, uint32_t b) {
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0) {
         const int S = dc_samples_per_block(dc_shape(b));
         return (int)((b + (uint32_t)S - 1) / (uint32_t)S);
+    }
+    if (net->t16 && net->t16_kernel != 2) {
+        const uint32_t S = 64u * (uint32_t)t16_groups();
+        return (int)((b + S - 1) / S);
     }
     return train_blocks(b);
 }
@@ -538,7 +544,7 @@ void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b,
     else if (net->t16)
         HIP_CHECK(launch_train16(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream,
-                                 net->t16_kernel != 2));
+                                 net->t16_kernel != 2, t16_groups()));
     else if (stamps)
         HIP_CHECK(launch_train_stamped(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                        net->slabs, net->loss_partials, stamps, net->stream));

@@ -285,7 +285,9 @@ struct ModelBuffers {
 // slabs: f16 (nrc_train16.hip slab_pair), reduced by launch_reduce_adam (ModelBuffers::slab_f16)
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s, bool split = false);  // split: the role-split kernel (NRC_T16_SPLIT at init)
+                          hipStream_t s, bool split = false, int groups = 2);
+// samples per block of the role-split t16 kernel: 64 x groups (knob "t16_groups"; 128 by default)
+int t16_groups();  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16
 // slab format as launch_train16; one slab per block of dc_samples_per_block(shape) samples.
 int dc_samples_per_block(int shape);
@@ -307,7 +309,8 @@ enum Knob : int {
     kKnobDcDw0Delay = 4,  // debug library: s_sleep(127) rounds dW wave 0 of the dc kernel spends after its step 5
     kKnobHashInfer = 5,   // Hash inference: -1 / 0 LDS-table feature pass + MLP kernel (round 3), 1 the gather kernel
     kKnobHashFeatAbl = 6,  // debug library: hash_feature_kernel ablation (1 no gathers, 2 no position loads, 4 no stores)
-    kKnobCount = 7
+    kKnobT16Groups = 7,    // role-split t16 training kernel: 16-sample groups per chain wave (1: 64-sample blocks; -1 = 2)
+    kKnobCount = 8
 };
 int knob(Knob k);
 

@@ -60,23 +60,23 @@ __device__ __forceinline__ h8 tr_op(const TrTile& t, int kk) {
 
 // dW tiles A_i x B_j (i < NA, j < NB) over 128 samples: A = delta-image tiles (rows), B = activation-image tiles
 // (columns). Every operand read is issued before the first MFMA.
-template <int NA, int NB>
+template <int NA, int NB, int KS = 4>  // KS k-steps of 32 samples (the block's samples)
 __device__ __forceinline__ void dw_tiles(const TrTile (&ta)[NA], const TrTile (&tb)[NB], f4 (&acc)[NA][NB]) {
-    h8 A[NA][4], B[NB][4];
+    h8 A[NA][KS], B[NB][KS];
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) A[i][kk] = tr_op(ta[i], kk);
+        for (int kk = 0; kk < KS; ++kk) A[i][kk] = tr_op(ta[i], kk);
 #pragma unroll
     for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) B[j][kk] = tr_op(tb[j], kk);
+        for (int kk = 0; kk < KS; ++kk) B[j][kk] = tr_op(tb[j], kk);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
+    for (int kk = 0; kk < KS; ++kk)
 #pragma unroll
         for (int i = 0; i < NA; ++i)
 #pragma unroll
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // in each backward step, compute the block's dW_L tiles from the images the chain waves wrote in the step before and
 // stream them to the slab. The two halves of a step share the SIMDs' MFMA pipes and hide each other's LDS and
 // dependency latency; the step's critical path is the chain alone instead of chain + dW.
-template <int AUX>
+template <int AUX, int G = 2>  // G: 16-sample groups per chain wave (64 G samples per block)
 __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                                int64_t b, float n_total, float loss_scale,
                                                                const h8* __restrict__ wf, const h8* __restrict__ wb,
@@ -511,8 +511,8 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     if (dw_wave) {
         // ---- dW waves: the forward's six barriers, then one dW step per backward step
         for (int i = 0; i < 6; ++i) lds_barrier();
-        const int G = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-        const int r0 = 8 * G + qq, r1 = r0 + 4;
+        const int lg = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+        const int r0 = 8 * lg + qq, r1 = r0 + 4;
         const int tm0 = 2 * (wave >> 1), tn0 = 2 * (wave & 1);
         int oa[2][2], ob[2][2];
 #pragma unroll
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
             f4 acc[1][1];
             const TrTile ta[1] = {TrTile{img_d1, off64(r0, pp), off64(r1, pp), 4096}};
             const TrTile tb[1] = {TrTile{img_a1, off64(r0, 4 * wave + pp), off64(r1, 4 * wave + pp), 4096}};
-            dw_tiles<1, 1>(ta, tb, acc);
+            dw_tiles<1, 1, 2 * G>(ta, tb, acc);
             slab_single_b<AUX>(slab, 5, 0, wave, lane, acc[0][0]);
         }
         lds_barrier();
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
                 tb[i] = TrTile{imga, ob[i][0], ob[i][1], 4096};
             }
             f4 acc[2][2];
-            dw_tiles<2, 2>(ta, tb, acc);
+            dw_tiles<2, 2, 2 * G>(ta, tb, acc);
 #pragma unroll
             for (int i = 0; i < 2; ++i) slab_pair_b<AUX>(slab, L, tm0 + i, tn0, lane, pack_pair(acc[i][0], acc[i][1]));
             lds_barrier();
@@ -556,12 +556,12 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
                 const TrTile tb[3] = {TrTile{img_a0, off64(r0, pp), off64(r1, pp), 4096},
                                       TrTile{img_a0, off64(r0, 4 + pp), off64(r1, 4 + pp), 4096},
                                       TrTile{img_a0, off64(r0, 8 + pp), off64(r1, 8 + pp), 4096}};
-                dw_tiles<2, 3>(ta, tb, acc);
+                dw_tiles<2, 3, 2 * G>(ta, tb, acc);
             } else {
                 const TrTile tb[3] = {TrTile{img_a0, off64(r0, 12 + pp), off64(r1, 12 + pp), 4096},
                                       TrTile{img_x2, off32(r0, pp), off32(r1, pp), 2048},
                                       TrTile{img_x2, off32(r0, 4 + pp), off32(r1, 4 + pp), 2048}};
-                dw_tiles<2, 3>(ta, tb, acc);
+                dw_tiles<2, 3, 2 * G>(ta, tb, acc);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
@@ -578,16 +578,16 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     }
 
     // ---- chain waves: as train16_kernel
-    int r[2];
-    bool valid[2];
+    int r[G];
+    bool valid[G];
     typedef float f3 __attribute__((ext_vector_type(3)));
-    f3 pq[2], tq[2];
-    f2 bl[2], id[2];
+    f3 pq[G], tq[G];
+    f2 bl[G], id[G];
     const int gg = g < 3 ? g : 0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        r[u] = 32 * wave + 16 * u + c;
-        const int64_t s = (int64_t)blockIdx.x * kTrainSamplesPerBlock + r[u];
+    for (int u = 0; u < G; ++u) {
+        r[u] = 16 * (G * wave + u) + c;
+        const int64_t s = (int64_t)blockIdx.x * (64 * G) + r[u];
         valid[u] = s < b;
         const int64_t sc = valid[u] ? s : b - 1;
         const float* qr = q + sc * NRC_INPUT_DIMS;
@@ -602,14 +602,17 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         __builtin_amdgcn_global_load_lds((const void*)(wf + (f < kT16FwdFrags ? f : kT16FwdFrags - 1) * 64 + lane),
                                          (__attribute__((address_space(3))) void*)(lwf + f * 64), 16, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(12)"
-                 : "+v"(pq[0]), "+v"(pq[1]), "+v"(bl[0]), "+v"(bl[1]), "+v"(id[0]), "+v"(id[1]), "+v"(tq[0]), "+v"(tq[1])
-                 :
-                 : "memory");
-    h8 x[2][3];
-    float tg[2][3];
+    if constexpr (G == 2)
+        asm volatile("s_waitcnt vmcnt(12)"
+                     : "+v"(pq[0]), "+v"(pq[1]), "+v"(bl[0]), "+v"(bl[1]), "+v"(id[0]), "+v"(id[1]), "+v"(tq[0]), "+v"(tq[1])
+                     :
+                     : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(12)" : "+v"(pq[0]), "+v"(bl[0]), "+v"(id[0]), "+v"(tq[0]) : : "memory");
+    h8 x[G][3];
+    float tg[G][3];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < G; ++u) {
         tg[u][0] = tq[u].x; tg[u][1] = tq[u].y; tg[u][2] = tq[u].z;
         encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u]);
         const u4 w = __builtin_bit_cast(u4, x[u][2]);
@@ -624,8 +627,8 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         __builtin_amdgcn_global_load_lds((const void*)(wb + f * 64 + lane),
                                          (__attribute__((address_space(3))) void*)(lwb + f * 64), 16, 0, 0);
     }
-    h8 a[5][2][2];
-    f4 o[2];
+    h8 a[5][G][2];
+    f4 o[G];
     {
         h8 w0[12], w1[8];
 #pragma unroll
@@ -635,18 +638,18 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
         for (int i = 0; i < 8; ++i) w1[i] = lwf[t16_fwd_frag(1, i >> 1, i & 1) * 64 + lane];
         __builtin_amdgcn_sched_barrier(0);
-        f4 cc[2][4];
+        f4 cc[G][4];
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
-            cc[0][mb] = cc[1][mb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int ks = 0; ks < 3; ++ks) {
-                cc[0][mb] = mfma16(w0[mb * 3 + ks], x[0][ks], cc[0][mb]);
-                cc[1][mb] = mfma16(w0[mb * 3 + ks], x[1][ks], cc[1][mb]);
-            }
+            for (int u = 0; u < G; ++u) cc[u][mb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+                for (int u = 0; u < G; ++u) cc[u][mb] = mfma16(w0[mb * 3 + ks], x[u][ks], cc[u][mb]);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < G; ++u) {
             a[0][u][0] = relu_b(cc[u][0], cc[u][1]);
             a[0][u][1] = relu_b(cc[u][2], cc[u][3]);
         }
@@ -668,25 +671,25 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
             if (l < 5) {
 #pragma unroll
                 for (int mb = 0; mb < 4; ++mb) {
-                    cc[0][mb] = cc[1][mb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int ks = 0; ks < 2; ++ks) {
-                        cc[0][mb] = mfma16(w1[mb * 2 + ks], a[l - 1][0][ks], cc[0][mb]);
-                        cc[1][mb] = mfma16(w1[mb * 2 + ks], a[l - 1][1][ks], cc[1][mb]);
-                    }
+                    for (int u = 0; u < G; ++u) cc[u][mb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                        for (int u = 0; u < G; ++u) cc[u][mb] = mfma16(w1[mb * 2 + ks], a[l - 1][u][ks], cc[u][mb]);
                 }
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < G; ++u) {
                     a[l][u][0] = relu_b(cc[u][0], cc[u][1]);
                     a[l][u][1] = relu_b(cc[u][2], cc[u][3]);
                 }
             } else {
-                o[0] = o[1] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    o[0] = mfma16(w1[ks], a[4][0][ks], o[0]);
-                    o[1] = mfma16(w1[ks], a[4][1][ks], o[1]);
-                }
+                for (int u = 0; u < G; ++u) o[u] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int u = 0; u < G; ++u) o[u] = mfma16(w1[ks], a[4][u][ks], o[u]);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -694,10 +697,12 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         }
     }
     float lossv = 0.0f;
-    h4 d5[2] = {h4{}, h4{}};
+    h4 d5[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) d5[u] = h4{};
     if (g == 0) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < G; ++u) {
             float y[3];
 #pragma unroll
             for (int k = 0; k < 3; ++k) y[k] = (float)(_Float16)fmaxf(o[u][k], 0.0f);
@@ -713,14 +718,14 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     }
     lossv = row_sum16(lossv);
     if (lane == 0) red[wave] = lossv;
-    int wo[2][4];
+    int wo[G][4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < G; ++u) {
         row_offsets(r[u], g, wo[u]);
         asm volatile("" : "+v"(wo[u][0]), "+v"(wo[u][1]), "+v"(wo[u][2]), "+v"(wo[u][3]));
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < G; ++u) {
         *(h4*)(img_d1 + off64(r[u], g)) = d5[u];
         put_rows64(img_a1, wo[u], a[4][u]);
     }
@@ -731,7 +736,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         loss_partials[blockIdx.x] = lp;
     }
 
-    h8 d[2][2], dn[2][2], W[4][2];
+    h8 d[G][2], dn[G][2], W[4][2];
     // step 5: delta_4 = W5^T delta_5 * [a_4 > 0] (16x16x16: K = 16 output rows) into buffer 0 with a_3
     {
         const h4* lwb4 = (const h4*)lwb;
@@ -739,7 +744,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) W5[mb] = lwb4[t16_bwd_frag(5, mb, 0) * 128 + lane];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < G; ++u) {
             f4 cc[4];
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) cc[mb] = mfma16k16(W5[mb], d5[u], f4{0.f, 0.f, 0.f, 0.f});
@@ -754,7 +759,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     // steps 4..1: delta_{L-1} into the other buffer with a_{L-2} (step 1: the input slots 0..63)
 #define NRC_T16S_STEP(L, NIMGD, NIMGA)                                                                              \
     {                                                                                                              \
-        _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
+        _Pragma("unroll") for (int u = 0; u < G; ++u) {                                                            \
             if constexpr (L > 1) {                                                                                 \
                 put_rows64(NIMGA, wo[u], a[L > 1 ? L - 2 : 0][u]);                                                 \
             } else {                                                                                               \
@@ -765,9 +770,9 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
                 }                                                                                                  \
             }                                                                                                      \
         }                                                                                                          \
-        chain_groups<2>(W, d, a[L - 1], dn);                                                                                \
+        chain_groups<G>(W, d, a[L - 1], dn);                                                                                \
         if constexpr (L > 1) load_wt<(L > 1 ? L - 1 : 1)>(lwb, lane, W);                                           \
-        _Pragma("unroll") for (int u = 0; u < 2; ++u) {                                                            \
+        _Pragma("unroll") for (int u = 0; u < G; ++u) {                                                            \
             put_rows64(NIMGD, wo[u], dn[u]);                                                                       \
             _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) d[u][s2] = dn[u][s2];                                 \
         }                                                                                                          \
@@ -780,13 +785,13 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #undef NRC_T16S_STEP
 }
 
-int t16_blocks(int64_t b) { return (int)((b + kTrainSamplesPerBlock - 1) / kTrainSamplesPerBlock); }
+int t16_blocks(int64_t b, int groups = 2) { return (int)((b + 64 * groups - 1) / (64 * groups)); }
 
 }  // namespace
 
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s, bool split) {
+                          hipStream_t s, bool split, int groups) {
     if (b <= 0) return hipSuccess;
     const dim3 grid(t16_blocks(b));
     const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
@@ -794,7 +799,18 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
         // slab stores as sc1 (AUX 16): they write through and drop the line from the XCD's L2, so the kernel does not end
         // with 5.9 MB of dirty slab lines to write back, and the reduce (on every XCD) reads them from memory either
         // way: fused step 14.2 -> 12.7 us against nt, gradients bitwise equal (profiles/r02_train/)
-        hipLaunchKernelGGL(train16_split_kernel<16>, grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
+        if (groups == 1) {
+            // 64 samples per block (debug library, A/B): twice the blocks (every CU at 16,384 samples), half the work
+            // each; bitwise the decoupled-chain shape 4, but 14.5-14.7 vs 12.9-13.7 us per step
+#if NRC_DEBUG_KERNELS
+            hipLaunchKernelGGL((train16_split_kernel<16, 1>), dim3(t16_blocks(b, 1)), dim3(128 * kWaves), 0, s, queries,
+                               targets, b, n_total, loss_scale, f, bw, slabs, loss_partials);
+            return hipGetLastError();
+#else
+            return hipErrorNotSupported;
+#endif
+        }
+        hipLaunchKernelGGL((train16_split_kernel<16, 2>), grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
                            loss_scale, f, bw, slabs, loss_partials);
         return hipGetLastError();
     }

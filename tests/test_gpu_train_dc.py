@@ -36,6 +36,7 @@ def knobs(nrc):
     yield nrc._lib
     nrc._lib.set_knob("train_kernel", -1)
     nrc._lib.set_knob("train_shape", -1)
+    nrc._lib.set_knob("t16_groups", -1)
     if nrc._lib.is_debug_library():
         nrc._lib.set_knob("dc_dw0_delay", -1)
 
@@ -84,6 +85,33 @@ def test_dc_shapes_match_oracle(nrc, orc, torch, dev, golden, knobs, shape, b, g
     assert abs(g[nrc.NUM_PARAMS] - loss_ref * scale) <= 1e-3 * abs(loss_ref * scale) + 1e-30
     assert (g[21504:22528].reshape(16, 64)[3:] == 0).all()  # padded output rows get no gradient
     net.destroy()
+
+
+@pytest.mark.parametrize("b", [16384, 5000, 17])
+def test_t16_64_sample_blocks(nrc, orc, torch, dev, golden, knobs, b):
+    """The role-split t16 kernel with one 16-sample group per chain wave (knob t16_groups = 1: 64 samples per block, every
+    CU busy at 16,384 samples): the same MFMA sequence per accumulator as the decoupled-chain kernel's 64-sample shape 4,
+    so the gradient is bitwise that shape's; and against the oracle at the gradient tolerance. Debug library (an A/B
+    kernel: slower than the 128-sample blocks)."""
+    if not nrc._lib.is_debug_library():
+        pytest.skip("A/B kernel of the debug library (libnrc_amd_debug.so)")
+    q_np, t_np = nrc.synthetic.cornell_batch(b, seed=1400 + b)
+    knobs.set_knob("t16_groups", 1)
+    knobs.set_knob("train_kernel", 1)  # the role-split kernel at every size
+    t16 = make_net(nrc, torch, golden["params_b"])
+    knobs.set_knob("train_kernel", -1)
+    knobs.set_knob("train_shape", 4)
+    dc = make_net(nrc, torch, golden["params_b"])
+    g = grad_of(nrc, torch, dev, t16, q_np, t_np, b, b)
+    g_dc = grad_of(nrc, torch, dev, dc, q_np, t_np, b, b)
+    g_ref, loss_ref = orc.grad(golden["params_b"], q_np, t_np, mode=orc.MIXED)
+    r = rel(g[:nrc.NUM_PARAMS], g_ref)
+    print(f"t16 G=1 b={b}: grad rel {r:.2e}, vs dc shape 4 max |diff| {np.abs(g - g_dc).max():.3e}")
+    assert r <= 2e-3
+    assert abs(g[nrc.NUM_PARAMS] - loss_ref) <= 1e-3 * abs(loss_ref)
+    np.testing.assert_array_equal(g, g_dc)
+    t16.destroy()
+    dc.destroy()
 
 
 def test_c4_rank_slice_train_dp(nrc, orc, torch, dev, golden):
