@@ -1096,13 +1096,18 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     // ABL & 8192 (ENC 0 / 3, TILES 1): queries through raw buffer loads (load_q_tile)
     constexpr bool kBufQ = (ABL & 8192) != 0 && (ENC == 0 || ENC == 3) && TILES == 1;
     const QOffsets vo{r * 60, r * 60 + 12 + 12 * h, r * 60 + 36 + 12 * h};
-    // ENC 3: the lane's 8 level features of the tile's query (levels 8h .. 8h + 7), prefetched with the query
+    // ENC 3: the lane's 8 level features of the tile's query (levels 8h .. 8h + 7), prefetched with the query, as raw
+    // buffer loads: one 32-bit lane offset per tile and the level stride in the scalar offset (instead of 8 64-bit
+    // addresses); rows past the workspace read 0, rows past n are never stored
     [[maybe_unused]] uint32_t F[8];
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rfeat =
+        buffer_rsrc(grid, ENC == 3 ? (int)(NRC_HASH_LEVELS * kHashFeatStride * 4) : 0);
     auto load_f = [&](int64_t tile) {
         if constexpr (ENC == 3) {
-            const int64_t sq = min(tile * 32 + r, last);
+            const int vo = (8 * h * (int)kHashFeatStride + (int)tile * 32 + r) * 4;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) F[i] = grid[(int64_t)(8 * h + i) * kHashFeatStride + sq];
+            for (int i = 0; i < 8; ++i)
+                F[i] = __builtin_amdgcn_raw_buffer_load_b32(rfeat, vo, i * (int)kHashFeatStride * 4, 0);
         }
     };
     static_assert(ENC != 3 || TILES == 1, "ENC 3 prefetches one tile");
