@@ -580,60 +580,37 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
     }
     const int64_t s0 = (int64_t)sub * n / P, s1 = (int64_t)(sub + 1) * n / P;
     const int cnt = (int)(s1 - s0);  // <= kHashFeatStride: 32-bit byte offsets below
-    uint32_t* const fb = feat + (int64_t)level * kHashFeatStride + s0;
+    // raw buffer descriptors over this block's range: position loads past it return 0, feature stores past it are
+    // dropped, so the loop has no branch around a memory op (a conditional store made the compiler wait vmcnt(0),
+    // i.e. for the store's acknowledgement, before the next iteration's prefetched position). All memory operations
+    // stay compiler-visible: an inline-asm load that the compiler cannot see in flight lets it reuse the destination
+    // registers before the data lands.
+    const __amdgpu_buffer_rsrc_t rq = buffer_rsrc(q + s0 * NRC_INPUT_DIMS, cnt * (NRC_INPUT_DIMS * 4));
+    const __amdgpu_buffer_rsrc_t rf = buffer_rsrc(feat + (int64_t)level * kHashFeatStride + s0, cnt * 4);
     typedef float f3 __attribute__((ext_vector_type(3)));
-    // Position loads and feature stores as inline asm: the compiler neither moves them nor waits for them (it sank
-    // compiler-visible loads issued two steps ahead to the loop latch, right before their use; a conditional store made
-    // it wait for the store's acknowledgement); the waits are explicit. vmcnt counts loads and stores in issue order;
-    // every step issues 2 loads then 2 stores, so the positions loaded two steps earlier are complete once at most 6
-    // operations are outstanding (the prologue pads the count with 2 x 2 extra loads). Lanes past the range load the
-    // range's last position and store its feature -- the same value to the same word as the lane that owns it.
-    const int64_t last = cnt > 0 ? cnt - 1 : 0;
-    const float* const qb = q + s0 * NRC_INPUT_DIMS;
-    auto load_pos = [&](int k, f3& dst) {
+    auto load_pos = [&](int k) -> f3 {
         if constexpr ((ABL & 2) != 0) {
             const float u = (float)(k & 1023) * (1.0f / 1024.0f);
-            dst = f3{u, 1.0f - u, u * u};
-        } else {
-            const float* src = qb + (int64_t)(k < last ? k : last) * NRC_INPUT_DIMS;
-            asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(dst) : "v"(src) : "memory");
+            return f3{u, 1.0f - u, u * u};
         }
+        return __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rq, k * (NRC_INPUT_DIMS * 4), 0, 0));
     };
-    auto store_feature = [&](int k, uint32_t f) {
-        if constexpr ((ABL & 4) == 0) {
-            uint32_t* dst = fb + (k < last ? k : last);
-            asm volatile("global_store_dword %0, %1, off" : : "v"(dst), "v"(f) : "memory");
-        } else {
-            f3 dummy;  // ablation: a load in place of the store keeps the vmcnt arithmetic
-            load_pos(k, dummy);
-            asm volatile("" : : "v"(dummy.x));
-        }
-    };
+    // two queries per lane per step (i, i + 1024), their positions two steps ahead in two register sets used
+    // alternately
     int i = threadIdx.x;
-    f3 PB[2][2], pad[4];
-    load_pos(i, PB[0][0]);
-    load_pos(i + 1024, PB[0][1]);
-    load_pos(i, pad[0]);
-    load_pos(i, pad[1]);
-    load_pos(i + 2048, PB[1][0]);
-    load_pos(i + 3072, PB[1][1]);
-    load_pos(i, pad[2]);
-    load_pos(i, pad[3]);
-    asm volatile("s_waitcnt vmcnt(8)" : "+v"(pad[0]), "+v"(pad[1]), "+v"(pad[2]), "+v"(pad[3]) : : "memory");
-    __syncthreads();  // the table DMA (issued before these 8 loads) has landed
+    f3 PB[2][2] = {{load_pos(i), load_pos(i + 1024)}, {load_pos(i + 2048), load_pos(i + 3072)}};
+    __syncthreads();  // (the compiler's vmcnt wait for the table DMA precedes it)
     const char* const ltb = reinterpret_cast<const char*>(lt);
     auto body = [&](auto dense_c) {
         constexpr bool kDense = decltype(dense_c)::value;
         auto step = [&](auto cur_c) -> bool {
             constexpr int cur = decltype(cur_c)::value;
             if (i - (int)threadIdx.x >= cnt) return false;  // block-uniform
-            if constexpr ((ABL & 2) == 0)
-                asm volatile("s_waitcnt vmcnt(6)" : "+v"(PB[cur][0]), "+v"(PB[cur][1]) : : "memory");
             LdsCorners C[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) hash_corners_lds<kDense>(PB[cur][u].x, PB[cur][u].y, PB[cur][u].z, level, C[u]);
-            load_pos(i + 4096, PB[cur][0]);
-            load_pos(i + 5120, PB[cur][1]);
+            PB[cur][0] = load_pos(i + 4096);
+            PB[cur][1] = load_pos(i + 5120);
             uint32_t v[2][8];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
@@ -646,7 +623,7 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
 #pragma unroll
                 for (int c = 0; c < 8; ++c) W.w[c] = C[u].w[c];
                 const uint32_t f = hash_interp(W, v[u]);
-                store_feature(i + 1024 * u, f);
+                __builtin_amdgcn_raw_buffer_store_b32(f, rf, (ABL & 4) ? kBufferOff : (i + 1024 * u) * 4, 0, 0);
             }
             i += 2048;
             return true;
