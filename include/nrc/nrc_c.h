@@ -187,8 +187,10 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 /* ---- test / tuning entries ---- */
 /* Process-wide A/B knobs (the library reads no environment variables): "train_kernel" (Frequency training kernel at
  * nrc_init: -1/0 decoupled chain, 1 / 2 round-2 t16 role-split / 4-wave, 32 round-1 32x32x16), "train_shape" (decoupled
- * chain block shape 0..5, -1 = by batch size), "scatter_min" / "scatter_max" (Hash grid-scatter slice plan). -1 restores
- * the production choice. */
+ * chain block shape 0..7, -1 = by batch size), "scatter_min" / "scatter_max" (Hash grid-scatter slice plan), "hash_infer"
+ * (Hash inference: 1 = the round-2 gather kernel instead of the LDS-table feature pass), "t16_groups" (1 = 64-sample blocks
+ * of the role-split kernel, debug library); debug library only: "dc_dw0_delay", "hash_feat_abl". -1 restores the
+ * production choice. */
 nrc_status nrc_debug_set_knob(const char* name, int value);
 nrc_status nrc_debug_get_knob(const char* name, int* value);
 /* Inference through a specific kernel variant for in-process A/B timing; results are identical in meaning to
