@@ -1,4 +1,4 @@
-"""Data-parallel sharding on CPU: torch.distributed gloo, world size 2 (the N > 1 path of bench.py,
+"""Data-parallel sharding on CPU: torch.distributed gloo, world sizes 2 and 4 (the N > 1 path of bench.py,
 with the gfx950 backend replaced by an oracle-backed stand-in that has the same train_grad /
 train_apply contract as nrc_amd.Network).
 
@@ -131,10 +131,11 @@ def _worker(rank, world, port, B, steps, out_dir, hash_grid=False, fixed=False):
     dist.destroy_process_group()
 
 
-def test_dp_step_equals_single_process_step(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_step_equals_single_process_step(tmp_path, world):
     import torch.multiprocessing as mp
 
-    world, B, steps = 2, 384, 3
+    B, steps = 384, 3
     mp.spawn(_worker, args=(world, _free_port(), B, steps, str(tmp_path)), nprocs=world, join=True)
     orc = nrc_loader.load_oracle()
     nrc = nrc_loader.load()
@@ -145,9 +146,10 @@ def test_dp_step_equals_single_process_step(tmp_path):
         g, loss = orc.grad(st.params, q, t, mode=orc.FP32, threads=2)
         st.apply(g)
         ref_losses.append(loss)
-    p0, p1 = np.load(tmp_path / "params_0.npy"), np.load(tmp_path / "params_1.npy")
-    np.testing.assert_array_equal(p0, p1)  # replicas identical
-    np.testing.assert_array_equal(np.load(tmp_path / "infer_0.npy"), np.load(tmp_path / "infer_1.npy"))
+    p0 = np.load(tmp_path / "params_0.npy")
+    for r in range(1, world):  # replicas identical
+        np.testing.assert_array_equal(p0, np.load(tmp_path / f"params_{r}.npy"))
+        np.testing.assert_array_equal(np.load(tmp_path / "infer_0.npy"), np.load(tmp_path / f"infer_{r}.npy"))
     assert np.linalg.norm(p0 - st.params) <= 1e-5 * np.linalg.norm(st.params)
     np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
 
