@@ -85,6 +85,30 @@ def test_infer_full_frame_deterministic_and_tiles_match_oracle(nrc, orc, dev, en
         net.destroy()
 
 
+@pytest.mark.parametrize("n", [(1 << 19) + 17, (1 << 21) + 77])
+def test_infer_rank_shard_and_ragged_frame(nrc, orc, dev, n):
+    """configs[3]'s per-rank shard size (2^19, plus a ragged tail) and a frame one partial tile past 2^21: the product
+    kernel's block ranges and LDS queue at other tile counts, every sampled tile against the oracle, the tail row
+    included, nothing written past n."""
+    import torch
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    try:
+        q_np = nrc.synthetic.cornell_queries(n, seed=33)
+        params = orc.init_params(1337) * np.float32(1.6)
+        net.set_state(nrc.StateSlot.INFER, params)
+        q = _t(q_np, dev)
+        o = torch.full((n + 8, 3), 777.0, device=dev)
+        net.infer(q, o, n)
+        torch.cuda.synchronize()
+        o = o.cpu().numpy()
+        assert (o[n:] == 777.0).all()
+        rows = np.union1d(_sample_rows(n), np.arange(n - 40, n))
+        _check_rows(o[rows], orc.forward(params, q_np[rows], orc.MIXED), 0.02)
+    finally:
+        net.destroy()
+
+
 def test_infer_accumulate_full_frame_deterministic(nrc, dev):
     """The fused infer + accumulate_render_radiance kernel on a 1080p frame: two launches, identical frame buffers."""
     import torch
