@@ -33,7 +33,7 @@ typedef enum nrc_status {
     NRC_ERR_HIP = 4,              /* HIP runtime failure (CU_CHECK -> std::runtime_error in the reference) */
     NRC_ERR_UNSUPPORTED = 5,
     NRC_ERR_OUT_OF_MEMORY = 6,
-    NRC_ERR_INTERNAL = 7
+    NRC_ERR_INTERNAL = 7          /* includes a training kernel's LDS-protocol timeout (sticky until nrc_init) */
 } nrc_status;
 
 typedef struct nrc_net nrc_net;
@@ -106,7 +106,10 @@ nrc_status nrc_train_async(nrc_net* net, const float* inputs_d, const float* tar
 
 /* infer(in, out, n) / infer(in, out, n, stream) (NRCNetwork.h:49-51). Processes exactly n queries
  * (the reference rounds n up to 256 and reads/writes past n, NRCNetwork.cu:72; this one never
- * touches the tail). n = 0 is a no-op. Uses the inference (EMA) weights. */
+ * touches the tail). n = 0 is a no-op. Uses the inference (EMA) weights. InputEncoding::Hash keeps one
+ * level-feature workspace per handle: an inference on another stream than the previous one first waits for it (an
+ * event), so calls on two streams serialise on the GPU rather than overlap. One handle is not for concurrent calls
+ * from several host threads. */
 nrc_status nrc_infer(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n);
 nrc_status nrc_infer_stream(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n, hipStream_t stream);
 
@@ -190,7 +193,9 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
  * chain block shape 0..7, -1 = by batch size), "scatter_min" / "scatter_max" (Hash grid-scatter slice plan), "hash_infer"
  * (Hash inference: 1 = the round-2 gather kernel instead of the LDS-table feature pass), "t16_groups" (1 = 64-sample blocks
  * of the role-split kernel, debug library); debug library only: "dc_dw0_delay", "hash_feat_abl". -1 restores the
- * production choice. */
+ * production choice. A value outside a knob's range (train_kernel -1/0/1/2/32, train_shape -1..7, scatter_* -1 or
+ * 16..2^20, hash_infer -1..1, t16_groups -1/1/2, dc_dw0_delay -1..2^20, hash_feat_abl -1..7) is
+ * NRC_ERR_INVALID_ARGUMENT and leaves the knob unchanged. */
 nrc_status nrc_debug_set_knob(const char* name, int value);
 nrc_status nrc_debug_get_knob(const char* name, int* value);
 /* Inference through a specific kernel variant for in-process A/B timing; results are identical in meaning to

@@ -316,16 +316,28 @@ struct nrc_net {
     float* dp_grad = nullptr;        // [grad_floats] gradient exchange buffer of nrc_train_dp
     float* loss_dev = nullptr;   // device view of loss_host
     float* loss_host = nullptr;
+    // training-protocol error word (round 4), in the same mapped allocation as the loss slots (index kProtoErrSlot):
+    // the decoupled-chain kernel sets it when a bounded LDS wait runs out (nrc_train_dc.hip lds_wait_ge); sticky until
+    // the next nrc_init, checked before every training launch and after every host sync of the training path
+    static constexpr int kProtoErrSlot = 4;
+    uint32_t* proto_err_dev() const { return reinterpret_cast<uint32_t*>(loss_dev + kProtoErrSlot); }
+    void check_protocol() const {
+        if (loss_host && reinterpret_cast<volatile uint32_t*>(loss_host)[kProtoErrSlot] != 0u)
+            throw ApiError(NRC_ERR_INTERNAL,
+                           "training kernel: an LDS protocol wait timed out (the gradient of that step and every state "
+                           "derived from it are invalid; re-initialise the network)");
+    }
     void alloc_loss_slots() {
         HIP_CHECK(hipMalloc(&work_queue, kInferPoolBytes));
         HIP_CHECK(hipMemset(work_queue, 0, kInferPoolBytes));
-        HIP_CHECK(hipHostMalloc(&loss_host, sizeof(float) * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_CHECK(hipHostMalloc(&loss_host, sizeof(float) * 8, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_CHECK(hipHostGetDevicePointer((void**)&loss_dev, loss_host, 0));
-        for (int i = 0; i < 4; ++i) loss_host[i] = 0.0f;
+        for (int i = 0; i < 8; ++i) loss_host[i] = 0.0f;
     }
     // stream-ordered read of loss slot 0 (blocks the host, as the reference's Trainer::loss does)
     float read_loss() {
         HIP_CHECK(hipStreamSynchronize(stream));
+        check_protocol();
         return loss_host[0];
     }
     // InputEncoding::Hash: grid part of the model arrays starts at n_mlp
@@ -336,6 +348,22 @@ struct nrc_net {
     _Float16 *table_train = nullptr, *table_infer = nullptr;
     uint32_t* hash_feat = nullptr;  // [NRC_HASH_LEVELS][kHashFeatStride] level features of an inference pass
     uint32_t* hash_feat_arg() const { return knob(kKnobHashInfer) == 1 ? nullptr : hash_feat; }
+    // The feature workspace is one per handle, and nrc_infer_stream / the fused accumulation may launch each call on
+    // another stream: a Hash inference on stream s first waits for the previous one's MLP pass when that
+    // ran on another stream (an event recorded after it), so overlapping calls serialise instead of overwriting each
+    // other's level features. Calls on one stream need nothing (stream order).
+    hipEvent_t feat_done = nullptr;
+    hipStream_t feat_stream = nullptr;
+    bool feat_pending = false;
+    void hash_feat_acquire(hipStream_t s) {
+        if (feat_pending && feat_stream != s) HIP_CHECK(hipStreamWaitEvent(s, feat_done, 0));
+    }
+    void hash_feat_release(hipStream_t s) {
+        if (!feat_done) HIP_CHECK(hipEventCreateWithFlags(&feat_done, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(feat_done, s));
+        feat_stream = s;
+        feat_pending = true;
+    }
     HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
     int scatter_blocks = 0;
     uint8_t* grid_nf = nullptr;       // [n_grid] non-finite contribution codes (GridNonFinite)
@@ -378,6 +406,10 @@ struct nrc_net {
         dp_grad = nullptr;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer); f(hash_feat);
         hash_feat = nullptr;
+        if (feat_done) (void)hipEventDestroy(feat_done);
+        feat_done = nullptr;
+        feat_stream = nullptr;
+        feat_pending = false;
         f(grid_nf); f(grid_nf_tag);
         grid_nf = nullptr;
         grid_nf_tag = nullptr;
@@ -526,6 +558,7 @@ int dc_shape(uint32_t b) {
 int train_block_count(const nrc_net* net, uint32_t b) {
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0) {
         const int S = dc_samples_per_block(dc_shape(b));
+        if (S <= 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "train_shape knob names no decoupled-chain shape");
         return (int)((b + (uint32_t)S - 1) / (uint32_t)S);
     }
     if (net->t16 && net->t16_kernel != 2) {
@@ -538,9 +571,11 @@ int train_block_count(const nrc_net* net, uint32_t b) {
 // 64-wide Frequency / FrequencySH fwd + loss + bwd + per-block dW slabs (n_total = 3 x global batch)
 void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total,
                     uint64_t* stamps = nullptr) {
+    net->check_protocol();  // an earlier step's kernel (completed by now or not) may have reported a timeout
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0)
         HIP_CHECK(launch_train_dc(dc_shape(b), in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, net->stream, stamps));
+                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, net->proto_err_dev(),
+                                  net->stream, stamps));
     else if (net->t16)
         HIP_CHECK(launch_train16(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream,
@@ -596,9 +631,14 @@ hipError_t infer_wide(nrc_net* net, int prec, const float* in, float* out, uint3
 hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
     if (net->wide())
         return infer_wide(net, (int)net->cfg.infer_precision, in, out, n, nullptr, nullptr, 0, -1, 1.0f, net->stream);
-    if (net->hash())
-        return launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream,
-                                 net->hash_feat_arg());
+    if (net->hash()) {
+        uint32_t* const feat = net->hash_feat_arg();
+        if (feat) net->hash_feat_acquire(net->stream);
+        const hipError_t e = launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f,
+                                               net->stream, feat);
+        if (e == hipSuccess && feat) net->hash_feat_release(net->stream);
+        return e;
+    }
     if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
         return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     return launch_infer(in, out, n, net->wf_infer, net->stream, net->work_queue, &net->pool_parity);
@@ -647,6 +687,21 @@ nrc_loss_slots nrc_amd::net_loss_slots(nrc_net* net) {
 int nrc_amd::knob(Knob k) { return g_knobs[k].load(std::memory_order_relaxed); }
 
 namespace {
+// accepted values per knob (an out-of-range train_shape made train_block_count divide by zero); -1 = default
+bool knob_value_ok(Knob k, int v) {
+    switch (k) {
+        case kKnobTrainKernel: return v == -1 || v == 0 || v == 1 || v == 2 || v == 32;
+        case kKnobTrainShape: return v >= -1 && v <= 7;
+        case kKnobScatterMin:
+        case kKnobScatterMax: return v == -1 || (v >= 16 && v <= (1 << 20));
+        case kKnobDcDw0Delay: return v >= -1 && v <= (1 << 20);
+        case kKnobHashInfer: return v >= -1 && v <= 1;
+        case kKnobHashFeatAbl: return v >= -1 && v <= 7;
+        case kKnobT16Groups: return v == -1 || v == 1 || v == 2;
+        default: return false;
+    }
+}
+
 const char* const kDebugOnly =
     "diagnostic kernel of the debug library: load libnrc_amd_debug.so (NRC_LIB_PATH) for stamps, clocks and A/B variants";
 }
@@ -658,6 +713,9 @@ nrc_status nrc_debug_set_knob(const char* name, int value) {
         if (!name) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null knob name");
         for (int k = 0; k < kKnobCount; ++k)
             if (std::strcmp(name, kKnobNames[k]) == 0) {
+                if (!knob_value_ok(static_cast<Knob>(k), value))
+                    throw ApiError(NRC_ERR_INVALID_ARGUMENT,
+                                   std::string("knob ") + name + ": value " + std::to_string(value) + " out of range");
                 g_knobs[k].store(value, std::memory_order_relaxed);
                 return;
             }
@@ -903,9 +961,13 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
         if (net->wide())
             HIP_CHECK(infer_wide(net, (int)net->cfg.infer_precision, in, out, n, reinterpret_cast<const float*>(thr),
                                  rgba, num_pixels, mode, w, net->stream));
-        else if (net->hash())
+        else if (net->hash()) {
+            uint32_t* const feat = net->hash_feat_arg();
+            if (feat) net->hash_feat_acquire(net->stream);
             HIP_CHECK(launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, reinterpret_cast<const float*>(thr),
-                                        rgba, num_pixels, mode, w, net->stream, net->hash_feat_arg()));
+                                        rgba, num_pixels, mode, w, net->stream, feat));
+            if (feat) net->hash_feat_release(net->stream);
+        }
         else if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
             HIP_CHECK(launch_infer_sh(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba, num_pixels,
                                       mode, w, net->stream));
@@ -1137,6 +1199,7 @@ void do_train_apply(nrc_net* net, const float* grad_d, float* loss_h, float* los
     if (loss_h) {
         if (loss_d) {
             HIP_CHECK(hipStreamSynchronize(net->stream));
+            net->check_protocol();
             HIP_CHECK(hipMemcpy(loss_h, loss_d, sizeof(float), hipMemcpyDeviceToHost));
         } else {
             *loss_h = net->read_loss();
@@ -1206,6 +1269,7 @@ nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst) {
         if (!host_dst) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null destination");
         float* src = slot_ptr(net, slot);
         HIP_CHECK(hipStreamSynchronize(net->stream));
+        net->check_protocol();
         HIP_CHECK(hipMemcpy(host_dst, src, sizeof(float) * net->n_total(), hipMemcpyDeviceToHost));
     });
 }

@@ -291,10 +291,11 @@ int t16_groups();  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16
 // slab format as launch_train16; one slab per block of dc_samples_per_block(shape) samples.
 int dc_samples_per_block(int shape);
-// stamps (diagnostic, may be null): 16 uint64 per wave [block][wave][16], dc_waves_per_block(shape) waves per block
+// stamps (diagnostic, may be null): 16 uint64 per wave [block][wave][16], dc_waves_per_block(shape) waves per block;
+// err (required): set to 1 by a wave whose bounded LDS-protocol wait ran out (the step's slabs are then invalid)
 hipError_t launch_train_dc(int shape, const float* queries, const float* targets, int64_t b, float n_total,
                            float loss_scale, const _Float16* wf, const _Float16* wb, _Float16* slabs,
-                           float* loss_partials, hipStream_t s, uint64_t* stamps = nullptr);
+                           float* loss_partials, uint32_t* err, hipStream_t s, uint64_t* stamps = nullptr);
 int dc_waves_per_block(int shape);
 // the production shape for a batch of b samples
 int dc_auto_shape(int64_t b);

@@ -599,7 +599,10 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
     // alternately
     int i = threadIdx.x;
     f3 PB[2][2] = {{load_pos(i), load_pos(i + 1024)}, {load_pos(i + 2048), load_pos(i + 3072)}};
-    __syncthreads();  // (the compiler's vmcnt wait for the table DMA precedes it)
+    // the table DMA is counted on vmcnt, and a workgroup barrier does not wait for it: every wave's copy must have
+    // landed before any wave reads the table (the other LDS-copy sites wait the same way)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     const char* const ltb = reinterpret_cast<const char*>(lt);
     auto body = [&](auto dense_c) {
         constexpr bool kDense = decltype(dense_c)::value;

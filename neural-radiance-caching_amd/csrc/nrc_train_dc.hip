@@ -48,9 +48,14 @@ constexpr int flag_dwdone(int L) { return 12 + (L - 2); }  // L = 2, 3, 4 -> 12,
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// bounded (~2^20 polls, tens of ms): a protocol error ends the kernel with wrong results instead of a hang
-__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
-    for (int i = 0; lds_load(p) < v && i < (1 << 20); ++i) __builtin_amdgcn_s_sleep(1);
+// bounded (2^20 polls, tens of ms) so that a protocol error cannot hang the GPU; a wave that gives up sets the launch's
+// error word (host-mapped, nrc_net::proto_err), which the host turns into NRC_ERR_INTERNAL at its next check (round 4:
+// before, a timeout gave a wrong gradient with NRC_OK)
+constexpr int kPollBound = 1 << 20;
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v, uint32_t* err, int lane) {
+    int i = 0;
+    for (; lds_load(p) < v && i < kPollBound; ++i) __builtin_amdgcn_s_sleep(1);
+    if (i == kPollBound && lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("" ::: "memory");  // no LDS read of the published data above the poll
 }
 // publish: this wave's LDS writes have landed (lgkmcnt), then one lane bumps the counter
@@ -91,7 +96,7 @@ struct Stamper {
 template <int CW, int GPW, int DWW, bool STAMP>
 __device__ __forceinline__ void dc_chain(const float* __restrict__ q, const float* __restrict__ t, int64_t b,
                                          float n_total, float loss_scale, const h8* __restrict__ wf,
-                                         const h8* __restrict__ wb, char* smem, int cw, int lane,
+                                         const h8* __restrict__ wb, char* smem, int cw, int lane, uint32_t* err,
                                          const Stamper<STAMP>& stamp) {
     using Lay = DcLayout<CW, GPW>;
     constexpr int S = Lay::S;
@@ -262,7 +267,7 @@ __device__ __forceinline__ void dc_chain(const float* __restrict__ q, const floa
             W[mb][1] = w[2 * mb + 1];
         }
         chain_groups<GPW>(W, d, a[L - 1], dn);
-        if (L <= 3) lds_wait_ge(flags + flag_dwdone(L + 1), (uint32_t)DWW);  // buffer (L - 1) & 1 held delta_{L+1}
+        if (L <= 3) lds_wait_ge(flags + flag_dwdone(L + 1), (uint32_t)DWW, err, lane);  // buffer (L-1)&1 held delta_{L+1}
         char* const buf = smem + Lay::OFF_D + ((L - 1) & 1) * Lay::IMG;
 #pragma unroll
         for (int u = 0; u < GPW; ++u) {
@@ -331,13 +336,14 @@ constexpr int dc_npairs() { return L == 5 ? 2 : L == 0 ? 12 : 8; }
 
 template <int CW, int GPW, int DWW, int L, bool STAMP>
 __device__ __forceinline__ void dc_dw_step(char* smem, int dw, int lane, _Float16* __restrict__ slab,
-                                           float* __restrict__ loss_partials, const Stamper<STAMP>& stamp) {
+                                           float* __restrict__ loss_partials, uint32_t* err,
+                                           const Stamper<STAMP>& stamp) {
     using Lay = DcLayout<CW, GPW>;
     constexpr int S = Lay::S;
     constexpr int NP = dc_npairs<L>();
     constexpr int PER = (NP + DWW - 1) / DWW;
     uint32_t* flags = (uint32_t*)(smem + Lay::OFF_FLAGS);
-    lds_wait_ge(flags + L, (uint32_t)CW);
+    lds_wait_ge(flags + L, (uint32_t)CW, err, lane);
     stamp(1 + 2 * (5 - L));
     if (L == 5 && dw == 0 && lane == 0) {
         const float* red = (const float*)(flags + kFlagRed);
@@ -390,24 +396,24 @@ __device__ int g_dc_dw0_delay = 0;
 
 template <int CW, int GPW, int DWW, bool STAMP>
 __device__ __forceinline__ void dc_dw(char* smem, int dw, int lane, _Float16* __restrict__ slab,
-                                      float* __restrict__ loss_partials, const Stamper<STAMP>& stamp) {
-    dc_dw_step<CW, GPW, DWW, 5, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
+                                      float* __restrict__ loss_partials, uint32_t* err, const Stamper<STAMP>& stamp) {
+    dc_dw_step<CW, GPW, DWW, 5, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
 #if NRC_DEBUG_KERNELS
     if (dw == 0)
         for (int i = 0; i < g_dc_dw0_delay; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
-    dc_dw_step<CW, GPW, DWW, 4, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
-    dc_dw_step<CW, GPW, DWW, 3, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
-    dc_dw_step<CW, GPW, DWW, 2, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
-    dc_dw_step<CW, GPW, DWW, 1, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
-    dc_dw_step<CW, GPW, DWW, 0, STAMP>(smem, dw, lane, slab, loss_partials, stamp);
+    dc_dw_step<CW, GPW, DWW, 4, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
+    dc_dw_step<CW, GPW, DWW, 3, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
+    dc_dw_step<CW, GPW, DWW, 2, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
+    dc_dw_step<CW, GPW, DWW, 1, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
+    dc_dw_step<CW, GPW, DWW, 0, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
 }
 
 template <int CW, int GPW, int DWW, bool STAMP = false>
 __global__ __launch_bounds__(64 * (CW + DWW), (CW + DWW + 3) / 4) void train_dc_kernel(
     const float* __restrict__ q, const float* __restrict__ t, int64_t b, float n_total, float loss_scale,
     const h8* __restrict__ wf, const h8* __restrict__ wb, _Float16* __restrict__ slabs, float* __restrict__ loss_partials,
-    uint64_t* __restrict__ stamps) {
+    uint32_t* err, uint64_t* __restrict__ stamps) {
     using Lay = DcLayout<CW, GPW>;
     __shared__ __attribute__((aligned(16))) char smem[Lay::BYTES];
     const int lane = threadIdx.x & 63;
@@ -418,28 +424,29 @@ __global__ __launch_bounds__(64 * (CW + DWW), (CW + DWW + 3) / 4) void train_dc_
     if (threadIdx.x < 16) ((uint32_t*)(smem + Lay::OFF_FLAGS))[threadIdx.x] = 0;
     __syncthreads();
     if (wave < CW)
-        dc_chain<CW, GPW, DWW, STAMP>(q, t, b, n_total, loss_scale, wf, wb, smem, wave, lane, stamp);
+        dc_chain<CW, GPW, DWW, STAMP>(q, t, b, n_total, loss_scale, wf, wb, smem, wave, lane, err, stamp);
     else
         dc_dw<CW, GPW, DWW, STAMP>(smem, wave - CW, lane, slabs + (int64_t)blockIdx.x * slab_floats(0), loss_partials,
-                                   stamp);
+                                   err, stamp);
     stamp.real(15);
 }
 
 template <int CW, int GPW, int DWW>
 hipError_t launch_dc(const float* q, const float* t, int64_t b, float n_total, float loss_scale, const _Float16* wf,
-                     const _Float16* wb, _Float16* slabs, float* loss_partials, hipStream_t s, uint64_t* stamps) {
+                     const _Float16* wb, _Float16* slabs, float* loss_partials, uint32_t* err, hipStream_t s,
+                     uint64_t* stamps) {
     constexpr int S = DcLayout<CW, GPW>::S;
     const int blocks = (int)((b + S - 1) / S);
 #if NRC_DEBUG_KERNELS
     if (stamps)
         hipLaunchKernelGGL((train_dc_kernel<CW, GPW, DWW, true>), dim3(blocks), dim3(64 * (CW + DWW)), 0, s, q, t, b,
-                           n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, stamps);
+                           n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, err, stamps);
     else
 #else
     if (stamps) return hipErrorNotSupported;  // stamped builds live in libnrc_amd_debug.so
 #endif
         hipLaunchKernelGGL((train_dc_kernel<CW, GPW, DWW>), dim3(blocks), dim3(64 * (CW + DWW)), 0, s, q, t, b,
-                           n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr);
+                           n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, err, nullptr);
     return hipGetLastError();
 }
 
@@ -480,8 +487,9 @@ int dc_waves_per_block(int shape) {
 
 hipError_t launch_train_dc(int shape, const float* queries, const float* targets, int64_t b, float n_total,
                            float loss_scale, const _Float16* wf, const _Float16* wb, _Float16* slabs,
-                           float* loss_partials, hipStream_t s, uint64_t* stamps) {
+                           float* loss_partials, uint32_t* err, hipStream_t s, uint64_t* stamps) {
     if (b <= 0) return hipSuccess;
+    if (!err) return hipErrorInvalidValue;
 #if NRC_DEBUG_KERNELS
     static int applied = 0;
     const int delay = std::max(knob(kKnobDcDw0Delay), 0);
@@ -492,14 +500,14 @@ hipError_t launch_train_dc(int shape, const float* queries, const float* targets
     }
 #endif
     switch (shape) {
-        case 0: return launch_dc<1, 1, 1>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 1: return launch_dc<1, 2, 1>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 2: return launch_dc<2, 2, 2>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 3: return launch_dc<4, 2, 4>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 4: return launch_dc<4, 1, 4>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 5: return launch_dc<2, 1, 2>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 6: return launch_dc<1, 1, 2>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
-        case 7: return launch_dc<2, 1, 4>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, s, stamps);
+        case 0: return launch_dc<1, 1, 1>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 1: return launch_dc<1, 2, 1>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 2: return launch_dc<2, 2, 2>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 3: return launch_dc<4, 2, 4>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 4: return launch_dc<4, 1, 4>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 5: return launch_dc<2, 1, 2>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 6: return launch_dc<1, 1, 2>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
+        case 7: return launch_dc<2, 1, 4>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s, stamps);
         default: return hipErrorInvalidValue;
     }
 }

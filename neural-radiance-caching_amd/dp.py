@@ -39,7 +39,11 @@ class DataParallelTrainer:
         self.grad = grad_buffer  # torch tensor of backend.grad_floats f32 on the backend's device
         self.group = group
         self.grid_fixed = grid_fixed  # Hash exact exchange: int64 [HASH_GRID_PARAMS] on the backend's device
-        self.mlp_params = mlp_params  # with grid_fixed: the MLP part of grad (loss at grad[-4])
+        # with grid_fixed: the MLP part of grad (loss at grad[-4]); required, since grad[:None] would be the whole
+        # buffer (the loss summed twice and the unwritten grid part reduced)
+        if grid_fixed is not None and (mlp_params is None or not 0 < int(mlp_params) <= len(grad_buffer) - 4):
+            raise ValueError("DataParallelTrainer: grid_fixed needs mlp_params (HASH_MLP_PARAMS), the MLP part of grad")
+        self.mlp_params = None if mlp_params is None else int(mlp_params)
         self._dist = dist
 
     def broadcast_state(self, net, device) -> None:

@@ -69,6 +69,25 @@ def test_library_loads_and_host_entry_points(nrc):
     assert L.nrc_create(None) == 1
 
 
+def test_knob_values_are_range_checked(nrc):
+    """nrc_debug_set_knob stored any integer, and train_shape >= 8 made the next training call divide by
+    zero (SIGFPE). Out-of-range values are NRC_ERR_INVALID_ARGUMENT now and leave the knob unchanged (no GPU needed)."""
+    L = nrc._lib
+    bad = {"train_shape": [8, 100, -2], "train_kernel": [3, 31, 33, -5], "t16_groups": [0, 3], "hash_infer": [2, -2],
+           "scatter_min": [0, 15, 1 << 21], "scatter_max": [7], "hash_feat_abl": [8], "dc_dw0_delay": [-2, 1 << 21]}
+    for name, values in bad.items():
+        before = L.get_knob(name)
+        for v in values:
+            with pytest.raises(nrc.NrcError) as e:
+                L.set_knob(name, v)
+            assert e.value.status == 1 and "out of range" in str(e.value), (name, v)
+            assert L.get_knob(name) == before
+    for name, v in [("train_shape", 7), ("train_kernel", 32), ("t16_groups", 1), ("scatter_min", 1024)]:
+        L.set_knob(name, v)
+        assert L.get_knob(name) == v
+        L.set_knob(name, -1)
+
+
 def test_python_mirror_is_silent_after_destroy(nrc):
     net = nrc.Network()
     net.destroy()

@@ -248,3 +248,18 @@ def test_dp_trainer_fixed_grid_exchange(tmp_path):
     np.testing.assert_array_equal(p0[M:], st.params[M:])
     assert np.linalg.norm(p0[:M] - st.params[:M]) <= 1e-5 * np.linalg.norm(st.params[:M])
     np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), ref_losses, rtol=1e-5)
+
+
+def test_dp_trainer_fixed_grid_requires_mlp_params():
+    """with grid_fixed but no mlp_params, grad[:None] was the whole buffer (the loss all-reduced twice, the
+    unwritten grid part reduced); the trainer now refuses that configuration."""
+    import torch
+
+    nrc = nrc_loader.load()
+    grad = torch.zeros(nrc.HASH_GRAD_FLOATS)
+    fixed = torch.zeros(nrc.HASH_GRID_PARAMS, dtype=torch.int64)
+    for bad in (None, 0, nrc.HASH_GRAD_FLOATS):
+        with pytest.raises(ValueError):
+            nrc.dp.DataParallelTrainer(object(), grad, grid_fixed=fixed, mlp_params=bad)
+    t = nrc.dp.DataParallelTrainer(object(), grad, grid_fixed=fixed, mlp_params=nrc.HASH_MLP_PARAMS)
+    assert t.mlp_params == nrc.HASH_MLP_PARAMS

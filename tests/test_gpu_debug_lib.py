@@ -65,7 +65,8 @@ def test_debug_library_variants_in_subprocess():
            "tests/test_gpu_parity.py::test_pooled_variant_bitwise_and_reusable",
            "tests/test_gpu_wide.py::test_wide_kernel_variant_bit_identical",
            "tests/test_gpu_debug_lib.py::test_debug_entry_points",
-           "tests/test_gpu_train_dc.py::test_dc_gradient_is_deterministic_with_a_slow_dw_wave"]
+           "tests/test_gpu_train_dc.py::test_dc_gradient_is_deterministic_with_a_slow_dw_wave",
+           "tests/test_gpu_train_dc.py::test_dc_protocol_timeout_is_reported"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     print(r.stdout[-3000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

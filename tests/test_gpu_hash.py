@@ -126,6 +126,32 @@ def test_hash_feature_pass_bitwise_gather_kernel(nrc, dev, hnet, orc, n):
     assert torch.equal(a, b), f"{int((a != b).any(dim=1).sum())} rows differ"
 
 
+def test_hash_inference_on_two_streams(nrc, dev, hnet, orc):
+    """the level-feature workspace is one per handle. Two inferences issued back to back on two streams (no
+    host sync between them; the first one's MLP pass still reading the workspace when the second is enqueued) must
+    each give the single-stream result: the library makes the second stream wait for the first call's event."""
+    import torch
+    hnet.set_state(nrc.StateSlot.INFER, _trained_like(orc))
+    n = 1 << 20
+    qa = _t(nrc.synthetic.cornell_queries(n, seed=31), dev)
+    qb = _t(nrc.synthetic.cornell_queries(n, seed=32), dev)
+    ref_a = torch.zeros((n, 3), device=dev)
+    ref_b = torch.zeros((n, 3), device=dev)
+    hnet.infer(qa, ref_a, n)
+    hnet.infer(qb, ref_b, n)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        a = torch.zeros((n, 3), device=dev)
+        b = torch.zeros((n, 3), device=dev)
+        torch.cuda.synchronize()
+        hnet.infer(qa, a, n, stream=s1)
+        hnet.infer(qb, b, n, stream=s2)
+        torch.cuda.synchronize()
+        assert torch.equal(a, ref_a) and torch.equal(b, ref_b)
+    hnet.setStream(torch.cuda.current_stream())
+
+
 def test_hash_feature_pass_fused_across_passes(nrc, dev, hnet, orc):
     """Fused accumulation over two feature passes, the render/train boundary inside the second: bitwise the gather
     kernel's frame buffer and train-suffix radiance."""

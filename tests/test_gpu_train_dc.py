@@ -178,3 +178,32 @@ def test_dc_gradient_is_deterministic_with_a_slow_dw_wave(nrc, torch, dev, knobs
             knobs.set_knob("dc_dw0_delay", delay)
             np.testing.assert_array_equal(grad_of(nrc, torch, dev, net, q_np, t_np, B, B), ref)
     net.destroy()
+
+
+def test_dc_protocol_timeout_is_reported(nrc, torch, dev, knobs):
+    """a bounded LDS-protocol wait that runs out must not pass silently. dW wave 0 idles ~2^17
+    rounds of s_sleep(127) (~1.07e9 clocks) after its step 5, far past the chain's 2^20-poll bound (<= ~4e8 clocks),
+    so the chain gives up waiting for delta_4's buffer; the wave sets the handle's error word and the next training
+    call or state read returns NRC_ERR_INTERNAL (sticky until nrc_init). Debug library only (tests/test_gpu_debug_lib.py
+    runs it there)."""
+    if not nrc._lib.is_debug_library():
+        pytest.skip("needs libnrc_amd_debug.so (NRC_LIB_PATH)")
+    knobs.set_knob("train_shape", 7)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    B = 2048
+    q_np, t_np = nrc.synthetic.cornell_batch(B, seed=300)
+    grad_of(nrc, torch, dev, net, q_np, t_np, B, B)  # clean step: no report
+    knobs.set_knob("dc_dw0_delay", 1 << 17)
+    grad_of(nrc, torch, dev, net, q_np, t_np, B, B)  # the launch that times out (reported at the next check)
+    knobs.set_knob("dc_dw0_delay", 0)
+    with pytest.raises(nrc._lib.NrcError) as e:
+        net.get_state(nrc.StateSlot.PARAMS)
+    assert e.value.status == 7 and "protocol" in str(e.value)
+    with pytest.raises(nrc._lib.NrcError) as e:
+        grad_of(nrc, torch, dev, net, q_np, t_np, B, B)
+    assert e.value.status == 7
+    net.init(stream=torch.cuda.current_stream())  # re-initialised: clean again
+    grad_of(nrc, torch, dev, net, q_np, t_np, B, B)
+    net.get_state(nrc.StateSlot.PARAMS)
+    net.destroy()
