@@ -751,13 +751,23 @@ __device__ __forceinline__ void layer_mfma(const h8 (&a)[2][KK], const h8 (&in)[
     f16v c[TILES][2];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
+    if constexpr ((ABL & 131072) != 0) {
+        // A-major order (round 4, energy A/B): consecutive MFMAs share the A operand (weight fragment) across tiles
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
+        for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-        for (int t = 0; t < TILES; ++t) {
-            c[t][0] = mfma(a[0][kk], in[t][kk], c[t][0]);
-            c[t][1] = mfma(a[1][kk], in[t][kk], c[t][1]);
-        }
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int t = 0; t < TILES; ++t) c[t][m] = mfma(a[m][kk], in[t][kk], c[t][m]);
+    } else {
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+            for (int t = 0; t < TILES; ++t) {
+                c[t][0] = mfma(a[0][kk], in[t][kk], c[t][0]);
+                c[t][1] = mfma(a[1][kk], in[t][kk], c[t][1]);
+            }
+    }
 #pragma unroll
     for (int t = 0; t < TILES; ++t) {
         y[t][0] = relu_h8<ABL>(c[t][0], 0);
@@ -808,14 +818,14 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
         {
             h8 a0[2][KK0];
             load_frags<KK0, ABL & 7>(lw_lane, 0, a0);
-            layer_mfma<TILES, KK0, ABL & 7>(a0, x, y);
+            layer_mfma<TILES, KK0, ABL & (7 | 131072)>(a0, x, y);
         }
         mark(1);
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
             h8 a[2][4];
             load_frags<4, ABL & 7>(lw_lane, l, a);
-            layer_mfma<TILES, 4, ABL & 7>(a, y, z);
+            layer_mfma<TILES, 4, ABL & (7 | 131072)>(a, y, z);
 #pragma unroll
             for (int t = 0; t < TILES; ++t)
 #pragma unroll
@@ -1251,7 +1261,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             ph[0] += tn - tprev;
             tprev = tn;
         }
-        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256 | 65536), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
+        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256 | 65536 | 131072), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
         if constexpr ((ABL & 8) && EPI < 0) {
             const int64_t s0 = g * TILES * 32;
             if (out16 && s0 + TILES * 32 <= n) {
@@ -2989,6 +2999,14 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 39: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192>, 1024, bpc[39], ntiles, queries, out, n, wf, s);
         // 48: 47 with the in-kernel clock
         case 48: return launch_clocked(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | 512>, 1024, bpc[48], ntiles, queries, out, n, wf, s);
+        // round 4 (energy per query): 47's body with two 32-query tiles per wave iteration, every
+        // weight-fragment read from LDS feeding both tiles (23.5 instead of 47 ds_read_b128 per tile); 52: 512-thread
+        // blocks at 2 waves per SIMD, 53: 52 with A-major MFMA order (consecutive MFMAs share the weight operand), 54:
+        // 768-thread blocks at 3 waves per SIMD (<= 168 VGPRs), 55: 54 A-major. Groups of 2 tiles: ntiles / 2 groups.
+        case 52: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, false, 48 | 1024 | 2048 | 65536>, 512, bpc[52], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 53: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, false, 48 | 1024 | 2048 | 65536 | 131072>, 512, bpc[53], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 54: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536>, 768, bpc[54], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 55: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536 | 131072>, 768, bpc[55], (ntiles + 1) / 2, queries, out, n, wf, s);
 #endif
         // 47 (default, round 3): 39 with the output layer on 4x4x4 16-block MFMAs (65536); in-process A/B at 2^21
         // queries 82.3-82.6 vs 82.7-83.4 us (profiles/r03_infer/ab_out4x4_v47.json)
