@@ -48,14 +48,19 @@ typedef struct nrc_config {
     uint64_t seed;       /* weight initialisation seed */
     /* Extensions (BASELINE.json configs[4]; not in the reference, whose FullyFusedMLP has 64 neurons): */
     uint32_t width;           /* MLP neurons: 64 (reference) or 128 (NRC_WIDE_*; Frequency / FrequencySH only) */
-    uint32_t infer_precision; /* nrc_precision of infer(): F16 (reference numerics) or FP8 (width 128 only) */
+    uint32_t infer_precision; /* nrc_precision of infer(): F16 (default), F16_ACC16 (tcnn's f16 accumulation, width 64
+                               * Frequency only) or FP8 (width 128 only) */
 } nrc_config;
 
-/* Arithmetic of infer() (nrc_config.infer_precision). FP8: e4m3 weights (one power-of-two scale per output row)
- * and e4m3 activations on the MX-scaled fp8 MFMA for layers 1..5, layer 0 in f16. */
+/* Arithmetic of infer() (nrc_config.infer_precision). F16: f16 operands, f32 accumulation per layer (the fast path).
+ * F16_ACC16: tiny-cuda-nn's FullyFusedMLP numerics, an f16 accumulator rounded after every 16-wide K chunk in K order
+ * (NRCNetworkConfigs.h:26-33; oracle mode ORC_TCNN), about 3-4x slower; infer / infer_stream only.
+ * FP8: e4m3 weights (one power-of-two scale per output row) and e4m3 activations on the MX-scaled fp8 MFMA for layers
+ * 1..5, layer 0 in f16. */
 typedef enum nrc_precision {
     NRC_PRECISION_F16 = 0,
-    NRC_PRECISION_FP8 = 1
+    NRC_PRECISION_FP8 = 1,
+    NRC_PRECISION_F16_ACC16 = 2
 } nrc_precision;
 
 /* HyperParams (NRCNetwork.h:10-13) */

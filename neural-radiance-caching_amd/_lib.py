@@ -25,7 +25,7 @@ HASH_MLP_PARAMS = 21504                              # NRC_HASH_MLP_PARAMS
 HASH_GRID_PARAMS = HASH_NUM_PARAMS - HASH_MLP_PARAMS  # NRC_HASH_GRID_PARAMS: int64 sums of nrc_train_grad_fixed
 FIXED_MAX_RANKS = 63                                 # NRC_FIXED_MAX_RANKS
 WIDE_NUM_PARAMS = 77824  # width-128 network (BASELINE configs[4])
-PRECISION_F16, PRECISION_FP8 = 0, 1
+PRECISION_F16, PRECISION_FP8, PRECISION_F16_ACC16 = 0, 1, 2  # nrc_precision (nrc_c.h)
 BATCH_SIZE = 16384
 INPUT_DIMS = 15
 OUTPUT_DIMS = 3

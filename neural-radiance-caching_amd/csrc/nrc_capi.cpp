@@ -641,6 +641,8 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
     }
     if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
         return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
+    if (net->cfg.infer_precision == NRC_PRECISION_F16_ACC16)
+        return launch_infer_tcnn(in, out, n, net->wf_infer, net->infer, net->stream);
     return launch_infer(in, out, n, net->wf_infer, net->stream, net->work_queue, &net->pool_parity);
 }
 
@@ -779,8 +781,11 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         const nrc_config c = cfg ? *cfg : nrc_default_config(encoding);
         if (c.width != NRC_WIDTH && c.width != NRC_WIDE_WIDTH)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "width must be 64 or 128");
-        if (c.infer_precision != NRC_PRECISION_F16 && c.infer_precision != NRC_PRECISION_FP8)
+        if (c.infer_precision != NRC_PRECISION_F16 && c.infer_precision != NRC_PRECISION_FP8 &&
+            c.infer_precision != NRC_PRECISION_F16_ACC16)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown infer_precision");
+        if (c.infer_precision == NRC_PRECISION_F16_ACC16 && (c.width != NRC_WIDTH || encoding != NRC_ENCODING_FREQUENCY))
+            throw ApiError(NRC_ERR_UNSUPPORTED, "F16_ACC16 (tcnn numerics) is implemented for the width-64 Frequency network");
         if (c.infer_precision == NRC_PRECISION_FP8 && c.width != NRC_WIDE_WIDTH)
             throw ApiError(NRC_ERR_UNSUPPORTED, "FP8 inference is implemented for the width-128 network only");
         if (c.width == NRC_WIDE_WIDTH && encoding == NRC_ENCODING_HASH)
@@ -958,6 +963,8 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
         if (num_pixels > 0 && (!thr || !rgba || (reinterpret_cast<uintptr_t>(rgba) & 15)))
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "throughput / 16-byte aligned float4 frame buffer required");
         const float w = 1.0f / (float)(iteration_index + 1u);  // nrc_helpers.cu:98
+        if (!net->wide() && net->cfg.infer_precision == NRC_PRECISION_F16_ACC16)
+            throw ApiError(NRC_ERR_UNSUPPORTED, "fused accumulation runs the F16 numerics (use infer + accumulate)");
         if (net->wide())
             HIP_CHECK(infer_wide(net, (int)net->cfg.infer_precision, in, out, n, reinterpret_cast<const float*>(thr),
                                  rgba, num_pixels, mode, w, net->stream));
@@ -1417,6 +1424,14 @@ nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* i
                                      hipStream_t stream) {
     return guarded([&] {
         check_live(net);
+        if (!net->wide() && precision == NRC_PRECISION_F16_ACC16) {  // tcnn numerics on a width-64 Frequency network
+            if (net->encoding != NRC_ENCODING_FREQUENCY)
+                throw ApiError(NRC_ERR_UNSUPPORTED, "F16_ACC16 is implemented for the Frequency encoding");
+            if (n == 0) return;
+            if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
+            HIP_CHECK(launch_infer_tcnn(in, out, n, net->wf_infer, net->infer, stream));
+            return;
+        }
         if (!net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "precision selection is for the width-128 network");
         // bits 4+: kernel variant (0 = production; 1 = 1024-thread blocks, Frequency only)
         const int prec = precision & 15, variant = precision >> 4;

@@ -217,7 +217,7 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
 constexpr int kProductInferVariant = 47;
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s, uint32_t* pools = nullptr, int* parity = nullptr);
-constexpr int kNumInferVariants = 56;  // 50: launch_infer16 (the t16 image)
+constexpr int kNumInferVariants = 60;  // 50: launch_infer16 (the t16 image)
 // Frequency inference on v_mfma_f32_16x16x32_f16 (nrc_infer16.hip) from the t16-layout inference image
 hipError_t launch_infer16(const float* queries, float* out, int64_t n, const _Float16* wf16, hipStream_t s);
 // per-wave (cycles, 100 MHz ticks) of the last clocked variant launch (31, 32)
@@ -237,6 +237,10 @@ hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float*
 hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
                            float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
 hipError_t launch_encode_sh(const float* queries, float* enc, int64_t n, hipStream_t s);
+// tcnn-numerics inference (NRC_PRECISION_F16_ACC16, Frequency, width 64): f16 accumulation per 16-wide K chunk;
+// w0 = the f32 inference weights (canonical blob; layer 0 is rebuilt from it in canonical K order)
+hipError_t launch_infer_tcnn(const float* queries, float* out, int64_t n, const _Float16* wf, const float* w0,
+                             hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, int variant = 0);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.

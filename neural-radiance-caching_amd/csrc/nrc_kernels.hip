@@ -751,7 +751,17 @@ __device__ __forceinline__ void layer_mfma(const h8 (&a)[2][KK], const h8 (&in)[
     f16v c[TILES][2];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) c[t][0] = c[t][1] = zero16();
-    if constexpr ((ABL & 131072) != 0) {
+    if constexpr ((ABL & 262144) != 0) {
+        // tile-major order (round 4, 2-tile A/B): tile 0's MFMAs of the layer, then tile 1's, so that tile 0's ReLU/pack
+        // VALU can issue beside tile 1's MFMAs and tile 1's beside tile 0's next layer
+#pragma unroll
+        for (int t = 0; t < TILES; ++t)
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) {
+                c[t][0] = mfma(a[0][kk], in[t][kk], c[t][0]);
+                c[t][1] = mfma(a[1][kk], in[t][kk], c[t][1]);
+            }
+    } else if constexpr ((ABL & 131072) != 0) {
         // A-major order (round 4, energy A/B): consecutive MFMAs share the A operand (weight fragment) across tiles
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk)
@@ -818,14 +828,14 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
         {
             h8 a0[2][KK0];
             load_frags<KK0, ABL & 7>(lw_lane, 0, a0);
-            layer_mfma<TILES, KK0, ABL & (7 | 131072)>(a0, x, y);
+            layer_mfma<TILES, KK0, ABL & (7 | 131072 | 262144)>(a0, x, y);
         }
         mark(1);
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
             h8 a[2][4];
             load_frags<4, ABL & 7>(lw_lane, l, a);
-            layer_mfma<TILES, 4, ABL & (7 | 131072)>(a, y, z);
+            layer_mfma<TILES, 4, ABL & (7 | 131072 | 262144)>(a, y, z);
 #pragma unroll
             for (int t = 0; t < TILES; ++t)
 #pragma unroll
@@ -1261,7 +1271,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             ph[0] += tn - tprev;
             tprev = tn;
         }
-        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256 | 65536 | 131072), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
+        mlp_tiles<TILES, PREFETCH, ABL & (7 | 256 | 65536 | 131072 | 262144), KK0>((lds_h8*)(lw + lane), x, o, ph, &tprev);
         if constexpr ((ABL & 8) && EPI < 0) {
             const int64_t s0 = g * TILES * 32;
             if (out16 && s0 + TILES * 32 <= n) {
@@ -3007,6 +3017,12 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 53: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, false, 48 | 1024 | 2048 | 65536 | 131072>, 512, bpc[53], (ntiles + 1) / 2, queries, out, n, wf, s);
         case 54: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536>, 768, bpc[54], (ntiles + 1) / 2, queries, out, n, wf, s);
         case 55: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536 | 131072>, 768, bpc[55], (ntiles + 1) / 2, queries, out, n, wf, s);
+        // 56 / 58: 52 / 54 with tile-major MFMA order; 57 / 59: 2 / 3 waves per SIMD with the layer-ahead fragment
+        // prefetch (PREFETCH; 32x32x16 output layer)
+        case 56: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, false, 48 | 1024 | 2048 | 65536 | 262144>, 512, bpc[56], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 57: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, true, 48 | 1024 | 2048>, 512, bpc[57], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 58: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536 | 262144>, 768, bpc[58], (ntiles + 1) / 2, queries, out, n, wf, s);
+        case 59: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, true, 48 | 1024 | 2048>, 768, bpc[59], (ntiles + 1) / 2, queries, out, n, wf, s);
 #endif
         // 47 (default, round 3): 39 with the output layer on 4x4x4 16-block MFMAs (65536); in-process A/B at 2^21
         // queries 82.3-82.6 vs 82.7-83.4 us (profiles/r03_infer/ab_out4x4_v47.json)
@@ -3098,6 +3114,154 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
         case 2: return launch_persistent_infer(infer_sh_kernel<2, 1024, 2048>, 1024, bpq[2], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// tcnn-numerics inference (round 4, opt-in: nrc_config.infer_precision = NRC_PRECISION_F16_ACC16).
+// tiny-cuda-nn's FullyFusedMLP forward keeps its accumulators in f16 (NRCNetworkConfigs.h:26-33; SURVEY App. A.5 [M]):
+// every 16-wide K chunk of every layer is added to an f16 accumulator, in K order, and rounded to f16 -- the oracle's
+// ORC_TCNN mode (oracle/nrc_oracle.c matvec). The production kernel accumulates a whole layer in f32 instead, which sits
+// 1.7-2.1e-3 from ORC_TCNN on random weights. Here:
+//   * chunk kk of a layer must hold the features 16 kk .. 16 kk + 15 in tcnn's order. Hidden layers already do (the
+//     accumulator-as-operand chain: chunk kk = rows 16 kk.. of the previous layer, acc_row); layer 0 does not (the
+//     encoder's lane slots mix features, slot_feature), so each wave writes its tile's encoded features to an LDS row per
+//     query in canonical order ([32][80] f16, the 14 pad features 1.0 written once) and reads chunk kk back as the
+//     B operand (lane half h: features 16 kk + 8 h ..), and the layer-0 A fragments are rebuilt in that order from the
+//     f32 inference weights at block start;
+//   * per chunk: acc = f16(MFMA(W_kk, x_kk, acc)) (the MFMA adds the chunk's 16 exact products to the f16-valued
+//     accumulator in f32, then one rounding to f16: the oracle's f16(acc + part) up to f32 double rounding);
+//   * output layer: the 32x32x16 form (rows 0..2 of lane half 0), the same chunking.
+// Same encoder (encode_v3) and output format as the production kernel; about 4x its VALU (the per-chunk roundings).
+constexpr int kTcnnRowHalves = 80;  // one query's 80 encoded features (160 B)
+__device__ __forceinline__ void round_f16_inplace(f16v& c, int count) {
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+        if (i >= count) break;
+        const h2 v = __builtin_bit_cast(h2, pk2(c[i], c[i + 1]));
+        c[i] = (float)v[0];
+        c[i + 1] = (float)v[1];
+    }
+}
+
+__global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restrict__ q, float* __restrict__ out,
+                                                            int64_t n, const h8* __restrict__ wf,
+                                                            const float* __restrict__ w0) {
+    constexpr int W = 8;  // waves per block
+    __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
+    __shared__ __attribute__((aligned(16))) _Float16 enc[W][32 * kTcnnRowHalves];
+    copy_to_lds<512, kFwdFrags * 64>(lw, wf);
+    __syncthreads();
+    // layer-0 fragments in canonical K order: fragment (mb, kk), lane L, element j = W0[32 mb + L % 32][16 kk + 8 (L / 32) + j]
+    for (int i = threadIdx.x; i < 10 * 64; i += 512) {
+        const int frag = i >> 6, L = i & 63, mb = frag / 5, kk = frag % 5;
+        const float* src = w0 + (32 * mb + (L & 31)) * NRC_ENC_WIDTH + 16 * kk + 8 * (L >> 5);
+        h8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)src[j];
+        lw[fwd_frag(0, mb, kk) * 64 + L] = v;
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    _Float16* const row = &enc[wave][r * kTcnnRowHalves];
+    // pad features 66..79 = 1.0 (never rewritten)
+    if (h == 0)
+#pragma unroll
+        for (int f = 66; f < 80; ++f) row[f] = (_Float16)1.0f;
+    __syncthreads();
+    char* const rowb = reinterpret_cast<char*>(row);
+    const int64_t ntiles = (n + 31) / 32;
+    for (int64_t g = (int64_t)blockIdx.x * W + wave; g < ntiles; g += (int64_t)gridDim.x * W) {
+        const int64_t s = g * 32 + r;
+        const QLane Q = load_q(q, s < n ? s : n - 1, h);
+        h8 x[5];
+        encode_v3(Q, h, x);
+        // slots -> canonical features (slot_feature): TriangleWave slots 6d.. -> 12 d + 6 h.., OneBlob slots 18.. ->
+        // 36 + 12 h.., Identity slots 30..32 -> 60 + 3 h..
+        uint32_t w[20];
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) {
+            const u4 t = __builtin_bit_cast(u4, x[kk]);
+            w[4 * kk] = t.x;
+            w[4 * kk + 1] = t.y;
+            w[4 * kk + 2] = t.z;
+            w[4 * kk + 3] = t.w;
+        }
+        asm volatile("" ::: "memory");  // the previous tile's chunk reads of this row stay above these writes
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) *(uint32_t*)(rowb + 2 * (12 * d + 6 * h) + 4 * i) = w[3 * d + i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) *(uint32_t*)(rowb + 2 * (36 + 12 * h) + 4 * i) = w[9 + i];
+        const h2 id01 = __builtin_bit_cast(h2, w[15]), id2 = __builtin_bit_cast(h2, w[16]);
+        row[60 + 3 * h] = id01[0];
+        row[61 + 3 * h] = id01[1];
+        row[62 + 3 * h] = id2[0];
+        // the wave's writes of every row land before its lanes read other lanes' rows (LDS is in order per wave)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        h8 in0[5];
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) in0[kk] = *(const h8*)(rowb + 32 * kk + 16 * h);
+        asm volatile("" ::: "memory");
+        lds_h8* const wl = (lds_h8*)(lw + lane);
+        // layer 0 (K = 80, 5 chunks) and the hidden layers (K = 64, 4 chunks)
+        h8 y[4];
+        {
+            f16v c[2];
+#pragma unroll
+            for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    c[m] = mfma(wl[fwd_frag(0, m, kk) * 64], in0[kk], kk ? c[m] : zero16());
+                    round_f16_inplace(c[m], 16);
+                }
+            y[0] = relu_h8(c[0], 0);
+            y[1] = relu_h8(c[0], 8);
+            y[2] = relu_h8(c[1], 0);
+            y[3] = relu_h8(c[1], 8);
+        }
+#pragma unroll
+        for (int l = 1; l < 5; ++l) {
+            lds_h8* const wll = launder(wl);
+            f16v c[2];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    c[m] = mfma(wll[fwd_frag(l, m, kk) * 64], y[kk], kk ? c[m] : zero16());
+                    round_f16_inplace(c[m], 16);
+                }
+            y[0] = relu_h8(c[0], 0);
+            y[1] = relu_h8(c[0], 8);
+            y[2] = relu_h8(c[1], 0);
+            y[3] = relu_h8(c[1], 8);
+        }
+        // output layer (rows 0..2 of lane half 0 = registers 0..2)
+        f16v o = zero16();
+        {
+            lds_h8* const wll = launder(wl);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                o = mfma(wll[fwd_frag(5, 0, kk) * 64], y[kk], o);
+                round_f16_inplace(o, 4);
+            }
+        }
+        if (h == 0 && s < n) {
+            float* dst = out + s * NRC_OUTPUT_DIMS;
+            dst[0] = fmaxf(o[0], 0.0f);  // f16-valued already: the output ReLU (NRCNetworkConfigs.h:29)
+            dst[1] = fmaxf(o[1], 0.0f);
+            dst[2] = fmaxf(o[2], 0.0f);
+        }
+    }
+}
+
+hipError_t launch_infer_tcnn(const float* queries, float* out, int64_t n, const _Float16* wf, const float* w0,
+                             hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (!wf || !w0) return hipErrorInvalidValue;
+    static int bpc = 0;
+    return launch_persistent_infer(infer_tcnn_kernel, 512, bpc, (n + 31) / 32, queries, out, n, wf, s, w0);
 }
 
 hipError_t launch_wide_pack(const float* w_infer, const float* w_train, const WideImages& im, hipStream_t s) {

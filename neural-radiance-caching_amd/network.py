@@ -332,7 +332,8 @@ def encode(inputs, encoded, n: int, stream=None) -> None:
 def default_config(encoding: InputEncoding = InputEncoding.Frequency, width: int = 64,
                    infer_precision: int = 0) -> NrcConfig:
     """The reference's hyper-parameters for an encoding; width 128 selects the BASELINE configs[4] network (f16
-    training and inference), infer_precision PRECISION_FP8 its FP8 inference path (training stays f16)."""
+    training and inference), infer_precision PRECISION_FP8 its FP8 inference path (training stays f16);
+    PRECISION_F16_ACC16 selects tiny-cuda-nn's f16-accumulate numerics for infer() (width 64, Frequency)."""
     c = lib().nrc_default_config(int(encoding))
     c.width = int(width)
     c.infer_precision = int(infer_precision)
