@@ -183,6 +183,21 @@ nrc_status nrc_get_comm_rank(const nrc_net* net, int* rank, int* world);
 nrc_status nrc_train_dp(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b_local,
                         uint32_t global_b, float* loss_h);
 
+/* One-shot peer exchange (round 4; width-64 Frequency / FrequencySH): instead of an RCCL all-reduce, each rank stores
+ * its gradient straight into a receive buffer of every peer over xGMI (IPC-mapped uncached device memory) and releases
+ * a flag; the Adam step waits for all flags and sums the world gradients in rank order (bitwise-identical replicas;
+ * at world 2 bitwise the RCCL sum). Set up once, collectively:
+ *   nrc_peer_exchange_handle(net, world, h)   allocate this rank's buffer, return its IPC handle (64 B);
+ *   exchange the handles by any means (torch.distributed, MPI, RCCL all-gather);
+ *   nrc_peer_exchange_open(net, rank, world, all_handles)   (world x 64 B in rank order) map the peers' buffers.
+ * While open, nrc_train_dp (and nrc_process_frame_shard) use it and need no communicator. Every rank must call
+ * nrc_train_dp the same number of times; a peer missing for ~10 s ends the wait with NRC_ERR_INTERNAL. Close on
+ * every rank after a barrier. */
+#define NRC_PEER_HANDLE_BYTES 64
+nrc_status nrc_peer_exchange_handle(nrc_net* net, int world, void* handle_out);
+nrc_status nrc_peer_exchange_open(nrc_net* net, int rank, int world, const void* handles);
+nrc_status nrc_peer_exchange_close(nrc_net* net);
+
 /* ---- state access (host buffers of nrc_get_num_params() f32; synchronous) ----
  * Frequency: NRC_NUM_PARAMS (layout.h canonical blob). Hash: NRC_HASH_NUM_PARAMS = MLP blob then the grid table
  * [entry][2] (the grid's per-entry Adam step counters are internal). */

@@ -322,10 +322,34 @@ struct nrc_net {
     static constexpr int kProtoErrSlot = 4;
     uint32_t* proto_err_dev() const { return reinterpret_cast<uint32_t*>(loss_dev + kProtoErrSlot); }
     void check_protocol() const {
-        if (loss_host && reinterpret_cast<volatile uint32_t*>(loss_host)[kProtoErrSlot] != 0u)
+        const uint32_t e = loss_host ? reinterpret_cast<volatile uint32_t*>(loss_host)[kProtoErrSlot] : 0u;
+        if (e == 2u)
+            throw ApiError(NRC_ERR_INTERNAL,
+                           "nrc_train_dp: a peer's gradient did not arrive (peer exchange wait timed out; the step's "
+                           "update and every state derived from it are invalid; re-initialise the network)");
+        if (e != 0u)
             throw ApiError(NRC_ERR_INTERNAL,
                            "training kernel: an LDS protocol wait timed out (the gradient of that step and every state "
                            "derived from it are invalid; re-initialise the network)");
+    }
+    // one-shot peer gradient exchange (nrc_peer_exchange_*; round 4): own receive buffer, the IPC-mapped buffers of
+    // the peers (px_peers.p[px_rank] = px_buf), the step sequence number
+    float* px_buf = nullptr;
+    PeerPtrs px_peers{};
+    int px_world = 0, px_rank = -1;
+    uint32_t px_seq = 0;
+    bool px_open = false;
+    void peer_close() {
+        if (px_open)
+            for (int r = 0; r < px_world; ++r)
+                if (r != px_rank && px_peers.p[r]) (void)hipIpcCloseMemHandle(px_peers.p[r]);
+        px_peers = PeerPtrs{};
+        if (px_buf) (void)hipFree(px_buf);
+        px_buf = nullptr;
+        px_world = 0;
+        px_rank = -1;
+        px_seq = 0;
+        px_open = false;
     }
     void alloc_loss_slots() {
         HIP_CHECK(hipMalloc(&work_queue, kInferPoolBytes));
@@ -393,6 +417,7 @@ struct nrc_net {
     size_t grad_floats() const { return n_total() + 4; }
 
     void release() {
+        peer_close();
         auto f = [](void* p) {
             if (p) (void)hipFree(p);
         };
@@ -676,6 +701,11 @@ void nrc_amd::net_train_dp_async(nrc_net* net, const float* in, const float* tgt
 
 bool nrc_amd::net_comm(nrc_net* net, int* rank, int* world) {
     check_live(net);
+    if (net->px_open) {  // the peer exchange takes precedence (nrc_train_dp uses it when open)
+        *rank = net->px_rank;
+        *world = net->px_world;
+        return true;
+    }
     *rank = net->comm_rank;
     *world = net->comm_world;
     return net->comm != nullptr;
@@ -1115,8 +1145,30 @@ void nccl_check(ncclResult_t r, const char* what) {
 void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b, float* loss_h,
                  float* loss_d) {
     check_live(net);
-    if (!net->comm) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm)");
+    if (!net->comm && !net->px_open)
+        throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm / nrc_peer_exchange_open)");
     if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
+    if (net->px_open) {
+        // one-shot peer exchange: local gradient -> every peer's receive slot (push) -> wait + rank-order sum + Adam/EMA
+        do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad);
+        net->px_seq = net->px_seq + 1u ? net->px_seq + 1u : 1u;
+        const int nfl = (int)net->grad_floats();
+        HIP_CHECK(launch_peer_push(net->dp_grad, nfl, net->px_peers, net->px_rank, net->px_world, net->px_seq,
+                                   net->stream));
+        net->step += 1;
+        HIP_CHECK(launch_peer_apply(net->px_buf, net->px_world, nfl, net->px_seq, net->proto_err_dev(),
+                                    loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
+        if (loss_h) {
+            if (loss_d) {
+                HIP_CHECK(hipStreamSynchronize(net->stream));
+                net->check_protocol();
+                HIP_CHECK(hipMemcpy(loss_h, loss_d, sizeof(float), hipMemcpyDeviceToHost));
+            } else {
+                *loss_h = net->read_loss();
+            }
+        }
+        return;
+    }
     if (net->hash()) {
         // exact grid exchange: each rank's fixed-point sums, exchange-encoded in place in the handle's accumulator,
         // summed as int64 beside the f32 MLP gradient and loss (one RCCL group on the handle's stream), then rounded
@@ -1268,6 +1320,65 @@ nrc_status nrc_get_comm_rank(const nrc_net* net, int* rank, int* world) {
 nrc_status nrc_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
                         float* loss_h) {
     return guarded([&] { do_train_dp(net, in, tgt, b_local, global_b, loss_h, nullptr); });
+}
+
+nrc_status nrc_peer_exchange_handle(nrc_net* net, int world, void* handle_out) {
+    return guarded([&] {
+        check_live(net);
+        if (!handle_out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle output");
+        if (net->hash() || net->wide())
+            throw ApiError(NRC_ERR_UNSUPPORTED, "the peer exchange is implemented for the width-64 Frequency / FrequencySH "
+                                                "networks (Hash and width 128 use the RCCL path)");
+        if (world < 2 || world > kPeerMaxRanks) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "world must be 2..16");
+        static_assert(sizeof(hipIpcMemHandle_t) == NRC_PEER_HANDLE_BYTES, "IPC handle size");
+        net->peer_close();
+        const size_t bytes = peer_buffer_bytes(world, (int)net->grad_floats());
+        // uncached device memory: the peers' xGMI stores and this GPU's loads meet in memory, not in a stale L2 line
+        HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&net->px_buf), bytes, hipDeviceMallocUncached));
+        HIP_CHECK(hipMemset(net->px_buf, 0, bytes));  // flags 0: before any peer can know the handle
+        HIP_CHECK(hipDeviceSynchronize());
+        net->px_world = world;
+        HIP_CHECK(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), net->px_buf));
+    });
+}
+
+nrc_status nrc_peer_exchange_open(nrc_net* net, int rank, int world, const void* handles) {
+    return guarded([&] {
+        check_live(net);
+        if (!handles) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handles");
+        if (!net->px_buf || net->px_open || world != net->px_world)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "call nrc_peer_exchange_handle with the same world first (once)");
+        if (rank < 0 || rank >= world) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "bad rank");
+        PeerPtrs p{};
+        const auto* h = static_cast<const hipIpcMemHandle_t*>(handles);
+        for (int r = 0; r < world; ++r) {
+            if (r == rank) {
+                p.p[r] = net->px_buf;
+                continue;
+            }
+            void* ptr = nullptr;
+            const hipError_t e = hipIpcOpenMemHandle(&ptr, h[r], hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {
+                for (int q = 0; q < r; ++q)
+                    if (q != rank && p.p[q]) (void)hipIpcCloseMemHandle(p.p[q]);
+                throw ApiError(NRC_ERR_HIP, std::string("hipIpcOpenMemHandle(rank ") + std::to_string(r) +
+                                                "): " + hipGetErrorString(e));
+            }
+            p.p[r] = static_cast<float*>(ptr);
+        }
+        net->px_peers = p;
+        net->px_rank = rank;
+        net->px_seq = 0;
+        net->px_open = true;
+    });
+}
+
+nrc_status nrc_peer_exchange_close(nrc_net* net) {
+    return guarded([&] {
+        check_live(net);
+        HIP_CHECK(hipStreamSynchronize(net->stream));
+        net->peer_close();
+    });
 }
 
 nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst) {

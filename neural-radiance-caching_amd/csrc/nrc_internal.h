@@ -255,6 +255,15 @@ hipError_t launch_train_stamped(const float* queries, const float* targets, int6
 
 // kApplyFixed (grid_adam_kernel only): the gradient is an all-reduced exchange-encoded fixed-point array (GridBuffers::fixed)
 enum ReduceMode { kReduceFused = 0, kReduceOnly = 1, kApplyOnly = 2, kPackOnly = 3, kApplyFixed = 4 };
+
+// One-shot peer gradient exchange of nrc_train_dp (nrc_kernels.hip, round 4): receive buffers of peer_buffer_bytes, one
+// per rank, IPC-mapped into every other rank; dst.p[r] = rank r's buffer as seen from this process.
+constexpr int kPeerMaxRanks = 16;
+struct PeerPtrs {
+    float* p[kPeerMaxRanks];
+};
+int peer_stride(int nfl);
+size_t peer_buffer_bytes(int world, int nfl);
 struct OptimArgs {
     float lr, beta1, beta2, eps, l2_reg, ema_decay, loss_scale;
     uint32_t step;
@@ -376,6 +385,10 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);
+hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int rank, int world, uint32_t seq,
+                            hipStream_t s);
+hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
+                             const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s);
 
 // ---- per-handle scratch used by the frame driver (nrc_capi.cpp): NRC_NUM_BATCHES loss slots on the device and a
 // pinned host mirror

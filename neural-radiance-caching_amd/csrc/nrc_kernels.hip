@@ -3738,5 +3738,91 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// One-shot peer gradient exchange of nrc_train_dp (round 4). Each rank owns a receive buffer
+// (uncached device memory, exported by IPC handle): data [2 parities][world][stride] f32, then one flag per (parity,
+// source rank), 64 B apart. A step with sequence number seq (parity seq & 1):
+//   peer_push_kernel   block r copies this rank's gradient (NRC_GRAD_FLOATS incl. the loss slot) into slot [par][rank]
+//                      of rank r's buffer (xGMI peer stores; r == rank: its own buffer), fences at system scope and
+//                      releases flag [par][rank] = seq there;
+//   peer_apply_kernel  waits (acquire, system scope) until every flag [par][*] of its own buffer reads seq, sums the
+//                      world gradients in rank order (the same float operations on every rank: bitwise-identical
+//                      replicas) and runs adam_pack_one (kApplyOnly) per parameter; block 0 sums the loss likewise.
+// Two parities suffice: a rank writes parity p of a peer only after that peer's flag for the previous step of the
+// other parity was seen by its own apply, which the peer issued after its apply of the step before (stream order).
+// The wait is bounded (about 10 s, then error word 2 and NRC_ERR_INTERNAL): a missing peer ends the kernel.
+// ------------------------------------------------------------------------------------------------
+constexpr int kPeerFlagStride = 16;  // u32 per flag (64 B)
+int peer_stride(int nfl) { return (nfl + 63) / 64 * 64; }
+size_t peer_buffer_bytes(int world, int nfl) {
+    return sizeof(float) * ((size_t)2 * world * peer_stride(nfl)) + sizeof(uint32_t) * 2 * world * kPeerFlagStride;
+}
+
+__global__ __launch_bounds__(1024) void peer_push_kernel(const float* __restrict__ grad, int nfl, PeerPtrs dst, int rank,
+                                                         int world, int stride, uint32_t seq) {
+    const int r = blockIdx.x, par = (int)(seq & 1u);
+    float* const d = dst.p[r] + ((int64_t)par * world + rank) * stride;
+    const float4* s4 = reinterpret_cast<const float4*>(grad);
+    float4* d4 = reinterpret_cast<float4*>(d);
+    for (int i = threadIdx.x; i < nfl / 4; i += 1024) d4[i] = s4[i];
+    __threadfence_system();  // this thread's peer stores are complete before the flag below
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t* const flags = reinterpret_cast<uint32_t*>(dst.p[r] + (int64_t)2 * world * stride);
+        __hip_atomic_store(flags + (par * world + rank) * kPeerFlagStride, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict__ xbuf, int world, int stride, uint32_t seq,
+                                                         uint32_t* err, float* __restrict__ loss_out, ModelBuffers mb,
+                                                         OptimArgs oa, float lr_t, float ema_debias) {
+    const int par = (int)(seq & 1u);
+    if (threadIdx.x < (unsigned)world) {
+        const uint32_t* f = reinterpret_cast<const uint32_t*>(xbuf + (int64_t)2 * world * stride) +
+                            (par * world + (int)threadIdx.x) * kPeerFlagStride;
+        int i = 0;
+        // fast polls first (~0.1 ms), then ~4 us apart: about 10 s in all
+        for (; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq && i < (1 << 21); ++i) {
+            if (i < 4096) __builtin_amdgcn_s_sleep(1);
+            else __builtin_amdgcn_s_sleep(127);
+        }
+        if (i == (1 << 21)) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    const float* const base = xbuf + (int64_t)par * world * stride;
+    auto ld = [&](int r, int p) {  // peer-written uncached memory, read at system scope
+        return __hip_atomic_load(base + (int64_t)r * stride + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    if (blockIdx.x == 0 && threadIdx.x == 0 && loss_out) {
+        float L = ld(0, mb.n_total);
+        for (int r = 1; r < world; ++r) L += ld(r, mb.n_total);
+        loss_out[0] = L;
+    }
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= mb.n_mlp) return;
+    float g = ld(0, p);
+    for (int r = 1; r < world; ++r) g += ld(r, p);
+    adam_pack_one(kApplyOnly, p, g, mb, oa, lr_t, ema_debias);
+}
+
+hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int rank, int world, uint32_t seq,
+                            hipStream_t s) {
+    if (world < 2 || world > kPeerMaxRanks || rank < 0 || rank >= world || (nfl & 3)) return hipErrorInvalidValue;
+    for (int r = 0; r < world; ++r)
+        if (!dst.p[r]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(peer_push_kernel, dim3(world), dim3(1024), 0, s, grad, nfl, dst, rank, world, peer_stride(nfl), seq);
+    return hipGetLastError();
+}
+
+hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
+                             const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+    if (world < 2 || world > 256 || !xbuf || !err) return hipErrorInvalidValue;
+    float lr_t, ema_debias;
+    adam_host_factors(oa, lr_t, ema_debias);
+    hipLaunchKernelGGL(peer_apply_kernel, dim3((mb.n_mlp + 255) / 256), dim3(256), 0, s, xbuf, world, peer_stride(nfl), seq,
+                       err, loss_out, mb, oa, lr_t, ema_debias);
+    return hipGetLastError();
+}
+
 }  // namespace nrc_amd
 

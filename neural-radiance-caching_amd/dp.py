@@ -31,6 +31,23 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return start, count
 
 
+def open_peer_exchange(net, group=None) -> None:
+    """Set up the library's one-shot peer gradient exchange (nrc_peer_exchange_*) on every rank of the group: each rank
+    allocates its receive buffer, the 64-byte IPC handles are all-gathered over torch.distributed (any backend), and
+    every rank maps its peers' buffers. Afterwards ``net.train_dp`` exchanges gradients GPU to GPU without RCCL."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    mine = torch.frombuffer(bytearray(net.peer_exchange_handle(world)), dtype=torch.uint8)
+    if dist.get_backend(group) == "nccl":
+        mine = mine.cuda()
+    parts = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    net.peer_exchange_open(rank, world, b"".join(bytes(p.cpu().numpy().tobytes()) for p in parts))
+    dist.barrier(group=group)
+
+
 class DataParallelTrainer:
     def __init__(self, backend, grad_buffer, group=None, grid_fixed=None, mlp_params: int | None = None):
         import torch.distributed as dist

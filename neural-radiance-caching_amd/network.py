@@ -253,6 +253,25 @@ class Network:
         check(self._lib.nrc_train_dp(self._h, pi, pt, b, int(global_b), ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
+    # ---- one-shot peer exchange (nrc_c.h nrc_peer_exchange_*; round 4) --------------------------------------
+    PEER_HANDLE_BYTES = 64
+
+    def peer_exchange_handle(self, world: int) -> bytes:
+        """Allocate this rank's receive buffer for a world of ranks; returns its IPC handle (64 bytes)."""
+        buf = ctypes.create_string_buffer(self.PEER_HANDLE_BYTES)
+        check(self._lib.nrc_peer_exchange_handle(self._h, int(world), buf))
+        return buf.raw
+
+    def peer_exchange_open(self, rank: int, world: int, handles: bytes) -> None:
+        """Map every peer's receive buffer (handles: world x 64 bytes in rank order); train_dp then uses the exchange."""
+        if len(handles) != int(world) * self.PEER_HANDLE_BYTES:
+            raise ValueError("handles: world x 64 bytes in rank order")
+        buf = ctypes.create_string_buffer(bytes(handles), len(handles))
+        check(self._lib.nrc_peer_exchange_open(self._h, int(rank), int(world), buf))
+
+    def peer_exchange_close(self) -> None:
+        check(self._lib.nrc_peer_exchange_close(self._h))
+
     @property
     def num_params(self) -> int:
         """Parameter count of the configured model (Frequency 22,528; Hash 21,504 MLP + 991,232 grid)."""

@@ -200,3 +200,58 @@ def test_two_ranks_on_one_gpu_gloo_hash_exact(tmp_path, nrc, torch, dev):
     assert np.linalg.norm(p[:M] - r[:M]) <= 3e-3 * np.linalg.norm(r[:M])
     np.testing.assert_allclose(np.load(tmp_path / "loss_0.npy"), [ref_loss], rtol=1e-5)
     ref.destroy()
+
+
+@pytest.mark.parametrize("B", [16384, 4096])
+def test_two_ranks_on_one_gpu_peer_exchange(tmp_path, nrc, torch, dev, golden, B):
+    """The one-shot peer exchange (nrc_peer_exchange_*): two processes on cuda:0, IPC handles
+    all-gathered over gloo, nrc_train_dp pushing each rank's gradient into the other's receive buffer and summing in
+    rank order. Replicas bit-identical, and bitwise the single-process step that sums the two shards' gradients
+    (g0 + g1, one f32 addition -- also what a 2-rank RCCL all-reduce computes) and applies them with nrc_train_apply."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    np.save(tmp_path / "params.npy", golden["params_b"])
+    steps = 3
+    procs = [subprocess.Popen([sys.executable, str(ROOT / "tools" / "dp_rank_worker.py"), str(tmp_path), str(B),
+                               "Frequency", str(steps), "peer"], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    logs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), logs
+    ref = nrc.Network()
+    ref.init(stream=torch.cuda.current_stream())
+    ref.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+    g = [torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev) for _ in range(2)]
+    ref_losses = []
+    for it in range(steps):
+        q_np, t_np = nrc.synthetic.cornell_batch(B, seed=80 + it)
+        for r in range(2):
+            s, c = nrc.dp.shard_range(B, r, 2)
+            ref.train_grad(to_dev(torch, dev, q_np[s:s + c]), to_dev(torch, dev, t_np[s:s + c]), c, B, g[r])
+        ref_losses.append(ref.train_apply(g[0] + g[1], loss=True))
+    for slot in ("params", "infer"):
+        a, b = np.load(tmp_path / f"{slot}_0.npy"), np.load(tmp_path / f"{slot}_1.npy")
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, ref.get_state(getattr(nrc.StateSlot, slot.upper())))
+    np.testing.assert_array_equal(np.load(tmp_path / "loss_0.npy"), np.array(ref_losses, np.float32))
+    ref.destroy()
+
+
+def test_peer_exchange_argument_checks(nrc, torch, dev):
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    with pytest.raises(nrc.NrcError):
+        net.peer_exchange_handle(1)  # world >= 2
+    with pytest.raises(nrc.NrcError):
+        net.peer_exchange_open(0, 2, bytes(128))  # no buffer allocated yet
+    h = net.peer_exchange_handle(2)
+    assert len(h) == 64
+    with pytest.raises(nrc.NrcError):
+        net.peer_exchange_open(0, 3, bytes(192))  # world differs from the allocation
+    net.peer_exchange_close()
+    net.destroy()
+    hnet = nrc.Network()
+    hnet.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+    with pytest.raises(nrc.NrcError) as e:
+        hnet.peer_exchange_handle(2)
+    assert e.value.status == 5
+    hnet.destroy()

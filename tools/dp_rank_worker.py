@@ -2,10 +2,12 @@
 nrc_train_grad / nrc_train_apply through nrc_amd.dp.DataParallelTrainer, every rank on cuda:0.
 
     RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tools/dp_rank_worker.py <out_dir> [global_batch]
-        [encoding] [steps]
+        [encoding] [steps] [exchange]
 
 global_batch (default 16,384) is split over the ranks; 4,096 gives configs[3]'s per-rank slice of 2,048 samples.
 encoding Hash: the exact grid exchange (DataParallelTrainer with an int64 grid_fixed buffer).
+exchange "peer": the library's one-shot peer exchange (nrc_peer_exchange_*, handles all-gathered over gloo) through
+nrc_train_dp instead of the Python all-reduce.
 """
 import os
 import sys
@@ -26,6 +28,7 @@ def main() -> None:
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     encoding = sys.argv[3] if len(sys.argv) > 3 else "Frequency"
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    peer = len(sys.argv) > 5 and sys.argv[5] == "peer"
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     nrc = nrc_loader.load()
@@ -42,14 +45,19 @@ def main() -> None:
     else:
         trainer = nrc.dp.DataParallelTrainer(net, grad)
     trainer.broadcast_state(net, dev)
+    if peer:
+        nrc.dp.open_peer_exchange(net)
     losses = []
     for it in range(steps):
         q, t = nrc.synthetic.cornell_batch(B, seed=80 + it)
         s, c = nrc.dp.shard_range(B, rank, world)
         qd = torch.from_numpy(np.ascontiguousarray(q[s:s + c])).to(dev)
         td = torch.from_numpy(np.ascontiguousarray(t[s:s + c])).to(dev)
-        losses.append(trainer.step(qd, td, c, B, loss=True))
+        losses.append(net.train_dp(qd, td, c, B, loss=True) if peer else trainer.step(qd, td, c, B, loss=True))
     torch.cuda.synchronize()
+    if peer:
+        dist.barrier()  # no rank unmaps or frees a buffer a peer may still write
+        net.peer_exchange_close()
     np.save(out / f"params_{rank}.npy", net.get_state(nrc.StateSlot.PARAMS))
     np.save(out / f"infer_{rank}.npy", net.get_state(nrc.StateSlot.INFER))
     np.save(out / f"loss_{rank}.npy", np.array(losses))
