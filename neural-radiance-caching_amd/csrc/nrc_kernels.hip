@@ -3753,23 +3753,38 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
 // The wait is bounded (about 10 s, then error word 2 and NRC_ERR_INTERNAL): a missing peer ends the kernel.
 // ------------------------------------------------------------------------------------------------
 constexpr int kPeerFlagStride = 16;  // u32 per flag (64 B)
+constexpr int kPeerSplit = 4;        // push blocks (and flags) per destination: each copies a quarter of the gradient
 int peer_stride(int nfl) { return (nfl + 63) / 64 * 64; }
 size_t peer_buffer_bytes(int world, int nfl) {
-    return sizeof(float) * ((size_t)2 * world * peer_stride(nfl)) + sizeof(uint32_t) * 2 * world * kPeerFlagStride;
+    return sizeof(float) * ((size_t)2 * world * peer_stride(nfl)) +
+           sizeof(uint32_t) * 2 * world * kPeerSplit * kPeerFlagStride;
 }
 
 __global__ __launch_bounds__(1024) void peer_push_kernel(const float* __restrict__ grad, int nfl, PeerPtrs dst, int rank,
                                                          int world, int stride, uint32_t seq) {
-    const int r = blockIdx.x, par = (int)(seq & 1u);
-    float* const d = dst.p[r] + ((int64_t)par * world + rank) * stride;
+    const int r = blockIdx.x / kPeerSplit, part = blockIdx.x % kPeerSplit, par = (int)(seq & 1u);
+    const int n4 = nfl / 4, b4 = part * n4 / kPeerSplit, e4 = (part + 1) * n4 / kPeerSplit;
     const float4* s4 = reinterpret_cast<const float4*>(grad);
-    float4* d4 = reinterpret_cast<float4*>(d);
-    for (int i = threadIdx.x; i < nfl / 4; i += 1024) d4[i] = s4[i];
-    __threadfence_system();  // this thread's peer stores are complete before the flag below
+    float4* d4 = reinterpret_cast<float4*>(dst.p[r] + ((int64_t)par * world + rank) * stride);
+    constexpr int kPer = 2;  // float4 per thread: a quarter of NRC_GRAD_FLOATS (1,409) over 1,024 threads
+    float4 v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) v[k] = s4[min(b4 + (int)threadIdx.x + 1024 * k, e4 - 1)];  // branch-free: both in flight
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int i = b4 + (int)threadIdx.x + 1024 * k;
+        if (i < e4) d4[i] = v[k];
+    }
+    // The destination is uncached device memory: the stores bypass the L2, and their acknowledgements (vmcnt) mean
+    // they have reached memory. Waiting for them, then the barrier, orders every thread's data before the flag -- with
+    // no system-scope release fence, whose L2 write-back (all of this XCD's dirty lines: the training slabs) cost 4-8 us
+    // per launch in the first version (profiles/r04_dp/).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t* const flags = reinterpret_cast<uint32_t*>(dst.p[r] + (int64_t)2 * world * stride);
-        __hip_atomic_store(flags + (par * world + rank) * kPeerFlagStride, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(flags + ((par * world + rank) * kPeerSplit + part) * kPeerFlagStride, seq, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -3777,12 +3792,14 @@ __global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict
                                                          uint32_t* err, float* __restrict__ loss_out, ModelBuffers mb,
                                                          OptimArgs oa, float lr_t, float ema_debias) {
     const int par = (int)(seq & 1u);
-    if (threadIdx.x < (unsigned)world) {
+    if (threadIdx.x < (unsigned)(world * kPeerSplit)) {  // one lane per (source rank, part) flag
         const uint32_t* f = reinterpret_cast<const uint32_t*>(xbuf + (int64_t)2 * world * stride) +
-                            (par * world + (int)threadIdx.x) * kPeerFlagStride;
+                            (par * world * kPeerSplit + (int)threadIdx.x) * kPeerFlagStride;
         int i = 0;
+        // relaxed system-scope polls of uncached memory (no L2 invalidate per poll); the data loads below are issued
+        // after the flag value has returned (the branch waits for it) and read memory, not a cache.
         // fast polls first (~0.1 ms), then ~4 us apart: about 10 s in all
-        for (; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq && i < (1 << 21); ++i) {
+        for (; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq && i < (1 << 21); ++i) {
             if (i < 4096) __builtin_amdgcn_s_sleep(1);
             else __builtin_amdgcn_s_sleep(127);
         }
@@ -3810,13 +3827,15 @@ hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int
     if (world < 2 || world > kPeerMaxRanks || rank < 0 || rank >= world || (nfl & 3)) return hipErrorInvalidValue;
     for (int r = 0; r < world; ++r)
         if (!dst.p[r]) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(peer_push_kernel, dim3(world), dim3(1024), 0, s, grad, nfl, dst, rank, world, peer_stride(nfl), seq);
+    if ((nfl / 4 + kPeerSplit - 1) / kPeerSplit > 2 * 1024) return hipErrorInvalidValue;  // kPer float4 per thread
+    hipLaunchKernelGGL(peer_push_kernel, dim3(world * kPeerSplit), dim3(1024), 0, s, grad, nfl, dst, rank, world,
+                       peer_stride(nfl), seq);
     return hipGetLastError();
 }
 
 hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
                              const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
-    if (world < 2 || world > 256 || !xbuf || !err) return hipErrorInvalidValue;
+    if (world < 2 || world > kPeerMaxRanks || !xbuf || !err) return hipErrorInvalidValue;
     float lr_t, ema_debias;
     adam_host_factors(oa, lr_t, ema_debias);
     hipLaunchKernelGGL(peer_apply_kernel, dim3((mb.n_mlp + 255) / 256), dim3(256), 0, s, xbuf, world, peer_stride(nfl), seq,
