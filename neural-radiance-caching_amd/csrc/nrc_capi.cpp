@@ -234,9 +234,9 @@ std::vector<int> build_t16_slab_map() {
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
 bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
-                                            "hash_infer", "hash_feat_abl", "t16_groups"};
+                                            "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p"};
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -730,6 +730,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobHashInfer: return v >= -1 && v <= 1;
         case kKnobHashFeatAbl: return v >= -1 && v <= 7;
         case kKnobT16Groups: return v == -1 || v == 1 || v == 2;
+        case kKnobHashFeatP: return v == -1 || (v >= 8 && v <= 256 && v % 8 == 0);
         default: return false;
     }
 }

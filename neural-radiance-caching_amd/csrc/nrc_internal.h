@@ -324,7 +324,8 @@ enum Knob : int {
     kKnobHashInfer = 5,   // Hash inference: -1 / 0 LDS-table feature pass + MLP kernel (round 3), 1 the gather kernel
     kKnobHashFeatAbl = 6,  // debug library: hash_feature_kernel ablation (1 no gathers, 2 no position loads, 4 no stores)
     kKnobT16Groups = 7,    // role-split t16 training kernel: 16-sample groups per chain wave (1: 64-sample blocks; -1 = 2)
-    kKnobCount = 8
+    kKnobHashFeatP = 8,    // Hash feature pass: query ranges per level (multiple of 8; -1 = 16 above 2^19 queries, else 8)
+    kKnobCount = 9
 };
 int knob(Knob k);
 

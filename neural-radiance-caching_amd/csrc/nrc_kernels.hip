@@ -3067,7 +3067,9 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
         static int bpf[3] = {};
         for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
             const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
-            const int P = cnt > ((int64_t)1 << 19) ? 16 : 8;  // query ranges per level (multiple of the 8 XCDs)
+            // query ranges per level (multiple of the 8 XCDs); knob hash_feat_p overrides (A/B)
+            const int kp = knob(kKnobHashFeatP);
+            const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 16 : 8;
             const float* qc0 = queries + c0 * NRC_INPUT_DIMS;
 #if NRC_DEBUG_KERNELS
             const int fa = knob(kKnobHashFeatAbl);
