@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--no-wide", action="store_true", help="skip the configs[4] width-128 f16/FP8 inference lines")
     ap.add_argument("--no-hash", action="store_true", help="skip the InputEncoding::Hash line")
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the configs[3] per-rank measurement")
+    ap.add_argument("--no-peer", action="store_true", help="N > 1: skip the one-shot peer-exchange training leg")
     ap.add_argument("--sustained", type=int, default=1000,
                     help="N = 1: sustained-inference launches timed after as many untimed ones (0: skip)")
     ap.add_argument("--settle-ms", type=float, default=60.0,
@@ -345,6 +346,61 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
                               "all-reduce latency over 8 ranks; unmeasured)"}}
 
 
+def dp_exchange_bench(nrc, net, dev, world: int, rank: int, frames_q, frames_t, b0: int, bn: int, frames: int,
+                      barrier, max_over_ranks) -> dict:
+    """N > 1: the same training frames through the library's one-shot peer exchange (nrc_peer_exchange_*: each rank
+    stores its gradient into every peer's receive buffer over xGMI, the Adam kernel sums them in rank order) instead of
+    the RCCL all-reduce -- per step for configs[3]'s split minibatch (b_local = 16,384 / N) and weak-scaled (16,384 per
+    rank, global batch N x 16,384). A setup or exchange failure is recorded, not raised (the inference line stands)."""
+    import torch
+    import torch.distributed as dist
+
+    B = nrc.BATCH_SIZE
+    res = {"exchange": "peer (IPC-mapped uncached receive buffers, xGMI stores, rank-order sum fused into Adam)"}
+    ok = torch.ones(1, dtype=torch.int32, device=dev)
+    try:
+        nrc.dp.open_peer_exchange(net)
+    except Exception as e:  # noqa: BLE001
+        res["error"] = f"open: {e}"
+        ok.zero_()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if not int(ok.item()):
+        res.setdefault("error", "open failed on another rank")
+        return res
+
+    def run(split: bool) -> float:
+        def frame(fi: int) -> None:
+            tq, tt = frames_q[fi % 4], frames_t[fi % 4]
+            for b in range(4):
+                s = b * B
+                if split:
+                    net.train_dp(tq[s + b0:], tt[s + b0:], bn, B)
+                else:
+                    net.train_dp(tq[s:], tt[s:], B, B * world)
+        frame(0)
+        barrier()
+        t0 = time.perf_counter()
+        for f in range(frames):
+            frame(f)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0) / frames / 4 * 1e3
+
+    try:
+        split_ms = run(True)
+        weak_ms = run(False)
+        res.update({"split_step_ms": split_ms, "split_samples_per_s": B / (split_ms * 1e-3),
+                    "weak_step_ms": weak_ms, "weak_samples_per_s": world * B / (weak_ms * 1e-3),
+                    "b_local_split": bn, "b_local_weak": B})
+    except Exception as e:  # noqa: BLE001
+        res["error"] = f"step: {e}"
+    barrier()
+    try:
+        net.peer_exchange_close()
+    except Exception as e:  # noqa: BLE001
+        res.setdefault("error", f"close: {e}")
+    return res
+
+
 def pmc_traffic() -> float | None:
     f = ROOT / "profiles" / f"pmc_infer_{ROUND}.json"
     if f.exists():
@@ -512,6 +568,13 @@ def main() -> None:
         train_step_graph_ms = graph_ms_per_call(net, stream, lambda i: net.train(frames_q[(i // 4) % 4][(i % 4) * nrc.BATCH_SIZE:],
                                                                                 frames_t[(i // 4) % 4][(i % 4) * nrc.BATCH_SIZE:]), 16, 10)
 
+    # ---- N > 1: the same training through the one-shot peer exchange (split and weak-scaled), beside RCCL's
+    dp_exchange = None
+    if distributed and not args.no_peer:
+        dp_exchange = dp_exchange_bench(nrc, net, dev, world, rank, frames_q, frames_t, b0, bn, args.train_frames,
+                                        barrier, max_over_ranks)
+        dp_exchange["rccl_split_step_ms"] = train_step_ms if comm is not None else None
+
     # ---- sustained inference: the clock the chip holds under a long run of back-to-back
     # launches is lower than in a short burst; the average of the last `sustained` of 2 x `sustained` launches
     sustained = None
@@ -578,6 +641,7 @@ def main() -> None:
         "weak": weak,
         "settle": settle,
         "c4_per_rank": c4_per_rank,
+        "dp_exchange": dp_exchange,
         "frame": frame,
         "wide_c5": wide,
         "hash": hashgrid,
