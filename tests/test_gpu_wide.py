@@ -5,7 +5,8 @@ Tolerances:
 * f16 path vs ORC_MIXED (same numerics model as the 64-wide network): relative L2 <= 1e-3 and at most 0.1 % of the
   queries beyond 16 f16 ulps of their output scale (north_star tolerance);
 * e4m3 conversion (med3 clamp + v_cvt_pk_fp8_f32) vs the oracle's RNE: bit-exact;
-* FP8 path vs ORC_FP8: relative L2 <= 3e-2 and >= 98 % of outputs within 2^-10 relative
+* FP8 path vs ORC_FP8: relative L2 <= 2.2e-2 (70,001 queries; 3e-2 at 1 and 33) and >= 98 % of outputs within 2^-10
+  relative
   (measured 1.4-1.9e-2 and 99.3 % at 70,001 queries). Not bit-exact by construction: the MX MFMA's 64-element fp8 block sum is
   not f32-exact (<= ~2.2e-5 of sum|a*b|, tools/microbench/fp8_probe.hip), so a pre-activation near an e4m3 rounding
   boundary can land one e4m3 step (2^-3 relative) away and that step propagates;
@@ -124,7 +125,10 @@ def test_wide_fp8_infer_parity(nrc, orc, dev, wnet, n):
         print(f"fp8 vs ORC_FP8 rel-L2 {r8:.2e} ({close:.3f} of outputs within 2^-10), ORC_FP8 vs the f16 network "
               f"{rel(y8, ymx):.2e}, GPU fp8 vs the f16 network {rel(o8, ymx):.2e}")
         assert close > 0.98
-    assert r8 <= 3e-2, r8
+    print(f"n={n}: fp8 vs ORC_FP8 rel-L2 {r8:.3e}")
+    # round 4: a frame-sized sample is held to 2.2e-2 (measured 1.4e-2 - 1.9e-2); a handful of
+    # queries keeps 3e-2 (one query one e4m3 step away moves a 33-query rel-L2 by more)
+    assert r8 <= (2.2e-2 if n > 1000 else 3e-2), r8
 
 
 def test_wide_fp8_configured_handle(nrc, orc, dev):
