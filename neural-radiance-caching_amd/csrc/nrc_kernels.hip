@@ -532,8 +532,9 @@ struct LdsCorners {
     uint32_t off[8];
     float w[8];
 };
+// round-3 form (scalar f32 products; A/B: hash_feature_kernel ablation bit 8)
 template <bool DENSE>
-__device__ __forceinline__ void hash_corners_lds(float px, float py, float pz, int l, LdsCorners& C) {
+__device__ __forceinline__ void hash_corners_lds_r3(float px, float py, float pz, int l, LdsCorners& C) {
     const float scale = (float)(16 << l) - 1.0f;
     const uint32_t res = 16u << l;
     const float xs[3] = {px, py, pz};
@@ -561,7 +562,64 @@ __device__ __forceinline__ void hash_corners_lds(float px, float py, float pz, i
     }
 }
 
-template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores
+template <bool DENSE>
+__device__ __forceinline__ void hash_corners_lds(float px, float py, float pz, int l, LdsCorners& C) {
+    const float scale = (float)(16 << l) - 1.0f;
+    const uint32_t res = 16u << l;
+    // round 4: the per-dimension and per-corner f32 products as packed pairs (v_pk_fma_f32 / v_pk_add_f32 /
+    // v_pk_mul_f32: two IEEE operations per instruction, the same roundings), since the feature pass is VALU-bound
+    const f2 p01 = __builtin_elementwise_fma(f2{scale, scale}, f2{px, py}, f2{0.5f, 0.5f});
+    const float pos[3] = {p01[0], p01[1], __builtin_fmaf(scale, pz, 0.5f)};
+    float fr[3];
+    uint32_t cell[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float fl = floorf(pos[d]);
+        cell[d] = (uint32_t)(int)fl;
+        fr[d] = pos[d] - fl;
+    }
+    const uint32_t mask4 = (l == 0 ? 4095u : 32767u) << 2;
+    const uint32_t ym = 4u * (DENSE ? res : NRC_HASH_PRIME1), zm = 4u * (DENSE ? res * res : NRC_HASH_PRIME2);
+    const uint32_t X[2] = {4u * cell[0], 4u * cell[0] + 4u};
+    const uint32_t Y[2] = {cell[1] * ym, cell[1] * ym + ym};
+    const uint32_t Z[2] = {cell[2] * zm, cell[2] * zm + zm};
+    const f2 om01 = f2{1.0f, 1.0f} - f2{fr[0], fr[1]};  // 1 - fr for x, y
+    const f2 wx = {om01[0], fr[0]};                       // (wx0, wx1)
+    const float wy[2] = {om01[1], fr[1]}, wz[2] = {1.0f - fr[2], fr[2]};
+    // (wx[bx] * wy[by]) * wz[bz] for bx = 0, 1 in one packed multiply each
+    f2 wxy[2], w[4];
+#pragma unroll
+    for (int by = 0; by < 2; ++by) wxy[by] = wx * f2{wy[by], wy[by]};
+#pragma unroll
+    for (int bz = 0; bz < 2; ++bz)
+#pragma unroll
+        for (int by = 0; by < 2; ++by) w[bz * 2 + by] = wxy[by] * f2{wz[bz], wz[bz]};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+        const uint32_t i = DENSE ? X[bx] + (Y[by] + Z[bz]) : X[bx] ^ (Y[by] ^ Z[bz]);
+        C.off[c] = i & mask4;
+        C.w[c] = w[bz * 2 + by][bx];
+    }
+}
+
+// hash_interp with the corner weights converted two at a time (corners 2k, 2k + 1 in one v_cvt_pk_f16_f32) and each
+// half broadcast into the packed FMA (op_sel): the same f16 roundings and FMA order, half the conversions
+__device__ __forceinline__ uint32_t hash_interp_pk(const float (&w)[8], const uint32_t (&v)[8]) {
+    h2v acc = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t w2 = pk2(w[2 * k], w[2 * k + 1]);
+        asm volatile("" : "+v"(w2));  // (half)w rounded before the FMA (no v_fma_mix folding)
+        const h2v wp = __builtin_bit_cast(h2v, w2);
+        acc = __builtin_elementwise_fma(h2v{wp[0], wp[0]}, __builtin_bit_cast(h2v, v[2 * k]), acc);
+        acc = __builtin_elementwise_fma(h2v{wp[1], wp[1]}, __builtin_bit_cast(h2v, v[2 * k + 1]), acc);
+    }
+    return __builtin_bit_cast(uint32_t, acc);
+}
+
+template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores;
+                        // 8 the round-3 scalar arithmetic (same results)
 __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __restrict__ q, int64_t n, int P,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ feat) {
@@ -611,7 +669,10 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
             if (i - (int)threadIdx.x >= cnt) return false;  // block-uniform
             LdsCorners C[2];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) hash_corners_lds<kDense>(PB[cur][u].x, PB[cur][u].y, PB[cur][u].z, level, C[u]);
+            for (int u = 0; u < 2; ++u) {
+                if constexpr ((ABL & 8) != 0) hash_corners_lds_r3<kDense>(PB[cur][u].x, PB[cur][u].y, PB[cur][u].z, level, C[u]);
+                else hash_corners_lds<kDense>(PB[cur][u].x, PB[cur][u].y, PB[cur][u].z, level, C[u]);
+            }
             PB[cur][0] = load_pos(i + 4096);
             PB[cur][1] = load_pos(i + 5120);
             uint32_t v[2][8];
@@ -622,10 +683,15 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
                     v[u][c] = (ABL & 1) ? C[u].off[c] : *reinterpret_cast<const uint32_t*>(ltb + C[u].off[c]);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                HashCorners W;
+                uint32_t f;
+                if constexpr ((ABL & 8) != 0) {
+                    HashCorners W;
 #pragma unroll
-                for (int c = 0; c < 8; ++c) W.w[c] = C[u].w[c];
-                const uint32_t f = hash_interp(W, v[u]);
+                    for (int c = 0; c < 8; ++c) W.w[c] = C[u].w[c];
+                    f = hash_interp(W, v[u]);
+                } else {
+                    f = hash_interp_pk(C[u].w, v[u]);
+                }
                 __builtin_amdgcn_raw_buffer_store_b32(f, rf, (ABL & 4) ? kBufferOff : (i + 1024 * u) * 4, 0, 0);
             }
             i += 2048;
@@ -3074,8 +3140,11 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
 #if NRC_DEBUG_KERNELS
             const int fa = knob(kKnobHashFeatAbl);
             if (fa > 0) {
-                auto k = fa == 1 ? hash_feature_kernel<1> : fa == 2 ? hash_feature_kernel<2> : fa == 4 ? hash_feature_kernel<4>
-                                                                                                   : hash_feature_kernel<7>;
+                auto k = fa == 1   ? hash_feature_kernel<1>
+                         : fa == 2 ? hash_feature_kernel<2>
+                         : fa == 4 ? hash_feature_kernel<4>
+                         : fa == 8 ? hash_feature_kernel<8>  // round-3 arithmetic (A/B of the packed form)
+                                   : hash_feature_kernel<7>;
                 hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
             } else
 #endif

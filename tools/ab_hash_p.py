@@ -1,8 +1,8 @@
-"""In-process interleaved A/B of the Hash feature pass's query-range count P (knob hash_feat_p): inference over 2^21
-synthetic Cornell queries, HIP events on the network's stream; outputs must be bitwise equal across P (the features of
-a query do not depend on which block computes them).
+"""In-process interleaved A/B of a Hash-inference knob (default: the feature pass's query-range count P, knob
+hash_feat_p; debug library: hash_feat_abl=8, the round-3 arithmetic): inference over 2^21 synthetic Cornell queries,
+HIP events on the network's stream; outputs must be bitwise equal across the values.
 
-    python tools/ab_hash_p.py [--ps 16,32,64] [--rounds 5] [--iters 20]
+    python tools/ab_hash_p.py [--knob hash_feat_p] [--ps 16,32,64] [--rounds 5] [--iters 20]
 """
 from __future__ import annotations
 
@@ -20,7 +20,9 @@ import nrc_loader  # noqa: E402
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ps", default="16,32,64")
+    ap.add_argument("--ps", default="16,32,64", help="knob values")
+    ap.add_argument("--knob", default="hash_feat_p")
+    ap.add_argument("--set", action="append", default=[], help="name=value knob held for the whole run")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--queries", type=int, default=1 << 21)
@@ -28,6 +30,9 @@ def main() -> None:
     import torch
 
     nrc = nrc_loader.load()
+    for kv in args.set:
+        k, v = kv.split("=")
+        nrc._lib.set_knob(k, int(v))
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream()
     net = nrc.Network()
@@ -41,7 +46,7 @@ def main() -> None:
     ps = [int(p) for p in args.ps.split(",")]
     outs = {}
     for p in ps:
-        nrc._lib.set_knob("hash_feat_p", p)
+        nrc._lib.set_knob(args.knob, p)
         outs[p] = torch.empty((n, 3), device=dev)
         net.infer(q, outs[p], n)
     torch.cuda.synchronize()
@@ -49,7 +54,7 @@ def main() -> None:
     times = {p: [] for p in ps}
     for _ in range(args.rounds):
         for p in ps:
-            nrc._lib.set_knob("hash_feat_p", p)
+            nrc._lib.set_knob(args.knob, p)
             for _ in range(3):
                 net.infer(q, outs[p], n)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -59,10 +64,10 @@ def main() -> None:
             e1.record(stream)
             torch.cuda.synchronize()
             times[p].append(e0.elapsed_time(e1) / args.iters * 1e3)
-    nrc._lib.set_knob("hash_feat_p", -1)
+    nrc._lib.set_knob(args.knob, -1)
     res = {p: {"median_us": float(np.median(times[p])), "min_us": float(np.min(times[p])),
                "bitwise_equal_to_first": equal[p]} for p in ps}
-    print(json.dumps({"queries": n, "by_P": res}))
+    print(json.dumps({"queries": n, "knob": args.knob, "held": args.set, "by_value": res}))
     net.destroy()
 
 
