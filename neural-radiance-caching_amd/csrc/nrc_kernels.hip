@@ -1255,6 +1255,12 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
                 for (int kk = 0; kk < 5; ++kk) x[t][kk] = __builtin_bit_cast(h8, (kk & 1) ? a : b);
             } else if constexpr ((ABL & 1024) != 0) {
                 encode_v3(Q[t], h, x[t]);
+                if constexpr ((ABL & 524288) != 0) {
+                    // energy probe (timing only, wrong outputs): 12 of the 14 constant-one pad slots (34..39 of both
+                    // halves) fed as zeros, i.e. what folding the pad weights into one bias slot per half would feed
+                    x[t][4] = h8{x[t][4][0], x[t][4][1], (_Float16)0, (_Float16)0, (_Float16)0, (_Float16)0,
+                                 (_Float16)0, (_Float16)0};
+                }
             } else {
                 encode_fast<(ABL & 16) != 0>(Q[t], h, x[t]);
             }
@@ -3089,6 +3095,8 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 57: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, true, 48 | 1024 | 2048>, 512, bpc[57], (ntiles + 1) / 2, queries, out, n, wf, s);
         case 58: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536 | 262144>, 768, bpc[58], (ntiles + 1) / 2, queries, out, n, wf, s);
         case 59: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, true, 48 | 1024 | 2048>, 768, bpc[59], (ntiles + 1) / 2, queries, out, n, wf, s);
+        // 60: energy probe (wrong outputs): 47 with 12 of the 14 pad slots of layer 0 fed as zeros
+        case 60: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | 524288>, 1024, bpc[60], ntiles, queries, out, n, wf, s);
 #endif
         // 47 (default, round 3): 39 with the output layer on 4x4x4 16-block MFMAs (65536); in-process A/B at 2^21
         // queries 82.3-82.6 vs 82.7-83.4 us (profiles/r03_infer/ab_out4x4_v47.json)
