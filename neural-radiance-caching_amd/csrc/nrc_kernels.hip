@@ -3141,9 +3141,11 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
         static int bpf[3] = {};
         for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
             const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
-            // query ranges per level (multiple of the 8 XCDs); knob hash_feat_p overrides (A/B)
+            // query ranges per level (multiple of the 8 XCDs); knob hash_feat_p overrides (A/B). Round 4: 32 above 2^19
+            // queries (4 blocks per CU, two ranges' positions per XCD L2 at a time): 179.7 vs 185.3 us (P = 16) per 2^21
+            // queries in-process, 24 / 48 / 64 / 128 slower (profiles/r04_hash/ab_hash_feat_p*.json)
             const int kp = knob(kKnobHashFeatP);
-            const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 16 : 8;
+            const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 32 : 8;
             const float* qc0 = queries + c0 * NRC_INPUT_DIMS;
 #if NRC_DEBUG_KERNELS
             const int fa = knob(kKnobHashFeatAbl);
