@@ -619,7 +619,7 @@ __device__ __forceinline__ uint32_t hash_interp_pk(const float (&w)[8], const ui
 }
 
 template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores;
-                        // 8 the round-3 scalar arithmetic (same results)
+                        // 8 the round-3 scalar arithmetic, 16 the round-3 unpipelined loop (same results)
 __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __restrict__ q, int64_t n, int P,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ feat) {
@@ -662,6 +662,65 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const char* const ltb = reinterpret_cast<const char*>(lt);
+    auto corners = [&](const f3& p, LdsCorners& C, auto dense_c) {
+        constexpr bool kDense = decltype(dense_c)::value;
+        if constexpr ((ABL & 8) != 0) hash_corners_lds_r3<kDense>(p.x, p.y, p.z, level, C);
+        else hash_corners_lds<kDense>(p.x, p.y, p.z, level, C);
+    };
+    auto gather = [&](const LdsCorners& C, uint32_t (&v)[8]) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = (ABL & 1) ? C.off[c] : *reinterpret_cast<const uint32_t*>(ltb + C.off[c]);
+    };
+    auto interp = [&](const LdsCorners& C, const uint32_t (&v)[8]) -> uint32_t {
+        if constexpr ((ABL & 8) != 0) {
+            HashCorners W;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) W.w[c] = C.w[c];
+            return hash_interp(W, v);
+        } else {
+            return hash_interp_pk(C.w, v);
+        }
+    };
+    // Round 4 (default): software-pipelined steps. PMC of the round-3 loop: LDS 47 % and VALU 43 % busy, waves waiting
+    // on their own dependencies 62 % of their cycles -- each step ran hash -> 16 gathers -> wait -> interpolate in
+    // series. Here a step is one query per lane, and step s + 1's corners are computed and its 8 gathers issued before
+    // step s's 8 are consumed: 16 gathers in flight per wave (the wait for the older 8 is lgkmcnt(8): gfx950's LDS
+    // counter field holds at most 15, so a 2-query step's 16 + 16 could not be waited for exactly) and the hashing
+    // overlaps the LDS latency. Same arithmetic per query.
+    auto body_pipe = [&](auto dense_c) {
+        f3 PP[2] = {PB[0][0], PB[0][1]};  // positions of steps 0, 1 (queries i, i + 1024), loaded above
+        LdsCorners C[2];
+        uint32_t v[2][8];
+        corners(PP[0], C[0], dense_c);
+        PP[0] = load_pos(i + 2048);  // step 2
+        gather(C[0], v[0]);
+        // step 0's gathers land before the loop (a compiler-visible s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched): the
+        // waitcnt pass merges the loop entry with the back edge, and gathers still in flight on the entry edge (into
+        // other registers than the back edge's) made it wait lgkmcnt(0) at the top of every other phase
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        // phase cur: step s (set cur, gathers in flight) -> prepare step s + 1 in set nxt, then finish step s
+        auto phase = [&](auto cur_c) -> bool {
+            constexpr int cur = decltype(cur_c)::value, nxt = 1 - cur;
+            if (i - (int)threadIdx.x >= cnt) return false;  // block-uniform
+            // step s + 1 (positions past the range read 0: valid LDS offsets, results never stored)
+            corners(PP[nxt], C[nxt], dense_c);
+            PP[nxt] = load_pos(i + 3072);  // step s + 3
+            gather(C[nxt], v[nxt]);
+            __builtin_amdgcn_raw_buffer_store_b32(interp(C[cur], v[cur]), rf, (ABL & 4) ? kBufferOff : i * 4, 0, 0);
+            i += 1024;
+            return true;
+        };
+        while (phase(std::integral_constant<int, 0>{}) && phase(std::integral_constant<int, 1>{})) {
+        }
+    };
+    if constexpr ((ABL & 16) == 0) {
+        if (level <= 1) body_pipe(std::integral_constant<bool, true>{});
+        else body_pipe(std::integral_constant<bool, false>{});
+        return;
+    }
+    // ABL & 16: the round-3 loop (A/B)
     auto body = [&](auto dense_c) {
         constexpr bool kDense = decltype(dense_c)::value;
         auto step = [&](auto cur_c) -> bool {
@@ -3154,6 +3213,7 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
                          : fa == 2 ? hash_feature_kernel<2>
                          : fa == 4 ? hash_feature_kernel<4>
                          : fa == 8 ? hash_feature_kernel<8>  // round-3 arithmetic (A/B of the packed form)
+                         : fa == 16 ? hash_feature_kernel<16>  // round-3 loop (A/B of the pipelined steps)
                                    : hash_feature_kernel<7>;
                 hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
             } else
