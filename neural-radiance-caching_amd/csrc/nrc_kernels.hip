@@ -3929,38 +3929,53 @@ __global__ __launch_bounds__(1024) void peer_push_kernel(const float* __restrict
     }
 }
 
+template <int WMAX>  // the world's bucket (2, 4, 8, 16): the rank-order sum is unrolled over WMAX ranks
 __global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict__ xbuf, int world, int stride, uint32_t seq,
                                                          uint32_t* err, float* __restrict__ loss_out, ModelBuffers mb,
                                                          OptimArgs oa, float lr_t, float ema_debias) {
     const int par = (int)(seq & 1u);
-    if (threadIdx.x < (unsigned)(world * kPeerSplit)) {  // one lane per (source rank, part) flag
+    const int nflags = world * kPeerSplit;
+    __shared__ uint32_t timed_out;
+    if (threadIdx.x < 64) {
+        // wave 0 polls every (source rank, part) flag, one per lane (lanes past them re-read flag 0): the loop is
+        // wave-uniform (ballot) and holds no store (tests/test_asm_hazards.py rule 3). Relaxed system-scope polls of
+        // uncached memory (no L2 invalidate per poll); the data loads below are issued after the flags have returned
+        // (the barrier follows the loop) and read memory, not a cache. Fast polls first (~0.1 ms), then ~4 us apart:
+        // about 10 s in all.
+        const int lane = threadIdx.x;
         const uint32_t* f = reinterpret_cast<const uint32_t*>(xbuf + (int64_t)2 * world * stride) +
-                            (par * world * kPeerSplit + (int)threadIdx.x) * kPeerFlagStride;
+                            (par * nflags + (lane < nflags ? lane : 0)) * kPeerFlagStride;
         int i = 0;
-        // relaxed system-scope polls of uncached memory (no L2 invalidate per poll); the data loads below are issued
-        // after the flag value has returned (the branch waits for it) and read memory, not a cache.
-        // fast polls first (~0.1 ms), then ~4 us apart: about 10 s in all
-        for (; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq && i < (1 << 21); ++i) {
+        for (; i < (1 << 21); ++i) {
+            const bool ready = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
+            if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;
             if (i < 4096) __builtin_amdgcn_s_sleep(1);
             else __builtin_amdgcn_s_sleep(127);
         }
-        if (i == (1 << 21)) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0) timed_out = i == (1 << 21) ? 1u : 0u;
     }
     __syncthreads();
+    if (timed_out && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const float* const base = xbuf + (int64_t)par * world * stride;
-    auto ld = [&](int r, int p) {  // peer-written uncached memory, read at system scope
+    // peer-written uncached memory, read at system scope; the world sum in rank order, branch-free (a rank past the
+    // world re-reads rank 0 and is not added)
+    auto ld = [&](int r, int p) {
         return __hip_atomic_load(base + (int64_t)r * stride + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     };
-    if (blockIdx.x == 0 && threadIdx.x == 0 && loss_out) {
-        float L = ld(0, mb.n_total);
-        for (int r = 1; r < world; ++r) L += ld(r, mb.n_total);
-        loss_out[0] = L;
-    }
+    auto world_sum = [&](int p) {
+        float v[WMAX];
+#pragma unroll
+        for (int r = 0; r < WMAX; ++r) v[r] = ld(r < world ? r : 0, p);
+        float g = v[0];
+#pragma unroll
+        for (int r = 1; r < WMAX; ++r) g = r < world ? g + v[r] : g;
+        return g;
+    };
+    if (blockIdx.x == 0 && threadIdx.x == 0 && loss_out) loss_out[0] = world_sum(mb.n_total);
     const int p = blockIdx.x * 256 + threadIdx.x;
     if (p >= mb.n_mlp) return;
-    float g = ld(0, p);
-    for (int r = 1; r < world; ++r) g += ld(r, p);
-    adam_pack_one(kApplyOnly, p, g, mb, oa, lr_t, ema_debias);
+    adam_pack_one(kApplyOnly, p, world_sum(p), mb, oa, lr_t, ema_debias);
 }
 
 hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int rank, int world, uint32_t seq,
@@ -3979,8 +3994,16 @@ hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq
     if (world < 2 || world > kPeerMaxRanks || !xbuf || !err) return hipErrorInvalidValue;
     float lr_t, ema_debias;
     adam_host_factors(oa, lr_t, ema_debias);
-    hipLaunchKernelGGL(peer_apply_kernel, dim3((mb.n_mlp + 255) / 256), dim3(256), 0, s, xbuf, world, peer_stride(nfl), seq,
-                       err, loss_out, mb, oa, lr_t, ema_debias);
+    const dim3 grid((mb.n_mlp + 255) / 256);
+    const int st = peer_stride(nfl);
+    if (world <= 2)
+        hipLaunchKernelGGL(peer_apply_kernel<2>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+    else if (world <= 4)
+        hipLaunchKernelGGL(peer_apply_kernel<4>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+    else if (world <= 8)
+        hipLaunchKernelGGL(peer_apply_kernel<8>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+    else
+        hipLaunchKernelGGL(peer_apply_kernel<16>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();
 }
 

@@ -11,3 +11,5 @@ NRC_LIB_PATH=neural-radiance-caching_amd/libnrc_amd_debug.so timeout -k 10 200 p
 cat gpurun_out/ab_hash_abl8.json
 timeout -k 10 200 python tools/ab_hash_p.py --ps 32,16 --rounds 5 > gpurun_out/ab_hash_p2.json 2> gpurun_out/ab_hash_p2.err || exit 5
 cat gpurun_out/ab_hash_p2.json
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dp.py -k "peer" -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_peer3.log 2>&1 || { echo "peer tests failed"; tail -20 gpurun_out/pytest_peer3.log; exit 9; }
+tail -1 gpurun_out/pytest_peer3.log
