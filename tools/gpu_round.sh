@@ -27,7 +27,9 @@ bench)
   cp gpurun_out/pmc_infer.json "profiles/pmc_infer_$ROUND.json"
   timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 4; }
   tail -1 gpurun_out/bench.log
-  cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --train-frames 5 --no-cpu --sustained 200 > "$ROOT/gpurun_out/prof_bench.log" 2>&1 || { echo "rocprof failed"; tail -20 "$ROOT/gpurun_out/prof_bench.log"; exit 5; }
+  # --no-c4: the infer kernel's rocprof summary then holds the 2^21-query launches only (the C4 shards'
+  # 2^19-query launches had been averaged in); the profiled run prints its own bench line (prof_bench.log)
+  cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --train-frames 5 --no-cpu --no-c4 --sustained 200 > "$ROOT/gpurun_out/prof_bench.log" 2>&1 || { echo "rocprof failed"; tail -20 "$ROOT/gpurun_out/prof_bench.log"; exit 5; }
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_train" -o run --output-format csv -- python3 "$ROOT/tools/time_train.py" --rounds 3 --iters 40 > "$ROOT/gpurun_out/prof_train.log" 2>&1 || { echo "train rocprof failed"; tail -20 "$ROOT/gpurun_out/prof_train.log"; exit 9; }
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_train128" -o run --output-format csv -- python3 "$ROOT/tools/time_train.py" --width 128 --rounds 3 --iters 40 > "$ROOT/gpurun_out/prof_train128.log" 2>&1 || { echo "train128 rocprof failed"; exit 10; }
   ;;
