@@ -619,7 +619,8 @@ __device__ __forceinline__ uint32_t hash_interp_pk(const float (&w)[8], const ui
 }
 
 template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores;
-                        // 8 the round-3 scalar arithmetic, 16 the round-3 unpipelined loop (same results)
+                        // 8 the round-3 scalar arithmetic, 16 the round-3 unpipelined loop (same results), 32 hashed
+                        // synthetic positions instead of the position loads
 __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __restrict__ q, int64_t n, int P,
                                                                const uint32_t* __restrict__ table,
                                                                uint32_t* __restrict__ feat) {
@@ -650,6 +651,18 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
         if constexpr ((ABL & 2) != 0) {
             const float u = (float)(k & 1023) * (1.0f / 1024.0f);
             return f3{u, 1.0f - u, u * u};
+        }
+        if constexpr ((ABL & 32) != 0) {  // no position loads, but scattered positions (the gathers keep their conflicts)
+            uint32_t hsh = (uint32_t)k * 0x9E3779B1u + (uint32_t)level;
+            float c[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                hsh ^= hsh >> 15;
+                hsh *= 0x2C1B3C6Du;
+                hsh ^= hsh >> 12;
+                c[d] = (float)(hsh >> 8) * (1.0f / 16777216.0f);
+            }
+            return f3{c[0], c[1], c[2]};
         }
         return __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rq, k * (NRC_INPUT_DIMS * 4), 0, 0));
     };
@@ -3214,6 +3227,9 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
                          : fa == 4 ? hash_feature_kernel<4>
                          : fa == 8 ? hash_feature_kernel<8>  // round-3 arithmetic (A/B of the packed form)
                          : fa == 16 ? hash_feature_kernel<16>  // round-3 loop (A/B of the pipelined steps)
+                         : fa == 32 ? hash_feature_kernel<32>  // no position loads, scattered positions
+                         : fa == 33 ? hash_feature_kernel<33>  // 32 without the gathers
+                         : fa == 36 ? hash_feature_kernel<36>  // 32 without the stores
                                    : hash_feature_kernel<7>;
                 hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
             } else
