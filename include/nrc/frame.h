@@ -87,6 +87,28 @@ nrc_status nrc_propagate_train_radiance(const nrc_train_suffix_end_vertex* end_v
                                         const nrc_training_record* records_d, nrc_float3* train_targets_d,
                                         uint32_t num_records, hipStream_t stream);
 
+/* USE_REFLECTANCE_FACTORING 1 (config.h:118; the reference's compile-time variant, off in its shipped build): the
+ * cache then learns radiance / reflectance, reflectance() = diffuse + specular of the RadianceQuery
+ * (neural_radiance_caching.h:118). Accumulation multiplies by the render query's reflectance after the throughput
+ * product (nrc_helpers.cu:95-97, 111-113, 118-120; copy_radiance_to_output_buffer :66-68); propagation multiplies the
+ * end radiance by the end query's reflectance and each record's target by its own before the update, stores
+ * safeDiv(radiance, reflectance) (a zero component gives 0, :28-35, :191-204) and carries the radiance itself.
+ * end_render_queries / end_train_queries are the inference queries of those pixels / tiles; train_queries the records'
+ * queries as traced (train_queries_d[0]). Divisions are IEEE (the reference's fast-math build divides approximately). */
+nrc_status nrc_accumulate_render_radiance_factored(const nrc_float3* end_render_radiance_d,
+                                                   const float* end_render_queries_d,
+                                                   const nrc_float3* end_render_throughput_d, float* output_rgba_d,
+                                                   uint32_t num_pixels, int mode, uint32_t iteration_index,
+                                                   hipStream_t stream);
+nrc_status nrc_copy_radiance_to_output_factored(const nrc_float3* radiance_d, const float* queries_d,
+                                                float* output_rgba_d, uint32_t num_pixels, hipStream_t stream);
+nrc_status nrc_propagate_train_radiance_factored(const nrc_train_suffix_end_vertex* end_vertices_d,
+                                                 const nrc_float3* end_train_radiance_d,
+                                                 const float* end_train_queries_d, uint32_t num_tiles,
+                                                 const nrc_training_record* records_d, nrc_float3* train_targets_d,
+                                                 const float* train_queries_d, uint32_t num_records,
+                                                 hipStream_t stream);
+
 /* The training shuffle's permutation (NRCUtil.cu:19-35 contract: a fresh pseudo-random permutation of
  * [0, n) per frame). The reference sorts curand keys with cub radix sort; here the permutation is a keyed
  * 4-round Feistel bijection with cycle walking, a pure function of (seed, frame_index, d) — no sort, no
@@ -131,6 +153,7 @@ typedef struct nrc_frame_params {
     int32_t train;                /* 0: inference/accumulation only */
     int32_t keep_render_results;  /* 1: also write the render queries' radiance to results_inference (unfused
                                      infer + accumulate, e.g. for the reference's debug dump); 0: fused */
+    int32_t reflectance_factoring; /* 1: USE_REFLECTANCE_FACTORING 1 (the *_factored kernels above; unfused) */
 } nrc_frame_params;
 
 /* Runs, on the handle's stream: infer -> accumulate (fused into infer for Full / CacheOnly unless

@@ -50,6 +50,7 @@ EXPORTS = [
     "nrc_debug_get_knob",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
+    "nrc_accumulate_render_radiance_factored", "nrc_copy_radiance_to_output_factored", "nrc_propagate_train_radiance_factored",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
     # include/nrc/stream.h (bound in stream.py)
     "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_open", "nrc_stream_close",

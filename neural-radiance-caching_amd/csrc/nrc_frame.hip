@@ -27,30 +27,57 @@ struct EndVertex {  // neural_radiance_caching.h:78-94
 };
 static_assert(sizeof(TrainRecord) == 28 && sizeof(EndVertex) == 16, "reference record sizes");
 
+// RadianceQuery::reflectance() = diffuse + specular (neural_radiance_caching.h:118; compact record: floats 9..11, 12..14)
+__device__ __forceinline__ F3 reflectance(const float* __restrict__ q, uint32_t i) {
+    const float* r = q + (size_t)i * NRC_INPUT_DIMS;
+    return F3{r[9] + r[12], r[10] + r[13], r[11] + r[14]};
+}
+
 // accumulate_render_radiance (nrc_helpers.cu:77-129), one pixel per lane; MODE is the RenderMode.
 // w = 1/(iterationIndex+1) comes from the host (correctly rounded).
-template <int MODE>
+// RF: USE_REFLECTANCE_FACTORING 1 (nrc_helpers.cu:95-97, 111-113, 118-120; copy_radiance_to_output_buffer :66-68): the
+// radiance times the render query's reflectance, after the throughput product
+template <int MODE, bool RF = false>
 __global__ __launch_bounds__(256) void accumulate_kernel(const F3* __restrict__ rad, const F3* __restrict__ thr,
-                                                         float4* __restrict__ rgba, uint32_t n, float w) {
+                                                         float4* __restrict__ rgba, uint32_t n, float w,
+                                                         const float* __restrict__ queries = nullptr) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     float4 o;
-    if constexpr (MODE == 0) {  // Full: dst += (T * L) * w
+    F3 R = {1.0f, 1.0f, 1.0f};
+    if constexpr (RF && MODE != 5) R = reflectance(queries, i);
+    if constexpr (MODE == 0) {  // Full: dst += (T * L) * w   (RF: ((T * L) * R) * w)
         const F3 L = rad[i], T = thr[i];
         o = rgba[i];
-        o.x = __builtin_fmaf(T.x * L.x, w, o.x);
-        o.y = __builtin_fmaf(T.y * L.y, w, o.y);
-        o.z = __builtin_fmaf(T.z * L.z, w, o.z);
-    } else if constexpr (MODE == 2) {  // CacheOnly
+        if constexpr (RF) {
+            o.x = __builtin_fmaf((T.x * L.x) * R.x, w, o.x);
+            o.y = __builtin_fmaf((T.y * L.y) * R.y, w, o.y);
+            o.z = __builtin_fmaf((T.z * L.z) * R.z, w, o.z);
+        } else {
+            o.x = __builtin_fmaf(T.x * L.x, w, o.x);
+            o.y = __builtin_fmaf(T.y * L.y, w, o.y);
+            o.z = __builtin_fmaf(T.z * L.z, w, o.z);
+        }
+    } else if constexpr (MODE == 2) {  // CacheOnly   (RF: (L * T) * R)
         const F3 L = rad[i], T = thr[i];
         o.x = L.x * T.x;
         o.y = L.y * T.y;
         o.z = L.z * T.z;
-    } else if constexpr (MODE == 4) {  // DebugCacheNoThroughputModulation / copy_radiance_to_output_buffer
+        if constexpr (RF) {
+            o.x *= R.x;
+            o.y *= R.y;
+            o.z *= R.z;
+        }
+    } else if constexpr (MODE == 4) {  // DebugCacheNoThroughputModulation / copy_radiance_to_output_buffer (RF: L * R)
         const F3 L = rad[i];
         o.x = L.x;
         o.y = L.y;
         o.z = L.z;
+        if constexpr (RF) {
+            o.x *= R.x;
+            o.y *= R.y;
+            o.z *= R.z;
+        }
     } else {  // 5: DebugThroughputOnly
         const F3 T = thr[i];
         o.x = T.x;
@@ -64,26 +91,49 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const F3* __restrict__ 
 // propagate_train_radiance (nrc_helpers.cu:131-224), one tile per lane walking its own record chain.
 // Chains are disjoint (one train path per tile), so the read-modify-write of targets needs no atomics.
 // Every lane exits: an index outside [0, nrec) ends the chain, and a chain is cut after nrec steps.
+// RF: USE_REFLECTANCE_FACTORING 1 (nrc_helpers.cu:156-160, 191-204): the targets hold radiance / reflectance; the end
+// radiance is multiplied by the end query's reflectance, each record's target by its own query's before the update and
+// divided by it after (safeDiv: a zero component gives 0, nrc_helpers.cu:28-35); the chain carries the radiance itself.
+template <bool RF = false>
 __global__ __launch_bounds__(256) void propagate_kernel(const EndVertex* __restrict__ ends,
                                                         const F3* __restrict__ end_rad, uint32_t tiles,
                                                         const TrainRecord* __restrict__ rec, F3* targets,
-                                                        uint32_t nrec) {
+                                                        uint32_t nrec, const float* __restrict__ end_q = nullptr,
+                                                        const float* __restrict__ train_q = nullptr) {
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= tiles) return;
     const EndVertex ev = ends[t];
     const F3 er = end_rad[t];
     F3 last = {er.x * ev.mask, er.y * ev.mask, er.z * ev.mask};  // :154
+    if constexpr (RF) {                                            // :159
+        const F3 R = reflectance(end_q, t);
+        last.x *= R.x;
+        last.y *= R.y;
+        last.z *= R.z;
+    }
     int i = ev.start;
     for (uint32_t steps = 0; i >= 0 && (uint32_t)i < nrec && steps < nrec; ++steps) {
         const int next = rec[i].prop_to;
         const F3 lt = rec[i].lt;
         F3 v = targets[i];
+        F3 R = {1.0f, 1.0f, 1.0f};
+        if constexpr (RF) {  // :191-193 radianceTo = targetTo * refl
+            R = reflectance(train_q, (uint32_t)i);
+            v.x *= R.x;
+            v.y *= R.y;
+            v.z *= R.z;
+        }
         v.x = __builtin_fmaf(lt.x, last.x, v.x);  // :199 radianceTo += localThroughput * lastRadiance
         v.y = __builtin_fmaf(lt.y, last.y, v.y);
         v.z = __builtin_fmaf(lt.z, last.z, v.z);
-        targets[i] = v;  // :205
-        last = v;        // :213
-        i = next;        // :214
+        if constexpr (RF) {  // :203 targetTo = safeDiv(radianceTo, refl)
+            targets[i] = F3{R.x != 0.0f ? v.x / R.x : 0.0f, R.y != 0.0f ? v.y / R.y : 0.0f,
+                            R.z != 0.0f ? v.z / R.z : 0.0f};
+        } else {
+            targets[i] = v;  // :205
+        }
+        last = v;  // :213
+        i = next;  // :214
     }
 }
 
@@ -171,27 +221,47 @@ inline dim3 grid_for(uint64_t threads) { return dim3((unsigned)((threads + 255) 
 }  // namespace
 
 hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,
-                             hipStream_t s) {
+                             hipStream_t s, const float* queries) {
     if (n == 0) return hipSuccess;
     const F3* r = reinterpret_cast<const F3*>(rad);
     const F3* t = reinterpret_cast<const F3*>(thr);
     float4* o = reinterpret_cast<float4*>(rgba);
+    const dim3 g = grid_for(n), b(256);
+    if (queries) {  // USE_REFLECTANCE_FACTORING 1
+        switch (mode) {
+        case 0: hipLaunchKernelGGL((accumulate_kernel<0, true>), g, b, 0, s, r, t, o, n, w, queries); break;
+        case 2: hipLaunchKernelGGL((accumulate_kernel<2, true>), g, b, 0, s, r, t, o, n, w, queries); break;
+        case 4: hipLaunchKernelGGL((accumulate_kernel<4, true>), g, b, 0, s, r, t, o, n, w, queries); break;
+        case 5: hipLaunchKernelGGL((accumulate_kernel<5, true>), g, b, 0, s, r, t, o, n, w, queries); break;
+        default: return hipSuccess;
+        }
+        return hipGetLastError();
+    }
     switch (mode) {
-    case 0: hipLaunchKernelGGL(accumulate_kernel<0>, grid_for(n), dim3(256), 0, s, r, t, o, n, w); break;
-    case 2: hipLaunchKernelGGL(accumulate_kernel<2>, grid_for(n), dim3(256), 0, s, r, t, o, n, w); break;
-    case 4: hipLaunchKernelGGL(accumulate_kernel<4>, grid_for(n), dim3(256), 0, s, r, t, o, n, w); break;
-    case 5: hipLaunchKernelGGL(accumulate_kernel<5>, grid_for(n), dim3(256), 0, s, r, t, o, n, w); break;
+    case 0: hipLaunchKernelGGL(accumulate_kernel<0>, g, b, 0, s, r, t, o, n, w, nullptr); break;
+    case 2: hipLaunchKernelGGL(accumulate_kernel<2>, g, b, 0, s, r, t, o, n, w, nullptr); break;
+    case 4: hipLaunchKernelGGL(accumulate_kernel<4>, g, b, 0, s, r, t, o, n, w, nullptr); break;
+    case 5: hipLaunchKernelGGL(accumulate_kernel<5>, g, b, 0, s, r, t, o, n, w, nullptr); break;
     default: return hipSuccess;  // NoCache / CacheFirstVertex: nothing to accumulate (nrc_helpers.cu:104-107)
     }
     return hipGetLastError();
 }
 
 hipError_t launch_propagate(const void* ends, const float* end_rad, uint32_t tiles, const void* records,
-                            float* targets, uint32_t nrec, hipStream_t s) {
+                            float* targets, uint32_t nrec, hipStream_t s, const float* end_queries,
+                            const float* train_queries) {
     if (tiles == 0 || nrec == 0) return hipSuccess;
-    hipLaunchKernelGGL(propagate_kernel, grid_for(tiles), dim3(256), 0, s, reinterpret_cast<const EndVertex*>(ends),
-                       reinterpret_cast<const F3*>(end_rad), tiles, reinterpret_cast<const TrainRecord*>(records),
-                       reinterpret_cast<F3*>(targets), nrec);
+    if ((end_queries == nullptr) != (train_queries == nullptr)) return hipErrorInvalidValue;
+    if (end_queries)
+        hipLaunchKernelGGL(propagate_kernel<true>, grid_for(tiles), dim3(256), 0, s,
+                           reinterpret_cast<const EndVertex*>(ends), reinterpret_cast<const F3*>(end_rad), tiles,
+                           reinterpret_cast<const TrainRecord*>(records), reinterpret_cast<F3*>(targets), nrec,
+                           end_queries, train_queries);
+    else
+        hipLaunchKernelGGL(propagate_kernel<false>, grid_for(tiles), dim3(256), 0, s,
+                           reinterpret_cast<const EndVertex*>(ends), reinterpret_cast<const F3*>(end_rad), tiles,
+                           reinterpret_cast<const TrainRecord*>(records), reinterpret_cast<F3*>(targets), nrec,
+                           nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -48,6 +48,29 @@ nrc_status nrc_accumulate_render_radiance(const nrc_float3* rad, const nrc_float
     });
 }
 
+nrc_status nrc_accumulate_render_radiance_factored(const nrc_float3* rad, const float* queries, const nrc_float3* thr,
+                                                   float* rgba, uint32_t n, int mode, uint32_t iteration_index,
+                                                   hipStream_t stream) {
+    return guarded([&] {
+        require(valid_mode(mode), "unknown render mode");
+        if (n == 0 || mode == NRC_RENDER_NO_CACHE || mode == NRC_RENDER_CACHE_FIRST_VERTEX) return;
+        require(rgba && aligned(rgba, 16), "output_rgba must be a 16-byte aligned float4 buffer");
+        require(mode == NRC_RENDER_DEBUG_THROUGHPUT_ONLY || (rad && queries), "radiance / query buffer is NULL");
+        require(mode == NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION || thr, "throughput buffer is NULL");
+        require(aligned(rad, 4) && aligned(thr, 4) && aligned(queries, 4), "buffers must be 4-byte aligned");
+        // DebugThroughputOnly does not read the queries (nrc_helpers.cu:124-127): any non-NULL pointer selects RF
+        static const float kNoQueries = 0.0f;
+        HIP_CHECK(launch_accumulate(reinterpret_cast<const float*>(rad), reinterpret_cast<const float*>(thr), rgba, n,
+                                    mode, accumulation_weight(iteration_index), stream, queries ? queries : &kNoQueries));
+    });
+}
+
+nrc_status nrc_copy_radiance_to_output_factored(const nrc_float3* rad, const float* queries, float* rgba, uint32_t n,
+                                                hipStream_t stream) {
+    return nrc_accumulate_render_radiance_factored(rad, queries, nullptr, rgba, n,
+                                                   NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0, stream);
+}
+
 nrc_status nrc_copy_radiance_to_output(const nrc_float3* rad, float* rgba, uint32_t n, hipStream_t stream) {
     return nrc_accumulate_render_radiance(rad, nullptr, rgba, n, NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0,
                                           stream);
@@ -64,6 +87,22 @@ nrc_status nrc_propagate_train_radiance(const nrc_train_suffix_end_vertex* ends,
         require(nrec <= (uint32_t)INT32_MAX, "num_records too large");
         HIP_CHECK(launch_propagate(ends, reinterpret_cast<const float*>(end_rad), tiles, records,
                                    reinterpret_cast<float*>(targets), nrec, stream));
+    });
+}
+
+nrc_status nrc_propagate_train_radiance_factored(const nrc_train_suffix_end_vertex* ends, const nrc_float3* end_rad,
+                                                 const float* end_queries, uint32_t tiles,
+                                                 const nrc_training_record* records, nrc_float3* targets,
+                                                 const float* train_queries, uint32_t nrec, hipStream_t stream) {
+    return guarded([&] {
+        if (tiles == 0 || nrec == 0) return;
+        require(ends && end_rad && records && targets && end_queries && train_queries, "NULL buffer");
+        require(aligned(ends, 4) && aligned(end_rad, 4) && aligned(records, 4) && aligned(targets, 4) &&
+                    aligned(end_queries, 4) && aligned(train_queries, 4),
+                "buffers must be 4-byte aligned");
+        require(nrec <= (uint32_t)INT32_MAX, "num_records too large");
+        HIP_CHECK(launch_propagate(ends, reinterpret_cast<const float*>(end_rad), tiles, records,
+                                   reinterpret_cast<float*>(targets), nrec, stream, end_queries, train_queries));
     });
 }
 
@@ -115,8 +154,10 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     require((uint64_t)screen + tiles <= UINT32_MAX, "screen_size + num_tiles overflows");
     const float* qi = fb->queries_inference_d;
     nrc_float3* ri = fb->results_inference_d;
-    // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion)
-    const bool fuse = !skip_render && !p->keep_render_results &&
+    // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion); with reflectance
+    // factoring the separate (factored) accumulation kernel runs instead
+    const bool rf = p->reflectance_factoring != 0;
+    const bool fuse = !skip_render && !p->keep_render_results && !rf &&
                       (mode == NRC_RENDER_FULL || mode == NRC_RENDER_CACHE_ONLY);
     if ((uint64_t)screen + tiles > 0) require(qi && ri, "inference buffers are NULL");
     auto infer_range = [&](uint32_t first, uint32_t count, uint32_t acc_pixels) {
@@ -137,15 +178,28 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
         infer_range(screen, tiles, 0);
     }
     // Device::nrcAccumulateRadiance (Device.cpp:1310-1337)
-    if (!skip_render && !fuse && npix > 0)
-        check(nrc_accumulate_render_radiance(fb->results_inference_d + p0, fb->last_render_throughput_d + p0,
-                                             fb->output_rgba_d + (size_t)p0 * 4, npix, mode, p->iteration_index, s));
+    if (!skip_render && !fuse && npix > 0) {
+        if (rf)
+            check(nrc_accumulate_render_radiance_factored(fb->results_inference_d + p0, qi + (size_t)p0 * NRC_INPUT_DIMS,
+                                                          fb->last_render_throughput_d + p0,
+                                                          fb->output_rgba_d + (size_t)p0 * 4, npix, mode,
+                                                          p->iteration_index, s));
+        else
+            check(nrc_accumulate_render_radiance(fb->results_inference_d + p0, fb->last_render_throughput_d + p0,
+                                                 fb->output_rgba_d + (size_t)p0 * 4, npix, mode, p->iteration_index, s));
+    }
     // Device::nrcVisualizeFirstRadiance (Device.cpp:1339-1370)
     if (mode == NRC_RENDER_CACHE_FIRST_VERTEX && npix > 0) {
         require(fb->queries_cache_vis_d && fb->results_cache_vis_d, "cache-vis buffers are NULL");
         check(nrc_infer_stream(net, fb->queries_cache_vis_d + (size_t)p0 * NRC_INPUT_DIMS,
                                reinterpret_cast<float*>(fb->results_cache_vis_d + p0), npix, s));
-        check(nrc_copy_radiance_to_output(fb->results_cache_vis_d + p0, fb->output_rgba_d + (size_t)p0 * 4, npix, s));
+        if (rf)
+            check(nrc_copy_radiance_to_output_factored(fb->results_cache_vis_d + p0,
+                                                       fb->queries_cache_vis_d + (size_t)p0 * NRC_INPUT_DIMS,
+                                                       fb->output_rgba_d + (size_t)p0 * 4, npix, s));
+        else
+            check(nrc_copy_radiance_to_output(fb->results_cache_vis_d + p0, fb->output_rgba_d + (size_t)p0 * 4, npix,
+                                              s));
     }
 
     // Training (Device.cpp:2505-2512): only when the trace produced records
@@ -154,8 +208,13 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     require(fb->train_queries_d[0] && fb->train_queries_d[1] && fb->train_targets_d[0] && fb->train_targets_d[1],
             "training double buffers are NULL");
     // Device::nrcPropagateRadiance (Device.cpp:1382-1419): end radiance = results after the render part
-    check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
-                                       fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
+    if (rf)  // the end queries are the inference queries after the render part; the records' are as traced
+        check(nrc_propagate_train_radiance_factored(fb->end_vertices_d, fb->results_inference_d + screen,
+                                                    qi + (size_t)screen * NRC_INPUT_DIMS, tiles, fb->train_records_d,
+                                                    fb->train_targets_d[0], fb->train_queries_d[0], (uint32_t)nrec, s));
+    else
+        check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
+                                           fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
     // Device::nrcShuffleTrainingData (Device.cpp:1427-1469)
     check(nrc_permute_train_data(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d,
                                  p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],

@@ -408,10 +408,12 @@ void net_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_
                         float* loss_d);
 
 // ---- per-frame kernels around the network (nrc_frame.hip, include/nrc/frame.h)
+// queries / end_queries + train_queries (RadianceQuery arrays, NULL = off): USE_REFLECTANCE_FACTORING 1
 hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,
-                             hipStream_t s);
+                             hipStream_t s, const float* queries = nullptr);
 hipError_t launch_propagate(const void* ends, const float* end_rad, uint32_t tiles, const void* records,
-                            float* targets, uint32_t nrec, hipStream_t s);
+                            float* targets, uint32_t nrec, hipStream_t s, const float* end_queries = nullptr,
+                            const float* train_queries = nullptr);
 hipError_t launch_permutation(uint64_t seed, uint32_t frame, int* perm, uint32_t n, hipStream_t s);
 hipError_t launch_permute(const float* qs, const float* ts, const int* perm, uint64_t seed, uint32_t frame,
                           uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s);

@@ -84,6 +84,9 @@ def _sigs():
         "nrc_copy_radiance_to_output": [vp, vp, u32, vp],
         "nrc_infer_accumulate": [vp, vp, vp, u32, vp, vp, u32, ctypes.c_int, u32],
         "nrc_propagate_train_radiance": [vp, vp, u32, vp, vp, u32, vp],
+        "nrc_accumulate_render_radiance_factored": [vp, vp, vp, vp, u32, ctypes.c_int, u32, vp],
+        "nrc_copy_radiance_to_output_factored": [vp, vp, vp, u32, vp],
+        "nrc_propagate_train_radiance_factored": [vp, vp, vp, u32, vp, vp, vp, u32, vp],
         "nrc_generate_train_permutation": [u64, u32, vp, u32, vp],
         "nrc_permute_train_data": [vp, vp, vp, u64, u32, i32, vp, vp, u32, vp],
         "nrc_process_frame": [vp, ctypes.POINTER(NrcFrameBuffers), ctypes.POINTER(NrcFrameParams),
@@ -111,7 +114,8 @@ class NrcFrameParams(ctypes.Structure):
     _fields_ = [("screen_size", ctypes.c_uint32), ("num_tiles", ctypes.c_uint32),
                 ("num_training_records", ctypes.c_int32), ("render_mode", ctypes.c_int32),
                 ("iteration_index", ctypes.c_uint32), ("frame_index", ctypes.c_uint32),
-                ("shuffle_seed", ctypes.c_uint64), ("train", ctypes.c_int32), ("keep_render_results", ctypes.c_int32)]
+                ("shuffle_seed", ctypes.c_uint64), ("train", ctypes.c_int32), ("keep_render_results", ctypes.c_int32),
+                ("reflectance_factoring", ctypes.c_int32)]
 
 
 def accumulate_render_radiance(radiance, throughput, output_rgba, num_pixels: int, mode: RenderMode,
@@ -119,6 +123,23 @@ def accumulate_render_radiance(radiance, throughput, output_rgba, num_pixels: in
     check(_sigs().nrc_accumulate_render_radiance(_ptr(radiance, "radiance"), _ptr(throughput, "throughput"),
                                                  _ptr(output_rgba, "output_rgba"), int(num_pixels), int(mode),
                                                  int(iteration_index), _stream(stream)))
+
+
+def accumulate_render_radiance_factored(radiance, queries, throughput, output_rgba, num_pixels: int, mode: RenderMode,
+                                        iteration_index: int, stream=None) -> None:
+    """USE_REFLECTANCE_FACTORING 1 form (frame.h): the radiance times the render query's reflectance."""
+    check(_sigs().nrc_accumulate_render_radiance_factored(
+        _ptr(radiance, "radiance"), _ptr(queries, "queries"), _ptr(throughput, "throughput"),
+        _ptr(output_rgba, "output_rgba"), int(num_pixels), int(mode), int(iteration_index), _stream(stream)))
+
+
+def propagate_train_radiance_factored(end_vertices, end_radiance, end_queries, num_tiles: int, records, targets,
+                                      train_queries, num_records: int, stream=None) -> None:
+    """USE_REFLECTANCE_FACTORING 1 form of propagate_train_radiance (frame.h): targets hold radiance / reflectance."""
+    check(_sigs().nrc_propagate_train_radiance_factored(
+        _ptr(end_vertices, "end_vertices"), _ptr(end_radiance, "end_radiance"), _ptr(end_queries, "end_queries"),
+        int(num_tiles), _ptr(records, "records"), _ptr(targets, "targets"), _ptr(train_queries, "train_queries"),
+        int(num_records), _stream(stream)))
 
 
 def infer_accumulate(net, queries, results, n: int, throughput, output_rgba, num_pixels: int, mode: RenderMode,
@@ -212,11 +233,13 @@ class FrameParams:
     shuffle_seed: int = 0
     train: bool = True
     keep_render_results: bool = False
+    reflectance_factoring: bool = False
 
     def as_struct(self) -> NrcFrameParams:
         return NrcFrameParams(int(self.screen_size), int(self.num_tiles), int(self.num_training_records),
                               int(self.render_mode), int(self.iteration_index), int(self.frame_index),
-                              int(self.shuffle_seed), int(bool(self.train)), int(bool(self.keep_render_results)))
+                              int(self.shuffle_seed), int(bool(self.train)), int(bool(self.keep_render_results)),
+                              int(bool(self.reflectance_factoring)))
 
 
 def process_frame(net, buffers: FrameBuffers, params: FrameParams, loss: bool = True):

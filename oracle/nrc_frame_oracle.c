@@ -92,6 +92,100 @@ void orc_propagate(const void* end_vertices, const float* end_radiance, int64_t 
     }
 }
 
+/* ---- USE_REFLECTANCE_FACTORING 1 (config.h:118): reflectance() = diffuse + specular of a compact RadianceQuery
+ * (neural_radiance_caching.h:118; floats 9..11 and 12..14). */
+static f3 reflectance(const float* q) {
+    f3 r;
+    r.x = q[9] + q[12];
+    r.y = q[10] + q[13];
+    r.z = q[11] + q[14];
+    return r;
+}
+
+/* accumulate_render_radiance with factoring: nrc_helpers.cu:93-97 (Full: radiance = T * L; radiance *= refl;
+ * dst += radiance * w), :109-113 (CacheOnly: L * T, then * refl), :116-120 (Debug...NoThroughputModulation: L * refl,
+ * also copy_radiance_to_output_buffer :65-68), :124-127 (DebugThroughputOnly: T). queries: the render queries. */
+void orc_accumulate_factored(const float* radiance, const float* throughput, const float* queries, float* rgba,
+                             int64_t n, int mode, uint32_t iteration_index) {
+    const float w = 1.0f / (float)(iteration_index + 1);
+    for (int64_t i = 0; i < n; i++) {
+        const float* L = radiance + 3 * i;
+        const float* T = throughput + 3 * i;
+        float* o = rgba + 4 * i;
+        float R[3] = {1.0f, 1.0f, 1.0f};
+        if (mode == 0 || mode == 2 || mode == 4) {
+            const f3 r = reflectance(queries + 15 * i);
+            R[0] = r.x;
+            R[1] = r.y;
+            R[2] = r.z;
+        }
+        switch (mode) {
+        case 0:
+            for (int c = 0; c < 3; c++) {
+                float r = T[c] * L[c];
+                r = r * R[c];
+                o[c] = fmaf(r, w, o[c]);
+            }
+            o[3] = 1.0f;
+            break;
+        case 2:
+            for (int c = 0; c < 3; c++) {
+                float r = L[c] * T[c];
+                o[c] = r * R[c];
+            }
+            o[3] = 1.0f;
+            break;
+        case 4:
+            for (int c = 0; c < 3; c++) o[c] = L[c] * R[c];
+            o[3] = 1.0f;
+            break;
+        case 5:
+            for (int c = 0; c < 3; c++) o[c] = T[c];
+            o[3] = 1.0f;
+            break;
+        default:
+            break;
+        }
+    }
+}
+
+/* propagate_train_radiance with factoring, nrc_helpers.cu:154-160 (lastRadiance = endRadiance * mask, then
+ * *= endQuery.reflectance()), :189-214 (radianceTo = target * refl; radianceTo += lt * last; target = safeDiv(
+ * radianceTo, refl) with safeDiv :28-35 = b != 0 ? a / b : 0 per component; last = radianceTo). */
+void orc_propagate_factored(const void* end_vertices, const float* end_radiance, const float* end_queries,
+                            int64_t num_tiles, const void* records, float* targets, const float* train_queries,
+                            int64_t num_records) {
+    const end_vertex* ev = (const end_vertex*)end_vertices;
+    const train_record* rec = (const train_record*)records;
+    for (int64_t t = 0; t < num_tiles; t++) {
+        f3 last;
+        last.x = end_radiance[3 * t + 0] * ev[t].mask;
+        last.y = end_radiance[3 * t + 1] * ev[t].mask;
+        last.z = end_radiance[3 * t + 2] * ev[t].mask;
+        const f3 re = reflectance(end_queries + 15 * t);
+        last.x *= re.x;
+        last.y *= re.y;
+        last.z *= re.z;
+        int32_t i = ev[t].start;
+        for (int64_t steps = 0; i >= 0 && i < num_records && steps < num_records; steps++) {
+            float* tg = targets + 3 * (int64_t)i;
+            const f3 R = reflectance(train_queries + 15 * (int64_t)i);
+            f3 v;
+            v.x = tg[0] * R.x;
+            v.y = tg[1] * R.y;
+            v.z = tg[2] * R.z;
+            v.x = fmaf(rec[i].lt.x, last.x, v.x);
+            v.y = fmaf(rec[i].lt.y, last.y, v.y);
+            v.z = fmaf(rec[i].lt.z, last.z, v.z);
+            tg[0] = R.x != 0.0f ? v.x / R.x : 0.0f;
+            tg[1] = R.y != 0.0f ? v.y / R.y : 0.0f;
+            tg[2] = R.z != 0.0f ? v.z / R.z : 0.0f;
+            last = v;
+            i = rec[i].prop_to;
+        }
+    }
+}
+
 /* ---- the shuffle permutation (keyed Feistel bijection, replaces curand keys + cub sort,
  * NRCUtil.cu:19-35). Stated independently of the HIP build from the written spec. */
 static uint32_t mix32(uint32_t x) { /* "lowbias32" integer hash */

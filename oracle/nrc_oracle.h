@@ -88,6 +88,12 @@ void orc_accumulate(const float* radiance, const float* throughput, float* rgba,
                     uint32_t iteration_index);
 void orc_propagate(const void* end_vertices, const float* end_radiance, int64_t num_tiles, const void* records,
                    float* targets, int64_t num_records);
+/* USE_REFLECTANCE_FACTORING 1 forms (queries: compact RadianceQuery arrays, 15 floats per record) */
+void orc_accumulate_factored(const float* radiance, const float* throughput, const float* queries, float* rgba,
+                             int64_t n, int mode, uint32_t iteration_index);
+void orc_propagate_factored(const void* end_vertices, const float* end_radiance, const float* end_queries,
+                            int64_t num_tiles, const void* records, float* targets, const float* train_queries,
+                            int64_t num_records);
 void orc_feistel_keys(uint64_t seed, uint32_t frame, uint32_t keys[4]);
 void orc_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n);
 void orc_permute(const float* q_src, const float* t_src, const int32_t* perm, uint64_t seed, uint32_t frame,

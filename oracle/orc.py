@@ -53,6 +53,8 @@ def lib() -> ctypes.CDLL:
         vp, u32, u64, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64
         L.orc_accumulate.argtypes = [vp, vp, vp, i64, ctypes.c_int, u32]
         L.orc_propagate.argtypes = [vp, vp, i64, vp, vp, i64]
+        L.orc_accumulate_factored.argtypes = [vp, vp, vp, vp, i64, ctypes.c_int, u32]
+        L.orc_propagate_factored.argtypes = [vp, vp, vp, i64, vp, vp, vp, i64]
         L.orc_feistel_keys.argtypes = [u64, u32, vp]
         L.orc_permutation.argtypes = [u64, u32, vp, u32]
         L.orc_permute.argtypes = [vp, vp, vp, u64, u32, ctypes.c_int32, vp, vp, u32]
@@ -198,25 +200,37 @@ def _v(a: np.ndarray) -> int:
 
 
 def accumulate(radiance: np.ndarray, throughput: np.ndarray, rgba: np.ndarray, mode: int,
-               iteration_index: int) -> np.ndarray:
-    """accumulate_render_radiance (nrc_helpers.cu:77-129); returns an updated copy of rgba [n, 4]."""
+               iteration_index: int, queries: np.ndarray | None = None) -> np.ndarray:
+    """accumulate_render_radiance (nrc_helpers.cu:77-129); returns an updated copy of rgba [n, 4]. queries (the render
+    queries [n, 15]): the USE_REFLECTANCE_FACTORING 1 form."""
     r = np.ascontiguousarray(radiance, dtype=np.float32)
     t = np.ascontiguousarray(throughput, dtype=np.float32)
     o = np.array(rgba, dtype=np.float32, order="C")
-    lib().orc_accumulate(_v(r), _v(t), _v(o), o.shape[0], int(mode), int(iteration_index))
+    if queries is None:
+        lib().orc_accumulate(_v(r), _v(t), _v(o), o.shape[0], int(mode), int(iteration_index))
+    else:
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        lib().orc_accumulate_factored(_v(r), _v(t), _v(q), _v(o), o.shape[0], int(mode), int(iteration_index))
     return o
 
 
 def propagate(end_vertices: np.ndarray, end_radiance: np.ndarray, records: np.ndarray, targets: np.ndarray,
-              num_records: int) -> np.ndarray:
+              num_records: int, end_queries: np.ndarray | None = None,
+              train_queries: np.ndarray | None = None) -> np.ndarray:
     """propagate_train_radiance (nrc_helpers.cu:131-224); end_vertices / records are the structured
-    dtypes of nrc_amd.frame (16 B / 28 B). Returns an updated copy of targets [n, 3]."""
+    dtypes of nrc_amd.frame (16 B / 28 B). Returns an updated copy of targets [n, 3]. end_queries [tiles, 15] and
+    train_queries [records, 15]: the USE_REFLECTANCE_FACTORING 1 form."""
     ev = np.ascontiguousarray(end_vertices)
     er = np.ascontiguousarray(end_radiance, dtype=np.float32)
     rec = np.ascontiguousarray(records)
     assert ev.dtype.itemsize == 16 and rec.dtype.itemsize == 28
     t = np.array(targets, dtype=np.float32, order="C")
-    lib().orc_propagate(_v(ev), _v(er), ev.shape[0], _v(rec), _v(t), int(num_records))
+    if end_queries is None:
+        lib().orc_propagate(_v(ev), _v(er), ev.shape[0], _v(rec), _v(t), int(num_records))
+    else:
+        eq = np.ascontiguousarray(end_queries, dtype=np.float32)
+        tq = np.ascontiguousarray(train_queries, dtype=np.float32)
+        lib().orc_propagate_factored(_v(ev), _v(er), _v(eq), ev.shape[0], _v(rec), _v(t), _v(tq), int(num_records))
     return t
 
 

@@ -192,3 +192,66 @@ def test_sh_encoding_oracle_matches_numpy(nrc, orc):
     y_sh = orc.forward(p, q[:64].astype(np.float32), orc.FP32, encoding=orc.FREQUENCY_SH)
     y_f = orc.forward(p, q[:64].astype(np.float32), orc.FP32)
     assert not np.array_equal(y_sh, y_f)
+
+
+def _refl(q):
+    """RadianceQuery::reflectance() = diffuse + specular (neural_radiance_caching.h:118), compact record."""
+    return (q[:, 9:12] + q[:, 12:15]).astype(np.float32)
+
+
+def test_accumulate_factored_matches_numpy(nrc, orc):
+    """USE_REFLECTANCE_FACTORING 1 (nrc_helpers.cu:95-97, 111-113, 118-120): the radiance times the render query's
+    reflectance, after the throughput product; DebugThroughputOnly ignores it."""
+    rng = np.random.default_rng(3)
+    n = 777
+    L = rng.lognormal(-1, 1.5, (n, 3)).astype(np.float32)
+    T = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    O = rng.uniform(0, 2, (n, 4)).astype(np.float32)
+    q = nrc.synthetic.cornell_queries(n, seed=3)
+    R = _refl(q)
+    for it in (0, 5):
+        w = np.float32(1.0) / np.float32(it + 1)
+        got = orc.accumulate(L, T, O, 0, it, queries=q)
+        want = (O[:, :3].astype(np.float64) + ((T * L) * R).astype(np.float64) * np.float64(w)).astype(np.float32)
+        np.testing.assert_array_max_ulp(got[:, :3], want, maxulp=1)
+    np.testing.assert_array_equal(orc.accumulate(L, T, O, 2, 5, queries=q)[:, :3], (L * T) * R)
+    np.testing.assert_array_equal(orc.accumulate(L, T, O, 4, 5, queries=q)[:, :3], L * R)
+    np.testing.assert_array_equal(orc.accumulate(L, T, O, 5, 5, queries=q)[:, :3], T)
+    for mode in (1, 3):
+        np.testing.assert_array_equal(orc.accumulate(L, T, O, mode, 5, queries=q), O)
+
+
+def _propagate_factored_py(ends, end_rad, end_q, recs, targets, train_q, nrec):
+    t = targets.astype(np.float32).copy()
+    for k in range(len(ends)):
+        last = (end_rad[k] * np.float32(ends["radiance_mask"][k])) * _refl(end_q[k:k + 1])[0]
+        i = int(ends["start_train_record"][k])
+        steps = 0
+        while 0 <= i < nrec and steps < nrec:
+            R = _refl(train_q[i:i + 1])[0]
+            v = (t[i] * R).astype(np.float64) + recs["local_throughput"][i].astype(np.float64) * last.astype(np.float64)
+            v = v.astype(np.float32)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                t[i] = np.where(R != 0, v / np.where(R != 0, R, 1), np.float32(0))
+            last = v
+            i = int(recs["prop_to"][i])
+            steps += 1
+    return t
+
+
+def test_propagate_factored_matches_python(nrc, orc):
+    """USE_REFLECTANCE_FACTORING 1 (nrc_helpers.cu:156-160, 189-214): targets hold radiance / reflectance, the chain
+    carries the radiance; a zero reflectance component gives a zero target (safeDiv, :28-35)."""
+    f = nrc.synthetic.cornell_frame(64, 48, (4, 4), seed=7, capacity=512)
+    rng = np.random.default_rng(8)
+    end_rad = rng.lognormal(-1, 1, (f.num_tiles, 3)).astype(np.float32)
+    end_q = nrc.synthetic.cornell_queries(f.num_tiles, seed=9)
+    nrec = min(f.num_training_records, 512)
+    train_q = np.array(f.train_queries, copy=True)
+    train_q[::7, 9:15] = 0.0  # some records with zero reflectance: safeDiv's zero branch
+    got = orc.propagate(f.end_vertices, end_rad, f.train_records, f.train_targets, nrec, end_queries=end_q,
+                        train_queries=train_q)
+    want = _propagate_factored_py(f.end_vertices, end_rad, end_q, f.train_records, f.train_targets, train_q, nrec)
+    np.testing.assert_array_max_ulp(got, want, maxulp=2)
+    plain = orc.propagate(f.end_vertices, end_rad, f.train_records, f.train_targets, nrec)
+    assert not np.array_equal(got, plain)

@@ -290,3 +290,82 @@ def test_process_frame_fused_equals_unfused(nrc, dev):
     np.testing.assert_array_equal(o0, o1)
     np.testing.assert_array_equal(r0, r1)
     np.testing.assert_array_equal(w0, w1)
+
+
+# ---- USE_REFLECTANCE_FACTORING 1 (frame.h *_factored, nrc_frame_params.reflectance_factoring): bit-exact vs the oracle
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("n", [1, 100_003])
+def test_accumulate_factored_bitwise(nrc, orc, dev, mode, n):
+    import torch
+    rng = np.random.default_rng(n + 7 * mode)
+    L = rng.lognormal(-1, 1.5, (n, 3)).astype(np.float32)
+    T = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    O = rng.uniform(0, 2, (n, 4)).astype(np.float32)
+    q = nrc.synthetic.cornell_queries(n, seed=n + mode)
+    for it in (0, 13):
+        out = _t(O, dev)
+        nrc.frame.accumulate_render_radiance_factored(_t(L, dev), _t(q, dev), _t(T, dev), out, n, mode, it)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), orc.accumulate(L, T, O, mode, it, queries=q))
+
+
+@pytest.mark.parametrize("shape", [(64, 48, (4, 4), 512), (1920, 1080, (8, 8), 65536)])
+def test_propagate_factored_bitwise(nrc, orc, dev, shape):
+    import torch
+    w, h, tile, cap = shape
+    f = nrc.synthetic.cornell_frame(w, h, tile, seed=13, capacity=cap)
+    nrec = min(f.num_training_records, cap)
+    rng = np.random.default_rng(5)
+    end_rad = rng.lognormal(-1, 1, (f.num_tiles, 3)).astype(np.float32)
+    end_q = nrc.synthetic.cornell_queries(f.num_tiles, seed=17)
+    train_q = np.array(f.train_queries, copy=True)
+    train_q[::5, 9:15] = 0.0  # zero reflectance on some records: safeDiv's zero branch
+    tg = _t(f.train_targets, dev)
+    nrc.frame.propagate_train_radiance_factored(nrc.frame.records_to_device(f.end_vertices, dev), _t(end_rad, dev),
+                                                _t(end_q, dev), f.num_tiles,
+                                                nrc.frame.records_to_device(f.train_records, dev), tg,
+                                                _t(train_q, dev), nrec)
+    torch.cuda.synchronize()
+    want = orc.propagate(f.end_vertices, end_rad, f.train_records, f.train_targets, nrec, end_queries=end_q,
+                         train_queries=train_q)
+    np.testing.assert_array_equal(tg.cpu().numpy(), want)
+
+
+def test_process_frame_reflectance_factoring(nrc, orc, dev):
+    """The frame driver with reflectance_factoring: unfused inference, the factored accumulation with the render
+    queries, the factored propagation with the tile queries (inference buffer after the pixels) and the records'
+    queries as traced; the shuffle and training unchanged. Every step after inference bit-exact vs the oracle."""
+    import torch
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(320, 240, (4, 4), seed=23, frame_index=2)
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream())
+    fb, tq0, tt0, rec = _device_frame(nrc, f, dev)
+    out0 = np.random.default_rng(1).uniform(0, 1, (f.screen_size, 4)).astype(np.float32)
+    fb.output_rgba.copy_(_t(out0, dev))
+    fp = F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records, F.RenderMode.Full, iteration_index=3,
+                       frame_index=2, shuffle_seed=7, reflectance_factoring=True)
+    F.process_frame(net, fb, fp)
+    torch.cuda.synchronize()
+    res = fb.results_inference.cpu().numpy()
+    S = f.screen_size
+    np.testing.assert_array_equal(fb.output_rgba.cpu().numpy(),
+                                  orc.accumulate(res[:S], f.last_render_throughput, out0, 0, 3,
+                                                 queries=f.queries_inference[:S]))
+    nrec = min(f.num_training_records, 65536)
+    tt_prop = orc.propagate(f.end_vertices, res[S:], rec, tt0, nrec, end_queries=f.queries_inference[S:],
+                            train_queries=tq0)
+    np.testing.assert_array_equal(fb.train_targets[0].cpu().numpy(), tt_prop)
+    qd, td = orc.permute(tq0, tt_prop, None, 7, 2, nrec, 65536)
+    np.testing.assert_array_equal(fb.train_targets[1].cpu().numpy(), td)
+    assert net.step == 4
+    # CacheFirstVertex: the cache-vis radiance times the cache-vis queries' reflectance
+    fb.output_rgba.zero_()
+    fp2 = F.FrameParams(f.screen_size, f.num_tiles, 0, F.RenderMode.CacheFirstVertex, reflectance_factoring=True,
+                        train=False)
+    F.process_frame(net, fb, fp2, loss=False)
+    torch.cuda.synchronize()
+    cv = fb.results_cache_vis.cpu().numpy()
+    np.testing.assert_array_equal(fb.output_rgba.cpu().numpy(),
+                                  orc.accumulate(cv, cv, np.zeros((S, 4), np.float32), 4, 0, queries=f.queries_cache_vis))
+    net.destroy()
