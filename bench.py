@@ -279,7 +279,8 @@ def graph_ms_per_call(net, stream, fn, k: int, reps: int) -> float:
 def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_ms: float, step16k_ms: float) -> dict:
     """configs[3] (C4) per-rank work, measured on ONE GPU: what each of the 8 ranks runs.
     Inference: its 2^19-query shard (no collective). Training: one 2,048-sample slice of a 16,384-sample global
-    minibatch through nrc_train_dp on a world-1 RCCL communicator (gradient pass normalised by the global batch ->
+    minibatch through nrc_train_dp over a world-1 peer exchange (gradient pass normalised by the global batch -> the
+    reduction with the exchange and Adam/EMA fused) and over a world-1 RCCL communicator (gradient pass ->
     ncclAllReduce -> Adam/EMA), plus the gradient pass (nrc_train_grad) and the apply (nrc_train_apply) on their own.
     HIP events on the handle's stream. The 8-GPU prediction divides the 1-GPU work by the per-rank time; the
     all-reduce at 8 ranks is NOT measured here (a world-1 communicator moves no bytes) and is stated as an assumption."""
@@ -306,10 +307,18 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
     state = [net.get_state(s) for s in (nrc.StateSlot.PARAMS, nrc.StateSlot.INFER, nrc.StateSlot.EMA,
                                         nrc.StateSlot.ADAM_M, nrc.StateSlot.ADAM_V)]
     step0 = net.step
-    comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
-    net.set_comm(comm)
     tq, tt = frames_q[0], frames_t[0]
     k = 4 * iters
+    # the production data-parallel path: the one-shot peer exchange fused into the reduction, at world 1 (the rank's
+    # own buffer: every store, flag and poll of the N-rank step, without the xGMI hop)
+    peer_ms = None
+    try:
+        net.peer_exchange_open(0, 1, net.peer_exchange_handle(1))
+        peer_ms = timed(lambda i: net.train_dp(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B), k)
+    finally:
+        net.peer_exchange_close()
+    comm = nrc.Communicator(nrc.Communicator.unique_id(), 1, 0)
+    net.set_comm(comm)
     dp_ms = timed(lambda i: net.train_dp(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B), k)
     dp_graph_ms = graph_ms_per_call(net, stream, lambda i: net.train_dp(tq[(i % 4) * B:], tt[(i % 4) * B:], b_local, B),
                                     16, 10)
@@ -326,24 +335,33 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
         net.set_state(s, v)
     net.step = step0
     allreduce_assumed_us = 25.0
+    xgmi_assumed_us = 3.0
+    dp_step = peer_ms if peer_ms is not None else dp_ms
     return {"workload": "configs[3] per-rank work on one GPU: 2^19-query inference shard; a 2048-sample slice of a "
-                        "16384-sample global minibatch (nrc_train_dp, world-1 RCCL communicator)",
+                        "16384-sample global minibatch (nrc_train_dp: the peer exchange fused into the reduction at "
+                        "world 1; beside it the same step over a world-1 RCCL communicator)",
             "infer_queries": n, "infer_kernel_ms": infer_ms, "infer_M_queries_per_s": n / (infer_ms * 1e-3) / 1e6,
             "train_b_local": b_local, "train_global_b": B,
-            "train_dp_step_ms": dp_ms, "train_grad_ms": grad_ms, "train_apply_ms": apply_ms,
+            "train_dp_step_ms": dp_step, "train_dp_path": "peer exchange (world 1)" if peer_ms is not None else "rccl",
+            "train_dp_rccl_step_ms": dp_ms, "train_grad_ms": grad_ms, "train_apply_ms": apply_ms,
             "train_local_fused_step_ms": local_ms,
-            "graph_replayed": {"train_dp_step_ms": dp_graph_ms, "train_local_fused_step_ms": local_graph_ms,
+            "graph_replayed": {"train_dp_rccl_step_ms": dp_graph_ms, "train_local_fused_step_ms": local_graph_ms,
                                "what": "the same calls replayed from a HIP graph: GPU time per step without the "
                                        "per-call host cost (Python, ctypes, one hipLaunchKernel per kernel)"},
             "prediction_8gpu": {
                 "infer_speedup": (t_full_ms / infer_ms) if infer_ms > 0 else None,
                 "infer_what": "1-GPU kernel time of the whole 2^22-query frame / per-rank 2^19-query kernel time "
                               "(no collective on the inference path)",
+                "xgmi_us_assumed": xgmi_assumed_us,
+                "train_step_ms_8gpu": dp_step + xgmi_assumed_us * 1e-3,
+                "train_speedup": step16k_ms / (dp_step + xgmi_assumed_us * 1e-3),
+                "train_what": "1-GPU 16384-sample step / (per-rank world-1 peer-exchange step + an ASSUMED xGMI "
+                              "store + flag latency; unmeasured on 8 GPUs)",
                 "allreduce_us_assumed": allreduce_assumed_us,
-                "train_step_ms_8gpu": grad_ms + apply_ms + allreduce_assumed_us * 1e-3,
-                "train_speedup": step16k_ms / (grad_ms + apply_ms + allreduce_assumed_us * 1e-3),
-                "train_what": "1-GPU 16384-sample step / (per-rank gradient pass + apply + an ASSUMED 88-KiB RCCL "
-                              "all-reduce latency over 8 ranks; unmeasured)"}}
+                "train_step_ms_8gpu_rccl": grad_ms + apply_ms + allreduce_assumed_us * 1e-3,
+                "train_speedup_rccl": step16k_ms / (grad_ms + apply_ms + allreduce_assumed_us * 1e-3),
+                "train_what_rccl": "1-GPU 16384-sample step / (per-rank gradient pass + apply + an ASSUMED 88-KiB "
+                                   "RCCL all-reduce latency over 8 ranks; unmeasured)"}}
 
 
 def dp_exchange_bench(nrc, net, dev, world: int, rank: int, frames_q, frames_t, b0: int, bn: int, frames: int,

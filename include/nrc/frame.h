@@ -126,6 +126,27 @@ nrc_status nrc_permute_train_data(const float* queries_src_d, const nrc_float3* 
                                   int32_t num_records, float* queries_dst_d, nrc_float3* targets_dst_d,
                                   uint32_t n_out, hipStream_t stream);
 
+/* The entry points above that read RadianceQuery records, for padded 16-float records (USE_COMPACT_RADIANCE_QUERY 0,
+ * layout.h; the reference's same kernels compiled with the other struct). nrc_process_frame follows the handle's
+ * nrc_config.query_layout by itself. */
+nrc_status nrc_accumulate_render_radiance_factored_padded(const nrc_float3* end_render_radiance_d,
+                                                          const float* end_render_queries_d,
+                                                          const nrc_float3* end_render_throughput_d,
+                                                          float* output_rgba_d, uint32_t num_pixels, int mode,
+                                                          uint32_t iteration_index, hipStream_t stream);
+nrc_status nrc_copy_radiance_to_output_factored_padded(const nrc_float3* radiance_d, const float* queries_d,
+                                                       float* output_rgba_d, uint32_t num_pixels, hipStream_t stream);
+nrc_status nrc_propagate_train_radiance_factored_padded(const nrc_train_suffix_end_vertex* end_vertices_d,
+                                                        const nrc_float3* end_train_radiance_d,
+                                                        const float* end_train_queries_d, uint32_t num_tiles,
+                                                        const nrc_training_record* records_d,
+                                                        nrc_float3* train_targets_d, const float* train_queries_d,
+                                                        uint32_t num_records, hipStream_t stream);
+nrc_status nrc_permute_train_data_padded(const float* queries_src_d, const nrc_float3* targets_src_d,
+                                         const int32_t* permutation_d, uint64_t seed, uint32_t frame_index,
+                                         int32_t num_records, float* queries_dst_d, nrc_float3* targets_dst_d,
+                                         uint32_t n_out, hipStream_t stream);
+
 /* ---- one frame of Device::render's post-trace NRC sequence (Device.cpp:2493-2515) ---- */
 typedef struct nrc_frame_buffers {
     /* [screen + tiles] queries / results: render queries first, then one per train-suffix end (tile) */

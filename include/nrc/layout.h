@@ -52,6 +52,26 @@ typedef struct nrc_radiance_query {
     float specular[3];
 } nrc_radiance_query;
 
+/* RadianceQuery, non-compact layout (USE_COMPACT_RADIANCE_QUERY 0: neural_radiance_caching.h:38-40, :107-111):
+ * 16 f32 = 64 bytes, a pad_ float after the position (hit.cu:608 writes 0.0f), float2 direction / normal /
+ * roughness. Selected per handle by nrc_config.query_layout = NRC_QUERY_PADDED; the encodings then carry the
+ * reference's extra Identity(1) of pad_ right after the position encoding (NRCNetworkConfigs.h:61-67, :106-111):
+ *   Frequency: TriangleWave 0..35 | pad_ 36 | OneBlob 37..60 | Identity 61..66 | 1.0 x 13 (67..79)
+ *   Hash:      HashGrid 0..31     | pad_ 32 | OneBlob 33..56 | Identity 57..62 | 1.0 (63)
+ * i.e. the same widths (80 / 64) with one constant-one column fewer; W0's columns follow that order. */
+#define NRC_INPUT_DIMS_PADDED 16
+#define NRC_QUERY_COMPACT 0 /* USE_COMPACT_RADIANCE_QUERY 1 (config.h:113): 15 floats */
+#define NRC_QUERY_PADDED  1 /* USE_COMPACT_RADIANCE_QUERY 0: 16 floats */
+typedef struct nrc_radiance_query_padded {
+    float position[3];
+    float pad_;
+    float direction[2];
+    float normal[2];
+    float roughness[2];
+    float diffuse[3];
+    float specular[3];
+} nrc_radiance_query_padded;
+
 /* Radiance outputs and training targets: packed float3, 12 bytes (neural_radiance_caching.h:144, :175). */
 typedef struct nrc_float3 { float x, y, z; } nrc_float3;
 

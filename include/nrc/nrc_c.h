@@ -7,7 +7,8 @@
  * message of the last failure on the calling thread is available from nrc_last_error().
  *
  * Buffers are the reference's, byte for byte (include/nrc/layout.h): queries are packed 60-byte
- * RadianceQuery records (15 f32, 4-byte aligned), outputs and targets packed 12-byte float3.
+ * RadianceQuery records (15 f32, 4-byte aligned; 64-byte records of 16 f32 with nrc_config.query_layout =
+ * NRC_QUERY_PADDED, the reference's USE_COMPACT_RADIANCE_QUERY 0), outputs and targets packed 12-byte float3.
  * All work is enqueued on a HIP stream and is asynchronous unless a host loss pointer is given
  * (that call blocks, as NRCNetwork.cu:54-55 does). A handle is not thread-safe.
  */
@@ -50,6 +51,12 @@ typedef struct nrc_config {
     uint32_t width;           /* MLP neurons: 64 (reference) or 128 (NRC_WIDE_*; Frequency / FrequencySH only) */
     uint32_t infer_precision; /* nrc_precision of infer(): F16 (default), F16_ACC16 (tcnn's f16 accumulation, width 64
                                * Frequency only) or FP8 (width 128 only) */
+    /* RadianceQuery layout of every query buffer of the handle (the reference's compile-time
+     * USE_COMPACT_RADIANCE_QUERY, config.h:113): NRC_QUERY_COMPACT (default, 15 f32) or NRC_QUERY_PADDED (16 f32 with
+     * pad_ and its Identity(1) feature, layout.h). Padded: width 64, Frequency or Hash, infer_precision F16; the
+     * parameter blob of nrc_get_state / nrc_set_state is in that encoding's column order (layout.h), while the
+     * data-parallel gradient buffer (nrc_train_grad / nrc_train_apply) is in the handle's internal order. */
+    uint32_t query_layout;
 } nrc_config;
 
 /* Arithmetic of infer() (nrc_config.infer_precision). F16: f16 operands, f32 accumulation per layer (the fast path).

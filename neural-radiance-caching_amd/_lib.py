@@ -27,6 +27,8 @@ FIXED_MAX_RANKS = 63                                 # NRC_FIXED_MAX_RANKS
 WIDE_NUM_PARAMS = 77824  # width-128 network (BASELINE configs[4])
 PRECISION_F16, PRECISION_FP8, PRECISION_F16_ACC16 = 0, 1, 2  # nrc_precision (nrc_c.h)
 BATCH_SIZE = 16384
+# nrc_config.query_layout (layout.h): compact 15-float RadianceQuery, padded 16-float (USE_COMPACT_RADIANCE_QUERY 0)
+QUERY_COMPACT, QUERY_PADDED = 0, 1
 INPUT_DIMS = 15
 OUTPUT_DIMS = 3
 
@@ -51,6 +53,8 @@ EXPORTS = [
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_accumulate_render_radiance_factored", "nrc_copy_radiance_to_output_factored", "nrc_propagate_train_radiance_factored",
+    "nrc_accumulate_render_radiance_factored_padded", "nrc_copy_radiance_to_output_factored_padded",
+    "nrc_propagate_train_radiance_factored_padded", "nrc_permute_train_data_padded",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
     # include/nrc/stream.h (bound in stream.py)
     "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_open", "nrc_stream_close",
@@ -62,7 +66,7 @@ class NrcConfig(ctypes.Structure):
     _fields_ = [("learning_rate", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
                 ("epsilon", ctypes.c_float), ("l2_reg", ctypes.c_float), ("ema_decay", ctypes.c_float),
                 ("loss_scale", ctypes.c_float), ("seed", ctypes.c_uint64), ("width", ctypes.c_uint32),
-                ("infer_precision", ctypes.c_uint32)]
+                ("infer_precision", ctypes.c_uint32), ("query_layout", ctypes.c_uint32)]
 
 
 class NrcHyperParams(ctypes.Structure):

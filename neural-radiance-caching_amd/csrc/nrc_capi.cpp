@@ -1,5 +1,6 @@
 // nrc_capi.cpp — C-ABI implementation (include/nrc/nrc_c.h). Owns parameters, optimizer state,
 // MFMA weight images and workspaces (the reference's tcnn::TrainableModel, NRCNetwork.cu:15-20).
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -234,9 +235,9 @@ std::vector<int> build_t16_slab_map() {
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
 bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
-                                            "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p"};
+                                            "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path"};
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -278,6 +279,12 @@ std::string config_json(int encoding, const nrc_config& c) {
         const std::string k = "\"n_neurons\":64";
         const size_t at = r.find(k);
         if (at != std::string::npos) r.replace(at, k.size(), "\"n_neurons\":" + std::to_string(c.width));
+    }
+    if (c.query_layout == NRC_QUERY_PADDED) {
+        // USE_COMPACT_RADIANCE_QUERY 0: Identity(1) of pad_ after the position encoding (NRCNetworkConfigs.h:61-67, :106-111)
+        const std::string k = "{\"n_bins\":4";
+        const size_t at = r.find(k);
+        if (at != std::string::npos) r.insert(at, "{\"n_dims_to_encode\":1,\"otype\":\"Identity\"},");
     }
     return r;
 }
@@ -413,6 +420,7 @@ struct nrc_net {
 
     bool hash() const { return encoding == NRC_ENCODING_HASH; }
     bool wide() const { return cfg.width == NRC_WIDE_WIDTH; }
+    bool padq() const { return cfg.query_layout == NRC_QUERY_PADDED; }
     size_t n_total() const { return (size_t)n_mlp + (size_t)n_grid; }
     size_t grad_floats() const { return n_total() + 4; }
 
@@ -597,14 +605,16 @@ int train_block_count(const nrc_net* net, uint32_t b) {
 void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total,
                     uint64_t* stamps = nullptr) {
     net->check_protocol();  // an earlier step's kernel (completed by now or not) may have reported a timeout
+    if (net->padq() && (!net->t16 || net->t16_kernel == 2 || stamps))
+        throw ApiError(NRC_ERR_UNSUPPORTED, "padded queries: the production training kernels only (knobs at default, no stamps)");
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0)
         HIP_CHECK(launch_train_dc(dc_shape(b), in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                   reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, net->proto_err_dev(),
-                                  net->stream, stamps));
+                                  net->stream, stamps, net->padq()));
     else if (net->t16)
         HIP_CHECK(launch_train16(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                  reinterpret_cast<_Float16*>(net->slabs), net->loss_partials, stamps, net->stream,
-                                 net->t16_kernel != 2, t16_groups()));
+                                 net->t16_kernel != 2, t16_groups(), net->padq()));
     else if (stamps)
         HIP_CHECK(launch_train_stamped(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                        net->slabs, net->loss_partials, stamps, net->stream));
@@ -633,7 +643,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     if (net->hash())
         HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                     net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                    net->step_scatter(blocks)));
+                                    net->step_scatter(blocks), net->padq()));
     else
         train_partials(net, in, tgt, b, 3.0f * (float)b);
     net->step += 1;
@@ -659,8 +669,9 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
     if (net->hash()) {
         uint32_t* const feat = net->hash_feat_arg();
         if (feat) net->hash_feat_acquire(net->stream);
+        if (net->padq() && !feat) throw ApiError(NRC_ERR_UNSUPPORTED, "padded queries: the feature-pass Hash inference only");
         const hipError_t e = launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f,
-                                               net->stream, feat);
+                                               net->stream, feat, net->padq());
         if (e == hipSuccess && feat) net->hash_feat_release(net->stream);
         return e;
     }
@@ -668,12 +679,36 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
         return launch_infer_sh(in, out, n, net->wf_infer, nullptr, nullptr, 0, -1, 1.0f, net->stream);
     if (net->cfg.infer_precision == NRC_PRECISION_F16_ACC16)
         return launch_infer_tcnn(in, out, n, net->wf_infer, net->infer, net->stream);
-    return launch_infer(in, out, n, net->wf_infer, net->stream, net->work_queue, &net->pool_parity);
+    return launch_infer(in, out, n, net->wf_infer, net->stream, net->work_queue, &net->pool_parity, net->padq());
 }
 
 void require_frequency(const nrc_net* net, const char* what) {
     if (net->encoding != NRC_ENCODING_FREQUENCY)
         throw ApiError(NRC_ERR_UNSUPPORTED, std::string(what) + " is implemented for InputEncoding::Frequency only");
+}
+
+// Padded RadianceQuery layout (nrc_config.query_layout = NRC_QUERY_PADDED): the handle computes in the compact
+// encoding's column order with the first constant-one column (Frequency 66, Hash 62) carrying pad_; the API blob
+// follows the reference's padded encoding (layout.h), where pad_'s Identity column sits right after the position
+// encoding (Frequency 36, Hash 32) and the columns up to the first one-column shift by one. to_api: internal -> API
+// order of W0's columns in place (else API -> internal); the other layers and the grid are the same in both.
+int padq_api_column(int encoding, int c) {
+    const int R = encoding == NRC_ENCODING_HASH ? 32 : 36;  // real columns before pad_
+    const int E = encoding == NRC_ENCODING_HASH ? 62 : 66;  // internal column carrying pad_
+    return c < R ? c : c < E ? c + 1 : c == E ? R : c;
+}
+void padq_w0_columns(int encoding, float* blob, bool to_api) {
+    const int in = encoding == NRC_ENCODING_HASH ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH;
+    std::vector<float> row(in);
+    for (int o = 0; o < NRC_WIDTH; ++o) {
+        float* w = blob + (size_t)o * in;
+        for (int c = 0; c < in; ++c) {
+            const int a = padq_api_column(encoding, c);
+            if (to_api) row[a] = w[c];
+            else row[c] = w[a];
+        }
+        std::copy(row.begin(), row.end(), w);
+    }
 }
 
 float* slot_ptr(nrc_net* net, int slot) {
@@ -711,6 +746,11 @@ bool nrc_amd::net_comm(nrc_net* net, int* rank, int* world) {
     return net->comm != nullptr;
 }
 
+bool nrc_amd::net_padq(nrc_net* net) {
+    check_live(net);
+    return net->padq();
+}
+
 nrc_loss_slots nrc_amd::net_loss_slots(nrc_net* net) {
     check_live(net);
     return {net->loss_dev, net->loss_host};
@@ -731,6 +771,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobHashFeatAbl: return v >= -1 && v <= 36;
         case kKnobT16Groups: return v == -1 || v == 1 || v == 2;
         case kKnobHashFeatP: return v == -1 || (v >= 8 && v <= 256 && v % 8 == 0);
+        case kKnobPeerPath: return v >= -1 && v <= 1;
         default: return false;
     }
 }
@@ -783,6 +824,7 @@ nrc_config nrc_default_config(int encoding) {
     c.seed = 1337;
     c.width = NRC_WIDTH;
     c.infer_precision = NRC_PRECISION_F16;
+    c.query_layout = NRC_QUERY_COMPACT;
     return c;
 }
 
@@ -821,6 +863,12 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             throw ApiError(NRC_ERR_UNSUPPORTED, "FP8 inference is implemented for the width-128 network only");
         if (c.width == NRC_WIDE_WIDTH && encoding == NRC_ENCODING_HASH)
             throw ApiError(NRC_ERR_UNSUPPORTED, "the width-128 network supports the Frequency / FrequencySH encodings");
+        if (c.query_layout != NRC_QUERY_COMPACT && c.query_layout != NRC_QUERY_PADDED)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown query_layout");
+        if (c.query_layout == NRC_QUERY_PADDED &&
+            (c.width != NRC_WIDTH || encoding == NRC_ENCODING_FREQUENCY_SH || c.infer_precision != NRC_PRECISION_F16))
+            throw ApiError(NRC_ERR_UNSUPPORTED, "padded RadianceQuery records (USE_COMPACT_RADIANCE_QUERY 0): the width-64 "
+                                                "Frequency / Hash networks with F16 inference");
         net->release();
         net->stream = stream;
         net->encoding = encoding;
@@ -1001,9 +1049,11 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
                                  rgba, num_pixels, mode, w, net->stream));
         else if (net->hash()) {
             uint32_t* const feat = net->hash_feat_arg();
+            if (net->padq() && !feat)
+                throw ApiError(NRC_ERR_UNSUPPORTED, "padded queries: the feature-pass Hash inference only");
             if (feat) net->hash_feat_acquire(net->stream);
             HIP_CHECK(launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, reinterpret_cast<const float*>(thr),
-                                        rgba, num_pixels, mode, w, net->stream, feat));
+                                        rgba, num_pixels, mode, w, net->stream, feat, net->padq()));
             if (feat) net->hash_feat_release(net->stream);
         }
         else if (net->encoding == NRC_ENCODING_FREQUENCY_SH)
@@ -1011,7 +1061,7 @@ nrc_status nrc_infer_accumulate(nrc_net* net, const float* in, float* out, uint3
                                       mode, w, net->stream));
         else
             HIP_CHECK(launch_infer_accumulate(in, out, n, net->wf_infer, reinterpret_cast<const float*>(thr), rgba,
-                                              num_pixels, mode, w, net->stream));
+                                              num_pixels, mode, w, net->stream, net->padq()));
     });
 }
 
@@ -1150,15 +1200,41 @@ void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_loc
         throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm / nrc_peer_exchange_open)");
     if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
     if (net->px_open) {
-        // one-shot peer exchange: local gradient -> every peer's receive slot (push) -> wait + rank-order sum + Adam/EMA
-        do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad);
         net->px_seq = net->px_seq + 1u ? net->px_seq + 1u : 1u;
         const int nfl = (int)net->grad_floats();
-        HIP_CHECK(launch_peer_push(net->dp_grad, nfl, net->px_peers, net->px_rank, net->px_world, net->px_seq,
-                                   net->stream));
-        net->step += 1;
-        HIP_CHECK(launch_peer_apply(net->px_buf, net->px_world, nfl, net->px_seq, net->proto_err_dev(),
-                                    loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
+        if (knob(kKnobPeerPath) != 0) {
+            // the exchange fused into the reduction: gradient pass -> one launch that reduces the slabs, pushes each
+            // block's partials to every rank, waits for the same block of every rank, sums in rank order, Adam/EMA
+            if (global_b < b_local || global_b == 0)
+                throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
+            int blocks = 1;
+            if (b_local > 0) {
+                if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
+                blocks = train_block_count(net, b_local);
+                net->ensure_slabs(blocks);
+                train_partials(net, in, tgt, b_local, 3.0f * (float)global_b);
+            } else {  // no local samples: one zero slab and a zero loss partial (the rank still takes part)
+                net->ensure_slabs(1);
+                const ModelBuffers mb = net->buffers();
+                HIP_CHECK(hipMemsetAsync(net->slabs, 0, (mb.slab_f16 ? 2 : 4) * (size_t)mb.n_slab, net->stream));
+                HIP_CHECK(hipMemsetAsync(net->loss_partials, 0, sizeof(float), net->stream));
+            }
+            net->step += 1;
+            HIP_CHECK(launch_reduce_exchange(net->slabs, blocks, net->loss_partials, net->px_peers, net->px_rank,
+                                             net->px_world, nfl, net->px_seq, net->proto_err_dev(),
+                                             loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step),
+                                             net->stream));
+        } else {
+            // round 4's first version (knob peer_path = 0; world >= 2): reduce to a gradient -> push the gradient to
+            // every peer's receive slot -> wait + rank-order sum + Adam/EMA
+            do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad);
+            HIP_CHECK(launch_peer_push(net->dp_grad, nfl, net->px_peers, net->px_rank, net->px_world, net->px_seq,
+                                       net->stream));
+            net->step += 1;
+            HIP_CHECK(launch_peer_apply(net->px_buf, net->px_world, nfl, net->px_seq, net->proto_err_dev(),
+                                        loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step),
+                                        net->stream));
+        }
         if (loss_h) {
             if (loss_d) {
                 HIP_CHECK(hipStreamSynchronize(net->stream));
@@ -1223,7 +1299,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
             // (unless grid_fixed is the buffer itself)
             HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
                                         net->wb_train, net->table_train, net->grid_grad, net->slabs, net->loss_partials,
-                                        net->stream, net->step_scatter(blocks)));
+                                        net->stream, net->step_scatter(blocks), net->padq()));
             if (grid_fixed)
                 HIP_CHECK(launch_grid_grad_export_fixed(net->grid_grad, grid_fixed, net->n_grid, net->nonfinite(),
                                                         net->stream));
@@ -1330,10 +1406,10 @@ nrc_status nrc_peer_exchange_handle(nrc_net* net, int world, void* handle_out) {
         if (net->hash() || net->wide())
             throw ApiError(NRC_ERR_UNSUPPORTED, "the peer exchange is implemented for the width-64 Frequency / FrequencySH "
                                                 "networks (Hash and width 128 use the RCCL path)");
-        if (world < 2 || world > kPeerMaxRanks) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "world must be 2..16");
+        if (world < 1 || world > kPeerMaxRanks) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "world must be 1..16");
         static_assert(sizeof(hipIpcMemHandle_t) == NRC_PEER_HANDLE_BYTES, "IPC handle size");
         net->peer_close();
-        const size_t bytes = peer_buffer_bytes(world, (int)net->grad_floats());
+        const size_t bytes = peer_buffer_bytes(world, (int)net->grad_floats(), net->buffers().n_slab);
         // uncached device memory: the peers' xGMI stores and this GPU's loads meet in memory, not in a stale L2 line
         HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&net->px_buf), bytes, hipDeviceMallocUncached));
         HIP_CHECK(hipMemset(net->px_buf, 0, bytes));  // flags 0: before any peer can know the handle
@@ -1390,6 +1466,7 @@ nrc_status nrc_get_state(nrc_net* net, int slot, float* host_dst) {
         HIP_CHECK(hipStreamSynchronize(net->stream));
         net->check_protocol();
         HIP_CHECK(hipMemcpy(host_dst, src, sizeof(float) * net->n_total(), hipMemcpyDeviceToHost));
+        if (net->padq()) padq_w0_columns(net->encoding, host_dst, true);
     });
 }
 
@@ -1399,7 +1476,13 @@ nrc_status nrc_set_state(nrc_net* net, int slot, const float* host_src) {
         if (!host_src) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null source");
         float* dst = slot_ptr(net, slot);
         HIP_CHECK(hipStreamSynchronize(net->stream));
-        HIP_CHECK(hipMemcpy(dst, host_src, sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
+        if (net->padq()) {
+            std::vector<float> tmp(host_src, host_src + net->n_total());
+            padq_w0_columns(net->encoding, tmp.data(), false);
+            HIP_CHECK(hipMemcpy(dst, tmp.data(), sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
+        } else {
+            HIP_CHECK(hipMemcpy(dst, host_src, sizeof(float) * net->n_total(), hipMemcpyHostToDevice));
+        }
         if (slot == NRC_STATE_PARAMS || slot == NRC_STATE_INFER) {
             repack(net, net->stream);
             HIP_CHECK(hipStreamSynchronize(net->stream));

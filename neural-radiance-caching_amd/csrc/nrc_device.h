@@ -32,17 +32,22 @@ struct QLane {
     float x3;          // FrequencySH only: OneBlob input 6+2h
 };
 
+// PADQ: padded 16-float records (nrc_config.query_layout = NRC_QUERY_PADDED): pad_ at float 3 (into x3), the rest one
+// float further
+template <bool PADQ = false>
 __device__ __forceinline__ QLane load_q(const float* __restrict__ q, int64_t s, int h) {
-    const float* r = q + s * NRC_INPUT_DIMS;
+    constexpr int X = PADQ ? 1 : 0;
+    const float* r = q + s * (NRC_INPUT_DIMS + X);
     QLane Q;
     Q.p0 = r[0];
     Q.p1 = r[1];
     Q.p2 = r[2];
-    const float* rb = r + 3 + 3 * h;
+    Q.x3 = PADQ ? r[3] : 0.0f;
+    const float* rb = r + 3 + X + 3 * h;
     Q.b0 = rb[0];
     Q.b1 = rb[1];
     Q.b2 = rb[2];
-    const float* ri = r + 9 + 3 * h;
+    const float* ri = r + 9 + X + 3 * h;
     Q.i0 = ri[0];
     Q.i1 = ri[1];
     Q.i2 = ri[2];
@@ -67,10 +72,11 @@ __device__ __forceinline__ QLane load_q_sh(const float* __restrict__ q, int64_t 
     return Q;
 }
 
-template <int ENC>
+template <int ENC, bool PADQ = false>
 __device__ __forceinline__ QLane load_q_enc(const float* __restrict__ q, int64_t s, int h) {
+    static_assert(!(PADQ && ENC == 2), "FrequencySH has no padded layout");
     if constexpr (ENC == 2) return load_q_sh(q, s, h);
-    else return load_q(q, s, h);
+    else return load_q<PADQ>(q, s, h);
 }
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));

@@ -27,9 +27,11 @@ struct EndVertex {  // neural_radiance_caching.h:78-94
 };
 static_assert(sizeof(TrainRecord) == 28 && sizeof(EndVertex) == 16, "reference record sizes");
 
-// RadianceQuery::reflectance() = diffuse + specular (neural_radiance_caching.h:118; compact record: floats 9..11, 12..14)
+// RadianceQuery::reflectance() = diffuse + specular (neural_radiance_caching.h:118; compact record: floats 9..11, 12..14;
+// X = 1: padded 16-float record, one float further)
+template <int X = 0>
 __device__ __forceinline__ F3 reflectance(const float* __restrict__ q, uint32_t i) {
-    const float* r = q + (size_t)i * NRC_INPUT_DIMS;
+    const float* r = q + (size_t)i * (NRC_INPUT_DIMS + X) + X;
     return F3{r[9] + r[12], r[10] + r[13], r[11] + r[14]};
 }
 
@@ -37,7 +39,7 @@ __device__ __forceinline__ F3 reflectance(const float* __restrict__ q, uint32_t 
 // w = 1/(iterationIndex+1) comes from the host (correctly rounded).
 // RF: USE_REFLECTANCE_FACTORING 1 (nrc_helpers.cu:95-97, 111-113, 118-120; copy_radiance_to_output_buffer :66-68): the
 // radiance times the render query's reflectance, after the throughput product
-template <int MODE, bool RF = false>
+template <int MODE, bool RF = false, int X = 0>  // X = 1: padded RadianceQuery records
 __global__ __launch_bounds__(256) void accumulate_kernel(const F3* __restrict__ rad, const F3* __restrict__ thr,
                                                          float4* __restrict__ rgba, uint32_t n, float w,
                                                          const float* __restrict__ queries = nullptr) {
@@ -45,7 +47,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const F3* __restrict__ 
     if (i >= n) return;
     float4 o;
     F3 R = {1.0f, 1.0f, 1.0f};
-    if constexpr (RF && MODE != 5) R = reflectance(queries, i);
+    if constexpr (RF && MODE != 5) R = reflectance<X>(queries, i);
     if constexpr (MODE == 0) {  // Full: dst += (T * L) * w   (RF: ((T * L) * R) * w)
         const F3 L = rad[i], T = thr[i];
         o = rgba[i];
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256) void accumulate_kernel(const F3* __restrict__ 
 // RF: USE_REFLECTANCE_FACTORING 1 (nrc_helpers.cu:156-160, 191-204): the targets hold radiance / reflectance; the end
 // radiance is multiplied by the end query's reflectance, each record's target by its own query's before the update and
 // divided by it after (safeDiv: a zero component gives 0, nrc_helpers.cu:28-35); the chain carries the radiance itself.
-template <bool RF = false>
+template <bool RF = false, int X = 0>  // X = 1: padded RadianceQuery records
 __global__ __launch_bounds__(256) void propagate_kernel(const EndVertex* __restrict__ ends,
                                                         const F3* __restrict__ end_rad, uint32_t tiles,
                                                         const TrainRecord* __restrict__ rec, F3* targets,
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256) void propagate_kernel(const EndVertex* __restr
     const F3 er = end_rad[t];
     F3 last = {er.x * ev.mask, er.y * ev.mask, er.z * ev.mask};  // :154
     if constexpr (RF) {                                            // :159
-        const F3 R = reflectance(end_q, t);
+        const F3 R = reflectance<X>(end_q, t);
         last.x *= R.x;
         last.y *= R.y;
         last.z *= R.z;
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(256) void propagate_kernel(const EndVertex* __restr
         F3 v = targets[i];
         F3 R = {1.0f, 1.0f, 1.0f};
         if constexpr (RF) {  // :191-193 radianceTo = targetTo * refl
-            R = reflectance(train_q, (uint32_t)i);
+            R = reflectance<X>(train_q, (uint32_t)i);
             v.x *= R.x;
             v.y *= R.y;
             v.z *= R.z;
@@ -175,23 +177,25 @@ __global__ __launch_bounds__(256) void permutation_kernel(FeistelKey fk, int* __
     perm[d] = (int)feistel_perm(d, fk);
 }
 
-// permute_train_data (nrc_helpers.cu:226-249) as a dword copy: threads [0, 15 n) write the query array,
-// threads [15 n, 18 n) the target array, so every wave's stores are contiguous; each lane re-derives its
-// record's source index (a few dozen integer ops, cheaper than a second pass through HBM).
+// permute_train_data (nrc_helpers.cu:226-249) as a dword copy: threads [0, QW n) write the query array,
+// threads [QW n, (QW + 3) n) the target array, so every wave's stores are contiguous; each lane re-derives its
+// record's source index (a few dozen integer ops, cheaper than a second pass through HBM). QW: dwords per
+// RadianceQuery (15 compact, 16 padded).
+template <uint32_t QW = 15u>
 __global__ __launch_bounds__(256) void permute_kernel(const uint32_t* __restrict__ qs, const uint32_t* __restrict__ ts,
                                                       const int* __restrict__ perm, FeistelKey fk, uint32_t nrec,
                                                       uint32_t* __restrict__ qd, uint32_t* __restrict__ td) {
     const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t nq = fk.n * 15u;
+    const uint32_t nq = fk.n * QW;
     if (g >= nq + fk.n * 3u) return;
     const bool is_q = g < nq;
     const uint32_t gg = is_q ? g : g - nq;
-    const uint32_t d = is_q ? gg / 15u : gg / 3u;  // constant divisors: mul-hi, no integer division
-    const uint32_t k = gg - d * (is_q ? 15u : 3u);
+    const uint32_t d = is_q ? gg / QW : gg / 3u;  // constant divisors: mul-hi, no integer division
+    const uint32_t k = gg - d * (is_q ? QW : 3u);
     const uint32_t p = perm ? (uint32_t)perm[d] : feistel_perm(d, fk);
     const uint32_t s = p % nrec;  // :245 (a negative caller entry reads as unsigned: never out of bounds)
     if (is_q)
-        qd[gg] = qs[(size_t)s * 15u + k];
+        qd[gg] = qs[(size_t)s * QW + k];
     else
         td[gg] = ts[(size_t)s * 3u + k];
 }
@@ -221,12 +225,22 @@ inline dim3 grid_for(uint64_t threads) { return dim3((unsigned)((threads + 255) 
 }  // namespace
 
 hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,
-                             hipStream_t s, const float* queries) {
+                             hipStream_t s, const float* queries, bool padq) {
     if (n == 0) return hipSuccess;
     const F3* r = reinterpret_cast<const F3*>(rad);
     const F3* t = reinterpret_cast<const F3*>(thr);
     float4* o = reinterpret_cast<float4*>(rgba);
     const dim3 g = grid_for(n), b(256);
+    if (queries && padq) {  // USE_REFLECTANCE_FACTORING 1 over padded RadianceQuery records
+        switch (mode) {
+        case 0: hipLaunchKernelGGL((accumulate_kernel<0, true, 1>), g, b, 0, s, r, t, o, n, w, queries); break;
+        case 2: hipLaunchKernelGGL((accumulate_kernel<2, true, 1>), g, b, 0, s, r, t, o, n, w, queries); break;
+        case 4: hipLaunchKernelGGL((accumulate_kernel<4, true, 1>), g, b, 0, s, r, t, o, n, w, queries); break;
+        case 5: hipLaunchKernelGGL((accumulate_kernel<5, true, 1>), g, b, 0, s, r, t, o, n, w, queries); break;
+        default: return hipSuccess;
+        }
+        return hipGetLastError();
+    }
     if (queries) {  // USE_REFLECTANCE_FACTORING 1
         switch (mode) {
         case 0: hipLaunchKernelGGL((accumulate_kernel<0, true>), g, b, 0, s, r, t, o, n, w, queries); break;
@@ -249,10 +263,15 @@ hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, ui
 
 hipError_t launch_propagate(const void* ends, const float* end_rad, uint32_t tiles, const void* records,
                             float* targets, uint32_t nrec, hipStream_t s, const float* end_queries,
-                            const float* train_queries) {
+                            const float* train_queries, bool padq) {
     if (tiles == 0 || nrec == 0) return hipSuccess;
     if ((end_queries == nullptr) != (train_queries == nullptr)) return hipErrorInvalidValue;
-    if (end_queries)
+    if (end_queries && padq)
+        hipLaunchKernelGGL((propagate_kernel<true, 1>), grid_for(tiles), dim3(256), 0, s,
+                           reinterpret_cast<const EndVertex*>(ends), reinterpret_cast<const F3*>(end_rad), tiles,
+                           reinterpret_cast<const TrainRecord*>(records), reinterpret_cast<F3*>(targets), nrec,
+                           end_queries, train_queries);
+    else if (end_queries)
         hipLaunchKernelGGL(propagate_kernel<true>, grid_for(tiles), dim3(256), 0, s,
                            reinterpret_cast<const EndVertex*>(ends), reinterpret_cast<const F3*>(end_rad), tiles,
                            reinterpret_cast<const TrainRecord*>(records), reinterpret_cast<F3*>(targets), nrec,
@@ -272,12 +291,18 @@ hipError_t launch_permutation(uint64_t seed, uint32_t frame, int* perm, uint32_t
 }
 
 hipError_t launch_permute(const float* qs, const float* ts, const int* perm, uint64_t seed, uint32_t frame,
-                          uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s) {
+                          uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s, bool padq) {
     if (n_out == 0 || nrec == 0) return hipSuccess;
-    hipLaunchKernelGGL(permute_kernel, grid_for((uint64_t)n_out * 18u), dim3(256), 0, s,
-                       reinterpret_cast<const uint32_t*>(qs), reinterpret_cast<const uint32_t*>(ts), perm,
-                       make_key(seed, frame, n_out), nrec, reinterpret_cast<uint32_t*>(qd),
-                       reinterpret_cast<uint32_t*>(td));
+    if (padq)
+        hipLaunchKernelGGL(permute_kernel<16u>, grid_for((uint64_t)n_out * 19u), dim3(256), 0, s,
+                           reinterpret_cast<const uint32_t*>(qs), reinterpret_cast<const uint32_t*>(ts), perm,
+                           make_key(seed, frame, n_out), nrec, reinterpret_cast<uint32_t*>(qd),
+                           reinterpret_cast<uint32_t*>(td));
+    else
+        hipLaunchKernelGGL(permute_kernel<15u>, grid_for((uint64_t)n_out * 18u), dim3(256), 0, s,
+                           reinterpret_cast<const uint32_t*>(qs), reinterpret_cast<const uint32_t*>(ts), perm,
+                           make_key(seed, frame, n_out), nrec, reinterpret_cast<uint32_t*>(qd),
+                           reinterpret_cast<uint32_t*>(td));
     return hipGetLastError();
 }
 

@@ -48,9 +48,9 @@ nrc_status nrc_accumulate_render_radiance(const nrc_float3* rad, const nrc_float
     });
 }
 
-nrc_status nrc_accumulate_render_radiance_factored(const nrc_float3* rad, const float* queries, const nrc_float3* thr,
-                                                   float* rgba, uint32_t n, int mode, uint32_t iteration_index,
-                                                   hipStream_t stream) {
+namespace {
+nrc_status accumulate_factored(const nrc_float3* rad, const float* queries, const nrc_float3* thr, float* rgba,
+                               uint32_t n, int mode, uint32_t iteration_index, hipStream_t stream, bool padq) {
     return guarded([&] {
         require(valid_mode(mode), "unknown render mode");
         if (n == 0 || mode == NRC_RENDER_NO_CACHE || mode == NRC_RENDER_CACHE_FIRST_VERTEX) return;
@@ -61,14 +61,34 @@ nrc_status nrc_accumulate_render_radiance_factored(const nrc_float3* rad, const 
         // DebugThroughputOnly does not read the queries (nrc_helpers.cu:124-127): any non-NULL pointer selects RF
         static const float kNoQueries = 0.0f;
         HIP_CHECK(launch_accumulate(reinterpret_cast<const float*>(rad), reinterpret_cast<const float*>(thr), rgba, n,
-                                    mode, accumulation_weight(iteration_index), stream, queries ? queries : &kNoQueries));
+                                    mode, accumulation_weight(iteration_index), stream, queries ? queries : &kNoQueries,
+                                    padq));
     });
+}
+}  // namespace
+
+nrc_status nrc_accumulate_render_radiance_factored(const nrc_float3* rad, const float* queries, const nrc_float3* thr,
+                                                   float* rgba, uint32_t n, int mode, uint32_t iteration_index,
+                                                   hipStream_t stream) {
+    return accumulate_factored(rad, queries, thr, rgba, n, mode, iteration_index, stream, false);
+}
+
+nrc_status nrc_accumulate_render_radiance_factored_padded(const nrc_float3* rad, const float* queries,
+                                                          const nrc_float3* thr, float* rgba, uint32_t n, int mode,
+                                                          uint32_t iteration_index, hipStream_t stream) {
+    return accumulate_factored(rad, queries, thr, rgba, n, mode, iteration_index, stream, true);
 }
 
 nrc_status nrc_copy_radiance_to_output_factored(const nrc_float3* rad, const float* queries, float* rgba, uint32_t n,
                                                 hipStream_t stream) {
-    return nrc_accumulate_render_radiance_factored(rad, queries, nullptr, rgba, n,
-                                                   NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0, stream);
+    return accumulate_factored(rad, queries, nullptr, rgba, n, NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0,
+                               stream, false);
+}
+
+nrc_status nrc_copy_radiance_to_output_factored_padded(const nrc_float3* rad, const float* queries, float* rgba,
+                                                       uint32_t n, hipStream_t stream) {
+    return accumulate_factored(rad, queries, nullptr, rgba, n, NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0,
+                               stream, true);
 }
 
 nrc_status nrc_copy_radiance_to_output(const nrc_float3* rad, float* rgba, uint32_t n, hipStream_t stream) {
@@ -90,10 +110,11 @@ nrc_status nrc_propagate_train_radiance(const nrc_train_suffix_end_vertex* ends,
     });
 }
 
-nrc_status nrc_propagate_train_radiance_factored(const nrc_train_suffix_end_vertex* ends, const nrc_float3* end_rad,
-                                                 const float* end_queries, uint32_t tiles,
-                                                 const nrc_training_record* records, nrc_float3* targets,
-                                                 const float* train_queries, uint32_t nrec, hipStream_t stream) {
+namespace {
+nrc_status propagate_factored(const nrc_train_suffix_end_vertex* ends, const nrc_float3* end_rad,
+                              const float* end_queries, uint32_t tiles, const nrc_training_record* records,
+                              nrc_float3* targets, const float* train_queries, uint32_t nrec, hipStream_t stream,
+                              bool padq) {
     return guarded([&] {
         if (tiles == 0 || nrec == 0) return;
         require(ends && end_rad && records && targets && end_queries && train_queries, "NULL buffer");
@@ -102,8 +123,24 @@ nrc_status nrc_propagate_train_radiance_factored(const nrc_train_suffix_end_vert
                 "buffers must be 4-byte aligned");
         require(nrec <= (uint32_t)INT32_MAX, "num_records too large");
         HIP_CHECK(launch_propagate(ends, reinterpret_cast<const float*>(end_rad), tiles, records,
-                                   reinterpret_cast<float*>(targets), nrec, stream, end_queries, train_queries));
+                                   reinterpret_cast<float*>(targets), nrec, stream, end_queries, train_queries, padq));
     });
+}
+}  // namespace
+
+nrc_status nrc_propagate_train_radiance_factored(const nrc_train_suffix_end_vertex* ends, const nrc_float3* end_rad,
+                                                 const float* end_queries, uint32_t tiles,
+                                                 const nrc_training_record* records, nrc_float3* targets,
+                                                 const float* train_queries, uint32_t nrec, hipStream_t stream) {
+    return propagate_factored(ends, end_rad, end_queries, tiles, records, targets, train_queries, nrec, stream, false);
+}
+
+nrc_status nrc_propagate_train_radiance_factored_padded(const nrc_train_suffix_end_vertex* ends,
+                                                        const nrc_float3* end_rad, const float* end_queries,
+                                                        uint32_t tiles, const nrc_training_record* records,
+                                                        nrc_float3* targets, const float* train_queries, uint32_t nrec,
+                                                        hipStream_t stream) {
+    return propagate_factored(ends, end_rad, end_queries, tiles, records, targets, train_queries, nrec, stream, true);
 }
 
 nrc_status nrc_generate_train_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n,
@@ -116,9 +153,9 @@ nrc_status nrc_generate_train_permutation(uint64_t seed, uint32_t frame, int32_t
     });
 }
 
-nrc_status nrc_permute_train_data(const float* qs, const nrc_float3* ts, const int32_t* perm, uint64_t seed,
-                                  uint32_t frame, int32_t num_records, float* qd, nrc_float3* td, uint32_t n_out,
-                                  hipStream_t stream) {
+namespace {
+nrc_status permute_train(const float* qs, const nrc_float3* ts, const int32_t* perm, uint64_t seed, uint32_t frame,
+                         int32_t num_records, float* qd, nrc_float3* td, uint32_t n_out, hipStream_t stream, bool padq) {
     return guarded([&] {
         const uint32_t nrec = (uint32_t)std::min<int64_t>(num_records, (int64_t)n_out);  // nrc_helpers.cu:236
         if (num_records <= 0 || n_out == 0) return;                                      // :237
@@ -127,8 +164,21 @@ nrc_status nrc_permute_train_data(const float* qs, const nrc_float3* ts, const i
         require(aligned(qs, 4) && aligned(ts, 4) && aligned(qd, 4) && aligned(td, 4) && aligned(perm, 4),
                 "buffers must be 4-byte aligned");
         HIP_CHECK(launch_permute(qs, reinterpret_cast<const float*>(ts), perm, seed, frame, nrec, qd,
-                                 reinterpret_cast<float*>(td), n_out, stream));
+                                 reinterpret_cast<float*>(td), n_out, stream, padq));
     });
+}
+}  // namespace
+
+nrc_status nrc_permute_train_data(const float* qs, const nrc_float3* ts, const int32_t* perm, uint64_t seed,
+                                  uint32_t frame, int32_t num_records, float* qd, nrc_float3* td, uint32_t n_out,
+                                  hipStream_t stream) {
+    return permute_train(qs, ts, perm, seed, frame, num_records, qd, td, n_out, stream, false);
+}
+
+nrc_status nrc_permute_train_data_padded(const float* qs, const nrc_float3* ts, const int32_t* perm, uint64_t seed,
+                                         uint32_t frame, int32_t num_records, float* qd, nrc_float3* td,
+                                         uint32_t n_out, hipStream_t stream) {
+    return permute_train(qs, ts, perm, seed, frame, num_records, qd, td, n_out, stream, true);
 }
 
 namespace {
@@ -154,6 +204,8 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     require((uint64_t)screen + tiles <= UINT32_MAX, "screen_size + num_tiles overflows");
     const float* qi = fb->queries_inference_d;
     nrc_float3* ri = fb->results_inference_d;
+    const bool padq = net_padq(net);  // RadianceQuery records of the handle's layout (nrc_config.query_layout)
+    const size_t QD = padq ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS;
     // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion); with reflectance
     // factoring the separate (factored) accumulation kernel runs instead
     const bool rf = p->reflectance_factoring != 0;
@@ -163,7 +215,7 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     auto infer_range = [&](uint32_t first, uint32_t count, uint32_t acc_pixels) {
         // queries [first, first + count); the first acc_pixels of them are render queries of pixels first..
         if (count == 0) return;
-        const float* q = qi + (size_t)first * NRC_INPUT_DIMS;
+        const float* q = qi + (size_t)first * QD;
         float* r = reinterpret_cast<float*>(ri + first);
         if (fuse && acc_pixels > 0)
             check(nrc_infer_accumulate(net, q, r, count, fb->last_render_throughput_d + first,
@@ -180,10 +232,8 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     // Device::nrcAccumulateRadiance (Device.cpp:1310-1337)
     if (!skip_render && !fuse && npix > 0) {
         if (rf)
-            check(nrc_accumulate_render_radiance_factored(fb->results_inference_d + p0, qi + (size_t)p0 * NRC_INPUT_DIMS,
-                                                          fb->last_render_throughput_d + p0,
-                                                          fb->output_rgba_d + (size_t)p0 * 4, npix, mode,
-                                                          p->iteration_index, s));
+            check(accumulate_factored(fb->results_inference_d + p0, qi + (size_t)p0 * QD, fb->last_render_throughput_d + p0,
+                                      fb->output_rgba_d + (size_t)p0 * 4, npix, mode, p->iteration_index, s, padq));
         else
             check(nrc_accumulate_render_radiance(fb->results_inference_d + p0, fb->last_render_throughput_d + p0,
                                                  fb->output_rgba_d + (size_t)p0 * 4, npix, mode, p->iteration_index, s));
@@ -191,12 +241,12 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     // Device::nrcVisualizeFirstRadiance (Device.cpp:1339-1370)
     if (mode == NRC_RENDER_CACHE_FIRST_VERTEX && npix > 0) {
         require(fb->queries_cache_vis_d && fb->results_cache_vis_d, "cache-vis buffers are NULL");
-        check(nrc_infer_stream(net, fb->queries_cache_vis_d + (size_t)p0 * NRC_INPUT_DIMS,
+        check(nrc_infer_stream(net, fb->queries_cache_vis_d + (size_t)p0 * QD,
                                reinterpret_cast<float*>(fb->results_cache_vis_d + p0), npix, s));
         if (rf)
-            check(nrc_copy_radiance_to_output_factored(fb->results_cache_vis_d + p0,
-                                                       fb->queries_cache_vis_d + (size_t)p0 * NRC_INPUT_DIMS,
-                                                       fb->output_rgba_d + (size_t)p0 * 4, npix, s));
+            check(accumulate_factored(fb->results_cache_vis_d + p0, fb->queries_cache_vis_d + (size_t)p0 * QD, nullptr,
+                                      fb->output_rgba_d + (size_t)p0 * 4, npix,
+                                      NRC_RENDER_DEBUG_CACHE_NO_THROUGHPUT_MODULATION, 0, s, padq));
         else
             check(nrc_copy_radiance_to_output(fb->results_cache_vis_d + p0, fb->output_rgba_d + (size_t)p0 * 4, npix,
                                               s));
@@ -209,16 +259,16 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
             "training double buffers are NULL");
     // Device::nrcPropagateRadiance (Device.cpp:1382-1419): end radiance = results after the render part
     if (rf)  // the end queries are the inference queries after the render part; the records' are as traced
-        check(nrc_propagate_train_radiance_factored(fb->end_vertices_d, fb->results_inference_d + screen,
-                                                    qi + (size_t)screen * NRC_INPUT_DIMS, tiles, fb->train_records_d,
-                                                    fb->train_targets_d[0], fb->train_queries_d[0], (uint32_t)nrec, s));
+        check(propagate_factored(fb->end_vertices_d, fb->results_inference_d + screen, qi + (size_t)screen * QD, tiles,
+                                 fb->train_records_d, fb->train_targets_d[0], fb->train_queries_d[0], (uint32_t)nrec, s,
+                                 padq));
     else
         check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
                                            fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
     // Device::nrcShuffleTrainingData (Device.cpp:1427-1469)
-    check(nrc_permute_train_data(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d,
-                                 p->shuffle_seed, p->frame_index, nrec, fb->train_queries_d[1],
-                                 fb->train_targets_d[1], NRC_NUM_TRAINING_RECORDS_PER_FRAME, s));
+    check(permute_train(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d, p->shuffle_seed,
+                        p->frame_index, nrec, fb->train_queries_d[1], fb->train_targets_d[1],
+                        NRC_NUM_TRAINING_RECORDS_PER_FRAME, s, padq));
     // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss. The minibatch losses
     // land in host-mapped slots and are read after one sync at the end (the reference syncs after
     // every minibatch, Device.cpp:1504); summed in the same order, so the mean is the same float.
@@ -230,7 +280,7 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     const uint32_t s0 = rank * base + std::min<uint32_t>(rank, rem), sn = base + (rank < (int)rem ? 1 : 0);
     for (int b = 0; b < NRC_NUM_BATCHES; ++b) {
         const size_t first = (size_t)b * NRC_BATCH_SIZE + (dp ? s0 : 0);
-        const float* bq = fb->train_queries_d[1] + first * NRC_INPUT_DIMS;
+        const float* bq = fb->train_queries_d[1] + first * QD;
         const float* bt = reinterpret_cast<const float*>(fb->train_targets_d[1] + first);
         if (dp)
             net_train_dp_async(net, bq, bt, sn, NRC_BATCH_SIZE, slots.dev + b);

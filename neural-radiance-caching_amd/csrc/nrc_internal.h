@@ -211,7 +211,7 @@ hipError_t launch_fp8_convert(const float* x, uint8_t* y, int64_t n, int relu, h
 constexpr int kStealMaxBlocks = 1024, kStealStride = 16, kStealSetWords = kStealMaxBlocks * kStealStride;
 constexpr int kInferPoolBytes = 2 * 32 * 32 * 4 + 2 * kStealSetWords * 4;
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s,
-                        uint32_t* pools = nullptr, int* parity = nullptr);
+                        uint32_t* pools = nullptr, int* parity = nullptr, bool padq = false);
 // the product kernel is variant 47; the debug library (NRC_DEBUG_KERNELS) also has the A/B variants 0, 23, 30, 39 (round
 // 2's product: 47 with the 32x32x16 output layer), 40 (39 + in-kernel clock) and 48 (47 + in-kernel clock)
 constexpr int kProductInferVariant = 47;
@@ -224,14 +224,14 @@ hipError_t launch_infer16(const float* queries, float* out, int64_t n, const _Fl
 hipError_t read_infer_clock(uint64_t* host, int64_t cap_waves, int64_t* waves);
 // inference with accumulate_render_radiance fused for queries [0, n_acc) (mode 0 Full / 2 CacheOnly)
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
-                                   float* rgba, int64_t n_acc, int mode, float w, hipStream_t s);
+                                   float* rgba, int64_t n_acc, int mode, float w, hipStream_t s, bool padq = false);
 // InputEncoding::Hash inference (mode -1: plain; 0 / 2: fused accumulation for queries [0, n_acc))
 // feat: the handle's [NRC_HASH_LEVELS][kHashFeatStride] level-feature workspace (hash_feature_kernel, round 3), or
 // nullptr for the round-2 gather kernel (also knob "hash_infer" = 1)
 constexpr int64_t kHashFeatStride = (int64_t)1 << 21;  // queries per feature pass (128 MiB of features)
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
                              const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s,
-                             uint32_t* feat = nullptr);
+                             uint32_t* feat = nullptr, bool padq = false);
 hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float* enc, int64_t n, hipStream_t s);
 // FrequencySH extension
 hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
@@ -263,7 +263,8 @@ struct PeerPtrs {
     float* p[kPeerMaxRanks];
 };
 int peer_stride(int nfl);
-size_t peer_buffer_bytes(int world, int nfl);
+// the receive buffer: the push/apply region (nfl floats per slot) and the fused exchange's region (slab order, n_slab)
+size_t peer_buffer_bytes(int world, int nfl, int n_slab);
 struct OptimArgs {
     float lr, beta1, beta2, eps, l2_reg, ema_decay, loss_scale;
     uint32_t step;
@@ -298,7 +299,7 @@ struct ModelBuffers {
 // slabs: f16 (nrc_train16.hip slab_pair), reduced by launch_reduce_adam (ModelBuffers::slab_f16)
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s, bool split = false, int groups = 2);
+                          hipStream_t s, bool split = false, int groups = 2, bool padq = false);
 // samples per block of the role-split t16 kernel: 64 x groups (knob "t16_groups"; 128 by default)
 int t16_groups();  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16
@@ -308,7 +309,7 @@ int dc_samples_per_block(int shape);
 // err (required): set to 1 by a wave whose bounded LDS-protocol wait ran out (the step's slabs are then invalid)
 hipError_t launch_train_dc(int shape, const float* queries, const float* targets, int64_t b, float n_total,
                            float loss_scale, const _Float16* wf, const _Float16* wb, _Float16* slabs,
-                           float* loss_partials, uint32_t* err, hipStream_t s, uint64_t* stamps = nullptr);
+                           float* loss_partials, uint32_t* err, hipStream_t s, uint64_t* stamps = nullptr, bool padq = false);
 int dc_waves_per_block(int shape);
 // the production shape for a batch of b samples
 int dc_auto_shape(int64_t b);
@@ -325,7 +326,9 @@ enum Knob : int {
     kKnobHashFeatAbl = 6,  // debug library: hash_feature_kernel ablation (1 no gathers, 2 no position loads, 4 no stores)
     kKnobT16Groups = 7,    // role-split t16 training kernel: 16-sample groups per chain wave (1: 64-sample blocks; -1 = 2)
     kKnobHashFeatP = 8,    // Hash feature pass: query ranges per level (multiple of 8; -1 = 16 above 2^19 queries, else 8)
-    kKnobCount = 9
+    kKnobPeerPath = 9,     // nrc_train_dp over the peer exchange: -1 / 1 the exchange fused into the reduction, 0 the
+                           // reduce + push + apply launches (round 4's first version)
+    kKnobCount = 10
 };
 int knob(Knob k);
 
@@ -382,7 +385,7 @@ hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, con
                                 int64_t* waves, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
-                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr);
+                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);
@@ -390,6 +393,10 @@ hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int
                             hipStream_t s);
 hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
                              const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s);
+// reduce + peer exchange + rank-order sum + Adam/EMA in one launch after the gradient pass (world 1..16)
+hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
+                                  int rank, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
+                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s);
 
 // ---- per-handle scratch used by the frame driver (nrc_capi.cpp): NRC_NUM_BATCHES loss slots on the device and a
 // pinned host mirror
@@ -403,6 +410,8 @@ namespace nrc_amd {
 nrc_loss_slots net_loss_slots(nrc_net* net);
 // the attached communicator (nrc_set_comm): false if none; rank / world of it
 bool net_comm(nrc_net* net, int* rank, int* world);
+// the handle's RadianceQuery records are padded (nrc_config.query_layout = NRC_QUERY_PADDED)
+bool net_padq(nrc_net* net);
 // nrc_train_dp with the loss left in a device slot (frame driver)
 void net_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
                         float* loss_d);
@@ -410,12 +419,12 @@ void net_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_
 // ---- per-frame kernels around the network (nrc_frame.hip, include/nrc/frame.h)
 // queries / end_queries + train_queries (RadianceQuery arrays, NULL = off): USE_REFLECTANCE_FACTORING 1
 hipError_t launch_accumulate(const float* rad, const float* thr, float* rgba, uint32_t n, int mode, float w,
-                             hipStream_t s, const float* queries = nullptr);
+                             hipStream_t s, const float* queries = nullptr, bool padq = false);
 hipError_t launch_propagate(const void* ends, const float* end_rad, uint32_t tiles, const void* records,
                             float* targets, uint32_t nrec, hipStream_t s, const float* end_queries = nullptr,
-                            const float* train_queries = nullptr);
+                            const float* train_queries = nullptr, bool padq = false);
 hipError_t launch_permutation(uint64_t seed, uint32_t frame, int* perm, uint32_t n, hipStream_t s);
 hipError_t launch_permute(const float* qs, const float* ts, const int* perm, uint64_t seed, uint32_t frame,
-                          uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s);
+                          uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s, bool padq = false);
 
 }  // namespace nrc_amd

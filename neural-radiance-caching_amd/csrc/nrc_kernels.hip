@@ -321,6 +321,9 @@ __device__ __forceinline__ void encode_fast(const QLane& Q, int h, h8 (&x)[5]) {
 // raw angles (theta in [0, pi], phi in (-pi, pi]) to OneBlob, so Cornell waves always take the wrap: this replaces
 // blob_many's wave-uniform branch (~25 extra VALU per input on the wrap side) by ~6 VALU per input on one path.
 // ------------------------------------------------------------------------------------------------
+// PADQ (padded RadianceQuery, nrc_config.query_layout): slot 33 of lane half 0 -- the first constant-one column,
+// canonical feature 66 -- carries the query's pad_ (Q.x3) instead: the reference's Identity(1) of pad_ (layout.h)
+template <bool PADQ = false>
 __device__ __forceinline__ void encode_v3(const QLane& Q, int h, h8 (&x)[5]) {
     uint32_t w[20];
     const float hs = h ? 64.0f : 1.0f;  // octaves 6..11 for the upper half
@@ -338,7 +341,7 @@ __device__ __forceinline__ void encode_v3(const QLane& Q, int h, h8 (&x)[5]) {
     blob_v3(Q.b1, w[11], w[12]);
     blob_v3(Q.b2, w[13], w[14]);
     w[15] = pk2(Q.i0, Q.i1);
-    w[16] = pk2(Q.i2, 1.0f);
+    w[16] = pk2(Q.i2, PADQ && h == 0 ? Q.x3 : 1.0f);
     w[17] = w[18] = w[19] = 0x3C003C00u;  // pad features = 1.0
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk) {
@@ -366,20 +369,37 @@ __device__ uint64_t g_infer_clock[6 * kInferClockWavesMax];
 struct QOffsets {
     int p, b, i;
 };
+// PADQ (padded 64-B records, vo from q_offsets<true>): the position and pad_ as one 16-byte load, pad_ in Q.x3.
+template <bool PADQ = false>
 __device__ __forceinline__ QLane load_q_tile(const float* __restrict__ q, int64_t n, int64_t tile, const QOffsets& vo) {
     typedef float f3 __attribute__((ext_vector_type(3)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int kQD = PADQ ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS;
     const int64_t s0 = tile * 32;
-    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(q + s0 * NRC_INPUT_DIMS, tile_rows(n, s0) * (NRC_INPUT_DIMS * 4));
+    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(q + s0 * kQD, tile_rows(n, s0) * (kQD * 4));
     // whole-vector bit_casts (clang 22 element bit_cast bug, see infer_v2_body)
-    const f3 a = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.p, 0, 0));
+    QLane Q;
+    if constexpr (PADQ) {
+        const f4 a = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo.p, 0, 0));
+        Q.p0 = a.x; Q.p1 = a.y; Q.p2 = a.z;
+        Q.x3 = a.w;
+    } else {
+        const f3 a = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.p, 0, 0));
+        Q.p0 = a.x; Q.p1 = a.y; Q.p2 = a.z;
+        Q.x3 = 0.0f;
+    }
     const f3 b = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.b, 0, 0));
     const f3 c = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rs, vo.i, 0, 0));
-    QLane Q;
-    Q.p0 = a.x; Q.p1 = a.y; Q.p2 = a.z;
     Q.b0 = b.x; Q.b1 = b.y; Q.b2 = b.z;
     Q.i0 = c.x; Q.i1 = c.y; Q.i2 = c.z;
-    Q.x3 = 0.0f;
     return Q;
+}
+// lane (r, h)'s byte offsets in a tile of records: position (+ pad_), OneBlob inputs 3+3h.., Identity inputs 9+3h..
+// (padded records: one float further each)
+template <bool PADQ>
+__device__ __forceinline__ QOffsets q_offsets(int r, int h) {
+    constexpr int R = PADQ ? 64 : 60, X = PADQ ? 4 : 0;
+    return QOffsets{r * R, r * R + 12 + X + 12 * h, r * R + 36 + X + 12 * h};
 }
 
 // element i (0..3) of a 16-byte load, by named components (see the bit_cast note in infer_v2_body)
@@ -471,6 +491,8 @@ __device__ __forceinline__ uint32_t hash_level_feature(float px, float py, float
 
 // 32 K slots of lane half h (see hash_slot_feature): 8 hash levels (16 features), 3 OneBlob dims, 3 identity,
 // one pad; as 4 B fragments.
+// PADQ: slot 31 of lane half 0 carries pad_ (Q.x3), as encode_hashf
+template <bool PADQ = false>
 __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_t* __restrict__ table, h8 (&x)[4]) {
     uint32_t w[16];
     // levels in two groups of 4 with a scheduling fence between them: the compiler otherwise hoists every
@@ -488,7 +510,7 @@ __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_
     blob_v3(Q.b1, w[10], w[11]);
     blob_v3(Q.b2, w[12], w[13]);
     w[14] = pk2(Q.i0, Q.i1);
-    w[15] = pk2(Q.i2, 1.0f);
+    w[15] = pk2(Q.i2, PADQ && h == 0 ? Q.x3 : 1.0f);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
@@ -498,7 +520,9 @@ __device__ __forceinline__ void encode_hash(const QLane& Q, int h, const uint32_
 }
 
 // encode_hash with the 8 level features of lane half h already computed (hash_feature_kernel): F[i] = level 8h + i
-__device__ __forceinline__ void encode_hashf(const QLane& Q, const uint32_t (&F)[8], h8 (&x)[4]) {
+// PADQ: slot 31 of lane half 0 (canonical feature 62, the first constant-one column) carries pad_ (Q.x3)
+template <bool PADQ = false>
+__device__ __forceinline__ void encode_hashf(const QLane& Q, const uint32_t (&F)[8], int h, h8 (&x)[4]) {
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = F[i];
@@ -508,7 +532,7 @@ __device__ __forceinline__ void encode_hashf(const QLane& Q, const uint32_t (&F)
     blob_v3(Q.b1, w[10], w[11]);
     blob_v3(Q.b2, w[12], w[13]);
     w[14] = pk2(Q.i0, Q.i1);
-    w[15] = pk2(Q.i2, 1.0f);
+    w[15] = pk2(Q.i2, PADQ && h == 0 ? Q.x3 : 1.0f);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
@@ -644,7 +668,8 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
     // i.e. for the store's acknowledgement, before the next iteration's prefetched position). All memory operations
     // stay compiler-visible: an inline-asm load that the compiler cannot see in flight lets it reuse the destination
     // registers before the data lands.
-    const __amdgpu_buffer_rsrc_t rq = buffer_rsrc(q + s0 * NRC_INPUT_DIMS, cnt * (NRC_INPUT_DIMS * 4));
+    constexpr int kQD = (ABL & 64) != 0 ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS;  // ABL 64: padded RadianceQuery
+    const __amdgpu_buffer_rsrc_t rq = buffer_rsrc(q + s0 * kQD, cnt * (kQD * 4));
     const __amdgpu_buffer_rsrc_t rf = buffer_rsrc(feat + (int64_t)level * kHashFeatStride + s0, cnt * 4);
     typedef float f3 __attribute__((ext_vector_type(3)));
     auto load_pos = [&](int k) -> f3 {
@@ -664,7 +689,7 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
             }
             return f3{c[0], c[1], c[2]};
         }
-        return __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rq, k * (NRC_INPUT_DIMS * 4), 0, 0));
+        return __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(rq, k * (kQD * 4), 0, 0));
     };
     // two queries per lane per step (i, i + 1024), their positions two steps ahead in two register sets used
     // alternately
@@ -1033,6 +1058,7 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
 // Options of the production kernels: 16 = omod doubling-chain triangle wave (variant 22), 32 = branch-free
 // prefetch and buffer load/store epilogue (variant 23).
 constexpr int kDefaultAbl = 48;
+constexpr int kAblPadQ = 1 << 20;  // padded RadianceQuery records (nrc_config.query_layout = NRC_QUERY_PADDED)
 
 // Optional epilogue: accumulate_render_radiance (nrc_helpers.cu:77-129) fused into inference for the render
 // queries [0, n_acc) (EPI = RenderMode Full 0 / CacheOnly 2); their radiance is consumed in registers and never
@@ -1233,7 +1259,10 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     QLane Q[TILES];
     // ABL & 8192 (ENC 0 / 3, TILES 1): queries through raw buffer loads (load_q_tile)
     constexpr bool kBufQ = (ABL & 8192) != 0 && (ENC == 0 || ENC == 3) && TILES == 1;
-    const QOffsets vo{r * 60, r * 60 + 12 + 12 * h, r * 60 + 36 + 12 * h};
+    // ABL kAblPadQ: padded RadianceQuery records (nrc_config.query_layout), through load_q_tile only
+    constexpr bool kPadQ = (ABL & kAblPadQ) != 0;
+    static_assert(!kPadQ || kBufQ, "padded queries: the buffer-load prefetch path");
+    const QOffsets vo = q_offsets<kPadQ>(r, h);
     // ENC 3: the lane's 8 level features of the tile's query (levels 8h .. 8h + 7), prefetched with the query, as raw
     // buffer loads: one 32-bit lane offset per tile and the level stride in the scalar offset (instead of 8 64-bit
     // addresses); rows past the workspace read 0, rows past n are never stored
@@ -1251,7 +1280,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     static_assert(ENC != 3 || TILES == 1, "ENC 3 prefetches one tile");
     load_f(g);
     if constexpr (kBufQ) {
-        Q[0] = load_q_tile(q, n, g, vo);
+        Q[0] = load_q_tile<kPadQ>(q, n, g, vo);
     } else {
 #pragma unroll
         for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((g * TILES + t) * 32 + r, last), h);
@@ -1317,7 +1346,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
             if constexpr (ENC == 1) {
                 encode_hash(Q[t], h, grid, x[t]);
             } else if constexpr (ENC == 3) {
-                encode_hashf(Q[t], F, x[t]);
+                encode_hashf<kPadQ>(Q[t], F, h, x[t]);
             } else if constexpr (ENC == 2) {
                 encode_sh<(ABL & 16) != 0>(Q[t], h, x[t]);
             } else if constexpr ((ABL & 1) != 0) {
@@ -1326,7 +1355,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
 #pragma unroll
                 for (int kk = 0; kk < 5; ++kk) x[t][kk] = __builtin_bit_cast(h8, (kk & 1) ? a : b);
             } else if constexpr ((ABL & 1024) != 0) {
-                encode_v3(Q[t], h, x[t]);
+                encode_v3<kPadQ>(Q[t], h, x[t]);
                 if constexpr ((ABL & 524288) != 0) {
                     // energy probe (timing only, wrong outputs): 12 of the 14 constant-one pad slots (34..39 of both
                     // halves) fed as zeros, i.e. what folding the pad weights into one bias slot per half would feed
@@ -1358,7 +1387,7 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         }
         load_f(ng);  // ENC 3 (after the encoder has consumed F)
         if constexpr (kBufQ) {
-            Q[0] = load_q_tile(q, n, ng, vo);
+            Q[0] = load_q_tile<kPadQ>(q, n, ng, vo);
         } else if constexpr ((ABL & 32) != 0) {
             // unconditional (clamped) prefetch: no branch around the loads, so the compiler's vmcnt bookkeeping
             // stays exact across the loop back-edge
@@ -1616,11 +1645,11 @@ __global__ __launch_bounds__(512, 2) void infer_hash_kernel(const float* __restr
 
 // InputEncoding::Hash inference from hash_feature_kernel's level features (round 3): variant 47's shape, queue and
 // 4x4x4 output layer (the gather kernel below takes the same output layer, so the two stay bitwise equal)
-template <int EPI>
+template <int EPI, int XABL = 0>
 __global__ __launch_bounds__(1024, 4) void infer_hashf_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                               int64_t n, const h8* __restrict__ wf, InferEpilogue epi,
                                                               const uint32_t* __restrict__ feat) {
-    infer_v2_body<1, 1024, false, 32 | 2048 | 8192 | 65536, EPI, 3>(q, out, n, wf, epi, feat);
+    infer_v2_body<1, 1024, false, 32 | 2048 | 8192 | 65536 | XABL, EPI, 3>(q, out, n, wf, epi, feat);
 }
 
 // FrequencySH extension inference (EPI -1 plain; 0 / 2 fused accumulation)
@@ -2216,7 +2245,8 @@ __device__ __forceinline__ void grid_atomic(h2v* __restrict__ grid_grad, uint32_
 // ENC 1 (InputEncoding::Hash): 64-wide layer 0, grid table `grid` (f16x2, training weights); the grid-feature
 // gradient W0^T delta_0 is scattered into grid_grad (f16x2 per entry) with packed-half atomics, as tcnn's
 // kernel_grid_backward does (half2 atomicAdd): one 4-byte atomic per corner for both features.
-template <bool STAMP, int ENC = 0>
+// PADQ: padded RadianceQuery records (Hash only in the product: nrc_config.query_layout = NRC_QUERY_PADDED)
+template <bool STAMP, int ENC = 0, bool PADQ = false>
 __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                        int64_t b, float n_total, float loss_scale,
                                                        const h8* __restrict__ wf, const h8* __restrict__ wb,
@@ -2256,7 +2286,7 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
     const int64_t s = (int64_t)blockIdx.x * kTrainSamplesPerBlock + sl;
     const bool valid = s < b;
     const int64_t sc = valid ? s : b - 1;
-    const QLane Q = load_q_enc<ENC>(q, sc, h);
+    const QLane Q = load_q_enc<ENC, PADQ>(q, sc, h);
     float tgt[3] = {0.f, 0.f, 0.f};
     if (h == 0) {
         tgt[0] = t[sc * 3 + 0];
@@ -2285,7 +2315,8 @@ __global__ __launch_bounds__(256, 1) void train_kernel(const float* __restrict__
         stamp();
     }
     h8 x[KK0];
-    if constexpr (ENC == 1) encode_hash(Q, h, grid, x);
+    static_assert(!PADQ || ENC == 1, "train_kernel: padded queries for the Hash encoding");
+    if constexpr (ENC == 1) encode_hash<PADQ>(Q, h, grid, x);
     else if constexpr (ENC == 2) encode_sh(Q, h, x);
     else encode_fast(Q, h, x);
     // pin the encoder here (the asm consumes x) and keep the image stores and their vmcnt waits behind it, so
@@ -3198,15 +3229,23 @@ hipError_t launch_infer_stamped(const float*, float*, int64_t, const _Float16*, 
 #endif
 
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s, uint32_t* pools,
-                        int* parity) {
+                        int* parity, bool padq) {
+    if (padq) {  // variant 47 over padded RadianceQuery records
+        if (n <= 0) return hipSuccess;
+        static int bpc = 0;
+        return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | kAblPadQ>, 1024,
+                                       bpc, (n + 31) / 32, queries, out, n, wf, s);
+    }
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, pools, parity);
 }
 
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
                              const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s,
-                             uint32_t* feat) {
+                             uint32_t* feat, bool padq) {
     if (n <= 0) return hipSuccess;
     if (mode != -1 && mode != 0 && mode != 2) return hipErrorInvalidValue;
+    if (padq && !feat) return hipErrorInvalidValue;  // padded queries: the feature-pass path only
+    const int qd = padq ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS;
     const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
     if (feat) {
         // round 3: per pass of <= kHashFeatStride queries, the LDS-table feature kernel, then the MLP kernel reading them
@@ -3218,7 +3257,7 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
             // queries in-process, 24 / 48 / 64 / 128 slower (profiles/r04_hash/ab_hash_feat_p*.json)
             const int kp = knob(kKnobHashFeatP);
             const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 32 : 8;
-            const float* qc0 = queries + c0 * NRC_INPUT_DIMS;
+            const float* qc0 = queries + c0 * qd;
 #if NRC_DEBUG_KERNELS
             const int fa = knob(kKnobHashFeatAbl);
             if (fa > 0) {
@@ -3234,16 +3273,23 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
                 hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
             } else
 #endif
-                hipLaunchKernelGGL(hash_feature_kernel<0>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+                if (padq) hipLaunchKernelGGL(hash_feature_kernel<64>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+                else hipLaunchKernelGGL(hash_feature_kernel<0>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
             const int64_t acc = std::min<int64_t>(std::max<int64_t>(n_acc - c0, 0), cnt);
             const InferEpilogue e{thr ? thr + c0 * 3 : nullptr, rgba ? reinterpret_cast<float4*>(rgba) + c0 : nullptr, acc, w};
-            const float* qc = queries + c0 * NRC_INPUT_DIMS;
+            const float* qc = queries + c0 * qd;
             float* oc = out ? out + c0 * NRC_OUTPUT_DIMS : nullptr;
             const int64_t nt = (cnt + 31) / 32;
             hipError_t err;
-            if (mode == -1) err = launch_persistent_infer(infer_hashf_kernel<-1>, 1024, bpf[0], nt, qc, oc, cnt, wf, s, e, (const uint32_t*)feat);
-            else if (mode == 0) err = launch_persistent_infer(infer_hashf_kernel<0>, 1024, bpf[1], nt, qc, oc, cnt, wf, s, e, (const uint32_t*)feat);
-            else err = launch_persistent_infer(infer_hashf_kernel<2>, 1024, bpf[2], nt, qc, oc, cnt, wf, s, e, (const uint32_t*)feat);
+            const uint32_t* fc = feat;
+            if (padq) {
+                static int bpp[3] = {};
+                if (mode == -1) err = launch_persistent_infer(infer_hashf_kernel<-1, kAblPadQ>, 1024, bpp[0], nt, qc, oc, cnt, wf, s, e, fc);
+                else if (mode == 0) err = launch_persistent_infer(infer_hashf_kernel<0, kAblPadQ>, 1024, bpp[1], nt, qc, oc, cnt, wf, s, e, fc);
+                else err = launch_persistent_infer(infer_hashf_kernel<2, kAblPadQ>, 1024, bpp[2], nt, qc, oc, cnt, wf, s, e, fc);
+            } else if (mode == -1) err = launch_persistent_infer(infer_hashf_kernel<-1>, 1024, bpf[0], nt, qc, oc, cnt, wf, s, e, fc);
+            else if (mode == 0) err = launch_persistent_infer(infer_hashf_kernel<0>, 1024, bpf[1], nt, qc, oc, cnt, wf, s, e, fc);
+            else err = launch_persistent_infer(infer_hashf_kernel<2>, 1024, bpf[2], nt, qc, oc, cnt, wf, s, e, fc);
             if (err != hipSuccess) return err;
         }
         return hipGetLastError();
@@ -3538,16 +3584,19 @@ hipError_t launch_encode_hash(const float* queries, const _Float16* grid, float*
 }
 
 hipError_t launch_infer_accumulate(const float* queries, float* out, int64_t n, const _Float16* wf, const float* thr,
-                                   float* rgba, int64_t n_acc, int mode, float w, hipStream_t s) {
+                                   float* rgba, int64_t n_acc, int mode, float w, hipStream_t s, bool padq) {
     if (n <= 0) return hipSuccess;
     const int64_t ntiles = (n + 31) / 32;
-    static int bpc[2] = {};
+    static int bpc[4] = {};
     const InferEpilogue epi{thr, reinterpret_cast<float4*>(rgba), n_acc, w};
     // one 1024-thread block per CU drawing tiles from an LDS work queue (round 2: 82.6 vs 86.7 us per 1080p frame for
     // the round-1 512-thread shape, bit-identical, profiles/r02_frame/; the round-1 shape was removed in round 3)
-    switch (mode) {
-        case 0: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, 2048 | 65536>, 1024, bpc[0], ntiles, queries, out, n, wf, s, epi);
-        case 2: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, 2048 | 65536>, 1024, bpc[1], ntiles, queries, out, n, wf, s, epi);
+    constexpr int X = 2048 | 65536, XP = X | kAblPadQ;
+    switch (mode + (padq ? 1 : 0)) {
+        case 0: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, X>, 1024, bpc[0], ntiles, queries, out, n, wf, s, epi);
+        case 2: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, X>, 1024, bpc[1], ntiles, queries, out, n, wf, s, epi);
+        case 1: return launch_persistent_infer(infer_accumulate_kernel<0, 1024, XP>, 1024, bpc[2], ntiles, queries, out, n, wf, s, epi);
+        case 3: return launch_persistent_infer(infer_accumulate_kernel<2, 1024, XP>, 1024, bpc[3], ntiles, queries, out, n, wf, s, epi);
         default: return hipErrorInvalidValue;
     }
 }
@@ -3842,16 +3891,21 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
 
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
-                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc) {
+                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc, bool padq) {
     if (b <= 0) return hipSuccess;
     const int blocks = train_blocks(b);
     const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
     if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap || !sc->nf.codes || !sc->nf.tag_dev || !sc->nf.tag)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((train_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
-                       loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
-                       reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
-                       bcap);
+    if (padq)
+        hipLaunchKernelGGL((train_kernel<false, 1, true>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
+                           loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
+                           reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy, bcap);
+    else
+        hipLaunchKernelGGL((train_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
+                           loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
+                           reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
+                           bcap);
     // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep of the exact 64-bit scatter,
     // profiles/r03_hash/scatter_plan_sweep.txt (round 1's f16 scatter: profiles/r01_hash/README.md)
     const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);
@@ -3912,10 +3966,6 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
 constexpr int kPeerFlagStride = 16;  // u32 per flag (64 B)
 constexpr int kPeerSplit = 4;        // push blocks (and flags) per destination: each copies a quarter of the gradient
 int peer_stride(int nfl) { return (nfl + 63) / 64 * 64; }
-size_t peer_buffer_bytes(int world, int nfl) {
-    return sizeof(float) * ((size_t)2 * world * peer_stride(nfl)) +
-           sizeof(uint32_t) * 2 * world * kPeerSplit * kPeerFlagStride;
-}
 
 __global__ __launch_bounds__(1024) void peer_push_kernel(const float* __restrict__ grad, int nfl, PeerPtrs dst, int rank,
                                                          int world, int stride, uint32_t seq) {
@@ -3992,6 +4042,168 @@ __global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict
     const int p = blockIdx.x * 256 + threadIdx.x;
     if (p >= mb.n_mlp) return;
     adam_pack_one(kApplyOnly, p, world_sum(p), mb, oa, lr_t, ema_debias);
+}
+
+// ------------------------------------------------------------------------------------------------
+// The exchange fused into the reduction (round 4): one launch after the gradient pass replaces reduce (kReduceOnly) +
+// peer_push_kernel + peer_apply_kernel. Block i of every rank reduces the same 64 slab positions (the slab map is the
+// same on every rank), so the exchange runs per block: wave 0 of block i stores its 64 reduced partials -- slab order,
+// one contiguous 256-B store per destination -- into slot [par][rank] of every rank's buffer, waits for those stores
+// (uncached memory: acknowledged = in memory), raises flag [par][i][rank] in each of them, then polls its own buffer's
+// flags [par][i][0..world) and sums the world's partials in rank order before the same Adam/EMA as kReduceFused.
+// A block waits only for the blocks of the same index on the other ranks, which store before they wait: no cycle,
+// whatever the residency. The Adam state is loaded with the slab loads, before the wait. Buffer layout after the
+// push/apply region's (peer_buffer_bytes): data [2][world][xstride] f32 (slab order, the loss at n_slab), flags
+// [2][nblk][kPeerMaxRanks] u32. The parity argument of the push/apply pair holds per block: a rank's step k kernel
+// starts after all its blocks of step k - 1 saw every peer's step k - 1 flags, which those peers raised after their
+// step k - 2 kernels (and reads) had ended.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ constexpr int px_stride(int n_slab) { return (n_slab + 1 + 63) / 64 * 64; }
+size_t px_region_offset(int world, int nfl) {
+    return sizeof(float) * ((size_t)2 * world * peer_stride(nfl)) + sizeof(uint32_t) * 2 * world * kPeerSplit * kPeerFlagStride;
+}
+size_t peer_buffer_bytes(int world, int nfl, int n_slab) {
+    const int nblk = n_slab / (kRedParams * kRedVec);
+    return px_region_offset(world, nfl) + sizeof(float) * (size_t)2 * world * px_stride(n_slab) +
+           sizeof(uint32_t) * (size_t)2 * nblk * kPeerMaxRanks;
+}
+
+template <bool H, int WMAX>
+__global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const float* __restrict__ slabs, int nslabs,
+                                                                      const float* __restrict__ loss_partials,
+                                                                      PeerPtrs dst, size_t region, int rank, int world,
+                                                                      uint32_t seq, uint32_t* err, float* loss_out,
+                                                                      ModelBuffers mb, OptimArgs oa, float lr_t,
+                                                                      float ema_debias) {
+#pragma clang fp contract(off)
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ f4 part[kRedGroups][kRedParams];
+    const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
+    const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;
+    const int par = (int)(seq & 1u), blk = blockIdx.x, nblk = gridDim.x;
+    const int xstride = px_stride(mb.n_slab);
+    float L = 0.0f;  // this rank's loss (block 0, wave 0)
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        L = lane_partial_sum(loss_partials, nslabs, threadIdx.x);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
+    }
+    // slab sums as reduce_adam_kernel's reduce modes (same loads, same float sums, Adam state prefetched)
+    const int mypos = blockIdx.x * kRedParams * kRedVec + (threadIdx.x & (kRedParams * kRedVec - 1));
+    int pp_raw;
+    if constexpr (H) pp_raw = t16_slab_param(mypos);
+    else pp_raw = mb.slab_param[mypos];
+    f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    auto ld = [&](int slab) -> f4 {
+        if constexpr (H) {
+            const h4 v = *(const h4*)((const _Float16*)slabs + (int64_t)slab * mb.n_slab + p0);
+            return f4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+        } else {
+            return *(const f4*)&slabs[(int64_t)slab * mb.n_slab + p0];
+        }
+    };
+    const int nmine = grp < nslabs ? (nslabs - grp + kRedGroups - 1) / kRedGroups : 0;
+    auto ldc = [&](int k) -> f4 { return ld(min(grp + k * kRedGroups, nslabs - 1)); };
+    const int pp = threadIdx.x < kRedParams * kRedVec ? pp_raw : -1;
+    AdamIn ain{};
+    if (pp >= 0) ain = adam_load(pp, mb);
+    f4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ldc(u);
+    asm volatile("" : "+v"(ain.fp), "+v"(ain.ft), "+v"(ain.bp));
+    for (int base = 0;;) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool in = base + u < nmine;
+            if (u & 1) a1 += in ? v[u] : f4{0.f, 0.f, 0.f, 0.f};
+            else a0 += in ? v[u] : f4{0.f, 0.f, 0.f, 0.f};
+        }
+        base += 8;
+        if (base >= nmine) break;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ldc(base + u);
+    }
+    part[grp][pl] = a0 + a1;
+    __syncthreads();
+    if (threadIdx.x >= kRedParams * kRedVec) return;
+    // wave 0 from here: one slab position per lane
+    const int lane = threadIdx.x, lp = lane / kRedVec, comp = lane % kRedVec;
+    float t8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][lp][comp] + part[2 * u + 1][lp][comp];
+    const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
+    // push: slot [par][rank] of every rank (own buffer included), then the loss (block 0)
+    for (int r = 0; r < world; ++r) {
+        float* const d = reinterpret_cast<float*>(reinterpret_cast<char*>(dst.p[r]) + region) +
+                         ((int64_t)par * world + rank) * xstride;
+        d[mypos] = g1;
+        if (blk == 0 && lane == 0) d[mb.n_slab] = L;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int64_t flag_base = (int64_t)2 * world * xstride;  // u32 index of flag [0][0][0] in the region
+    // (dst.p indexed by a wave-uniform rank: a per-lane index into the kernel-argument array would go through scratch)
+    for (int r = 0; r < world; ++r) {
+        uint32_t* const f = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dst.p[r]) + region) + flag_base +
+                            ((int64_t)par * nblk + blk) * kPeerMaxRanks + rank;
+        if (lane == 0) __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // wait for every rank's block blk (one flag per lane; lanes past the world re-read flag 0); wave-uniform, no store
+    const char* const own = reinterpret_cast<const char*>(dst.p[rank]) + region;
+    const uint32_t* const fw = reinterpret_cast<const uint32_t*>(own) + flag_base +
+                               ((int64_t)par * nblk + blk) * kPeerMaxRanks + (lane < world ? lane : 0);
+    int i = 0;
+    for (; i < (1 << 21); ++i) {
+        const bool ready = __hip_atomic_load(fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
+        if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;
+        if (i < 4096) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(127);
+    }
+    if (i == (1 << 21) && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the world sum in rank order (branch-free: a rank past the world re-reads rank 0 and is not added)
+    const float* const xb = reinterpret_cast<const float*>(own) + (int64_t)par * world * xstride;
+    auto world_sum = [&](int pos) {
+        float w8[WMAX];
+#pragma unroll
+        for (int r = 0; r < WMAX; ++r)
+            w8[r] = __hip_atomic_load(xb + (int64_t)(r < world ? r : 0) * xstride + pos, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+        float g = w8[0];
+#pragma unroll
+        for (int r = 1; r < WMAX; ++r) g = r < world ? g + w8[r] : g;
+        return g;
+    };
+    const float gsum = world_sum(mypos);
+    if (blk == 0 && lane == 0 && loss_out) loss_out[0] = world_sum(mb.n_slab);
+    if (pp < 0) return;  // padding position (dummy layer-0 K slots)
+    adam_pack_pre(pp, gsum, ain, mb, oa, lr_t, ema_debias);
+}
+
+hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
+                                  int rank, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
+                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+    if (world < 1 || world > kPeerMaxRanks || rank < 0 || rank >= world || !err || nslabs < 1) return hipErrorInvalidValue;
+    for (int r = 0; r < world; ++r)
+        if (!dst.p[r]) return hipErrorInvalidValue;
+    float lr_t, ema_debias;
+    adam_host_factors(oa, lr_t, ema_debias);
+    const dim3 grid(mb.n_slab / (kRedParams * kRedVec));
+    const size_t region = px_region_offset(world, nfl);
+#define NRC_RX(HH, W)                                                                                                   \
+    hipLaunchKernelGGL((reduce_exchange_kernel<HH, W>), grid, dim3(kRedThreads), 0, s, slabs, nslabs, loss_partials,    \
+                       dst, region, rank, world, seq, err, loss_out, mb, oa, lr_t, ema_debias)
+#define NRC_RXW(HH)            \
+    if (world <= 2) NRC_RX(HH, 2); \
+    else if (world <= 4) NRC_RX(HH, 4); \
+    else if (world <= 8) NRC_RX(HH, 8); \
+    else NRC_RX(HH, 16)
+    if (mb.slab_f16) {
+        NRC_RXW(true);
+    } else {
+        NRC_RXW(false);
+    }
+#undef NRC_RXW
+#undef NRC_RX
+    return hipGetLastError();
 }
 
 hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int rank, int world, uint32_t seq,

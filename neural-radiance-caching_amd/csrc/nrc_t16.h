@@ -36,8 +36,10 @@ __device__ __forceinline__ h8 relu_b(const f4& lo, const f4& hi) {
 // Encoded input of sample c in lane group g: 24 K slots (t16_slot_feature) as three B-operand k-steps.
 // TriangleWave by the tent map (as encode_v3, octaves 3g .. 3g + 2 of each position dim), OneBlob in closed form
 // with the clamped wrap (blob_v3), Identity, padding 1.0.
+// pad: the value of slot 11 of lane group 0 -- canonical feature 66, the first constant-one column -- which is 1.0
+// for compact queries and the query's pad_ for padded ones (nrc_config.query_layout, the reference's Identity(1))
 __device__ __forceinline__ void encode16(float p0, float p1, float p2, float bA, float bB, float iA, float iB, int g,
-                                         h8 (&x)[3]) {
+                                         h8 (&x)[3], float pad = 1.0f) {
     const float sc = (float)(1 << (3 * g));
     float t[9];
     const float p[3] = {p0, p1, p2};
@@ -56,7 +58,7 @@ __device__ __forceinline__ void encode16(float p0, float p1, float p2, float bA,
     w[2] = pk2_abs_v(t[4], t[5]);
     w[3] = pk2_abs_v(t[6], t[7]);
     w[4] = pk2(__builtin_fabsf(t[8]), iA);
-    w[5] = pk2(iB, 1.0f);
+    w[5] = pk2(iB, g == 0 ? pad : 1.0f);
     blob_v3(bA, w[6], w[7]);
     blob_v3(bB, w[8], w[9]);
     w[10] = w[11] = 0x3C003C00u;

@@ -17,6 +17,8 @@
 //   LDS), the next layer's images written to the other buffer, the dW tiles streamed to the block's slab.
 #include "nrc_t16.h"
 
+#include <type_traits>
+
 namespace nrc_amd {
 namespace {
 
@@ -486,7 +488,9 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // in each backward step, compute the block's dW_L tiles from the images the chain waves wrote in the step before and
 // stream them to the slab. The two halves of a step share the SIMDs' MFMA pipes and hide each other's LDS and
 // dependency latency; the step's critical path is the chain alone instead of chain + dW.
-template <int AUX, int G = 2>  // G: 16-sample groups per chain wave (64 G samples per block)
+// G: 16-sample groups per chain wave (64 G samples per block); PADQ: padded RadianceQuery records (16 floats: the
+// position load takes pad_ along, 16 bytes instead of 12, the other loads one float further)
+template <int AUX, int G = 2, bool PADQ = false>
 __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                                int64_t b, float n_total, float loss_scale,
                                                                const h8* __restrict__ wf, const h8* __restrict__ wb,
@@ -581,7 +585,11 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     int r[G];
     bool valid[G];
     typedef float f3 __attribute__((ext_vector_type(3)));
-    f3 pq[G], tq[G];
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    typedef std::conditional_t<PADQ, f4v, f3> PQ;
+    constexpr int X = PADQ ? 1 : 0;
+    PQ pq[G];
+    f3 tq[G];
     f2 bl[G], id[G];
     const int gg = g < 3 ? g : 0;
 #pragma unroll
@@ -590,10 +598,11 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         const int64_t s = (int64_t)blockIdx.x * (64 * G) + r[u];
         valid[u] = s < b;
         const int64_t sc = valid[u] ? s : b - 1;
-        const float* qr = q + sc * NRC_INPUT_DIMS;
-        asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(pq[u]) : "v"(qr) : "memory");
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(bl[u]) : "v"(qr + 3 + 2 * gg) : "memory");
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(id[u]) : "v"(qr + 9 + 2 * gg) : "memory");
+        const float* qr = q + sc * (NRC_INPUT_DIMS + X);
+        if constexpr (PADQ) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(pq[u]) : "v"(qr) : "memory");
+        else asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(pq[u]) : "v"(qr) : "memory");
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(bl[u]) : "v"(qr + 3 + X + 2 * gg) : "memory");
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(id[u]) : "v"(qr + 9 + X + 2 * gg) : "memory");
         asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(tq[u]) : "v"(t + sc * 3) : "memory");
     }
 #pragma unroll
@@ -614,7 +623,9 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         tg[u][0] = tq[u].x; tg[u][1] = tq[u].y; tg[u][2] = tq[u].z;
-        encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u]);
+        float pad = 1.0f;
+        if constexpr (PADQ) pad = pq[u].w;
+        encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
         const u4 w = __builtin_bit_cast(u4, x[u][2]);
         *(u2*)(img_x2 + off32(r[u], 2 * g)) = u2{w.x, w.y};
         *(u2*)(img_x2 + off32(r[u], 2 * g + 1)) = u2{w.z, w.w};
@@ -791,10 +802,16 @@ int t16_blocks(int64_t b, int groups = 2) { return (int)((b + 64 * groups - 1) /
 
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
-                          hipStream_t s, bool split, int groups) {
+                          hipStream_t s, bool split, int groups, bool padq) {
     if (b <= 0) return hipSuccess;
     const dim3 grid(t16_blocks(b));
     const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
+    if (padq) {  // padded RadianceQuery records: the production shape only
+        if (!split || stamps || groups != 2) return hipErrorNotSupported;
+        hipLaunchKernelGGL((train16_split_kernel<16, 2, true>), grid, dim3(128 * kWaves), 0, s, queries, targets, b,
+                           n_total, loss_scale, f, bw, slabs, loss_partials);
+        return hipGetLastError();
+    }
     if (split && !stamps) {
         // slab stores as sc1 (AUX 16): they write through and drop the line from the XCD's L2, so the kernel does not end
         // with 5.9 MB of dirty slab lines to write back, and the reduce (on every XCD) reads them from memory either

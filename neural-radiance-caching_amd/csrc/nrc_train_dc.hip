@@ -93,7 +93,7 @@ struct Stamper {
     }
 };
 
-template <int CW, int GPW, int DWW, bool STAMP>
+template <int CW, int GPW, int DWW, bool STAMP, bool PADQ = false>  // PADQ: padded RadianceQuery records
 __device__ __forceinline__ void dc_chain(const float* __restrict__ q, const float* __restrict__ t, int64_t b,
                                          float n_total, float loss_scale, const h8* __restrict__ wf,
                                          const h8* __restrict__ wb, char* smem, int cw, int lane, uint32_t* err,
@@ -111,21 +111,24 @@ __device__ __forceinline__ void dc_chain(const float* __restrict__ q, const floa
     int r[GPW];
     bool valid[GPW];
     float pq[GPW][3], bl[GPW][2], iv[GPW][2], tg[GPW][3];
+    [[maybe_unused]] float pad[GPW];
+    constexpr int X = PADQ ? 1 : 0;
 #pragma unroll
     for (int u = 0; u < GPW; ++u) {
         r[u] = 16 * GPW * cw + 16 * u + c;
         const int64_t s = (int64_t)blockIdx.x * S + r[u];
         valid[u] = s < b;
         const int64_t sc = valid[u] ? s : b - 1;
-        // position, OneBlob dims 3 + 2g, 4 + 2g, Identity dims 9 + 2g, 10 + 2g (lane group 3: dummies with zero
-        // weights, fed from group 0's dims so that they stay finite), target
-        const float* qr = q + sc * NRC_INPUT_DIMS;
+        // position (+ pad_), OneBlob dims 3 + 2g, 4 + 2g, Identity dims 9 + 2g, 10 + 2g (lane group 3: dummies with
+        // zero weights, fed from group 0's dims so that they stay finite), target
+        const float* qr = q + sc * (NRC_INPUT_DIMS + X);
 #pragma unroll
         for (int k = 0; k < 3; ++k) pq[u][k] = qr[k];
-        bl[u][0] = qr[3 + 2 * gg];
-        bl[u][1] = qr[4 + 2 * gg];
-        iv[u][0] = qr[9 + 2 * gg];
-        iv[u][1] = qr[10 + 2 * gg];
+        if constexpr (PADQ) pad[u] = qr[3];
+        bl[u][0] = qr[3 + X + 2 * gg];
+        bl[u][1] = qr[4 + X + 2 * gg];
+        iv[u][0] = qr[9 + X + 2 * gg];
+        iv[u][1] = qr[10 + X + 2 * gg];
 #pragma unroll
         for (int k = 0; k < 3; ++k) tg[u][k] = t[sc * 3 + k];
     }
@@ -142,7 +145,8 @@ __device__ __forceinline__ void dc_chain(const float* __restrict__ q, const floa
     h8 x[GPW][3];
 #pragma unroll
     for (int u = 0; u < GPW; ++u) {
-        encode16(pq[u][0], pq[u][1], pq[u][2], bl[u][0], bl[u][1], iv[u][0], iv[u][1], g, x[u]);
+        if constexpr (PADQ) encode16(pq[u][0], pq[u][1], pq[u][2], bl[u][0], bl[u][1], iv[u][0], iv[u][1], g, x[u], pad[u]);
+        else encode16(pq[u][0], pq[u][1], pq[u][2], bl[u][0], bl[u][1], iv[u][0], iv[u][1], g, x[u]);
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const u4 w = __builtin_bit_cast(u4, x[u][ks]);
@@ -409,7 +413,7 @@ __device__ __forceinline__ void dc_dw(char* smem, int dw, int lane, _Float16* __
     dc_dw_step<CW, GPW, DWW, 0, STAMP>(smem, dw, lane, slab, loss_partials, err, stamp);
 }
 
-template <int CW, int GPW, int DWW, bool STAMP = false>
+template <int CW, int GPW, int DWW, bool STAMP = false, bool PADQ = false>
 __global__ __launch_bounds__(64 * (CW + DWW), (CW + DWW + 3) / 4) void train_dc_kernel(
     const float* __restrict__ q, const float* __restrict__ t, int64_t b, float n_total, float loss_scale,
     const h8* __restrict__ wf, const h8* __restrict__ wb, _Float16* __restrict__ slabs, float* __restrict__ loss_partials,
@@ -424,19 +428,25 @@ __global__ __launch_bounds__(64 * (CW + DWW), (CW + DWW + 3) / 4) void train_dc_
     if (threadIdx.x < 16) ((uint32_t*)(smem + Lay::OFF_FLAGS))[threadIdx.x] = 0;
     __syncthreads();
     if (wave < CW)
-        dc_chain<CW, GPW, DWW, STAMP>(q, t, b, n_total, loss_scale, wf, wb, smem, wave, lane, err, stamp);
+        dc_chain<CW, GPW, DWW, STAMP, PADQ>(q, t, b, n_total, loss_scale, wf, wb, smem, wave, lane, err, stamp);
     else
         dc_dw<CW, GPW, DWW, STAMP>(smem, wave - CW, lane, slabs + (int64_t)blockIdx.x * slab_floats(0), loss_partials,
                                    err, stamp);
     stamp.real(15);
 }
 
-template <int CW, int GPW, int DWW>
+template <int CW, int GPW, int DWW, bool PADQ = false>
 hipError_t launch_dc(const float* q, const float* t, int64_t b, float n_total, float loss_scale, const _Float16* wf,
                      const _Float16* wb, _Float16* slabs, float* loss_partials, uint32_t* err, hipStream_t s,
                      uint64_t* stamps) {
     constexpr int S = DcLayout<CW, GPW>::S;
     const int blocks = (int)((b + S - 1) / S);
+    if constexpr (PADQ) {  // padded RadianceQuery records: no stamped build
+        if (stamps) return hipErrorNotSupported;
+        hipLaunchKernelGGL((train_dc_kernel<CW, GPW, DWW, false, true>), dim3(blocks), dim3(64 * (CW + DWW)), 0, s, q,
+                           t, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, err, nullptr);
+        return hipGetLastError();
+    }
 #if NRC_DEBUG_KERNELS
     if (stamps)
         hipLaunchKernelGGL((train_dc_kernel<CW, GPW, DWW, true>), dim3(blocks), dim3(64 * (CW + DWW)), 0, s, q, t, b,
@@ -487,9 +497,14 @@ int dc_waves_per_block(int shape) {
 
 hipError_t launch_train_dc(int shape, const float* queries, const float* targets, int64_t b, float n_total,
                            float loss_scale, const _Float16* wf, const _Float16* wb, _Float16* slabs,
-                           float* loss_partials, uint32_t* err, hipStream_t s, uint64_t* stamps) {
+                           float* loss_partials, uint32_t* err, hipStream_t s, uint64_t* stamps, bool padq) {
     if (b <= 0) return hipSuccess;
     if (!err) return hipErrorInvalidValue;
+    if (padq) {  // padded RadianceQuery records: the production shape (dc_auto_shape) only
+        if (shape != 7) return hipErrorNotSupported;
+        return launch_dc<2, 1, 4, true>(queries, targets, b, n_total, loss_scale, wf, wb, slabs, loss_partials, err, s,
+                                        stamps);
+    }
 #if NRC_DEBUG_KERNELS
     static int applied = 0;
     const int delay = std::max(knob(kKnobDcDw0Delay), 0);

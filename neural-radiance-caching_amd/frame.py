@@ -89,6 +89,10 @@ def _sigs():
         "nrc_propagate_train_radiance_factored": [vp, vp, vp, u32, vp, vp, vp, u32, vp],
         "nrc_generate_train_permutation": [u64, u32, vp, u32, vp],
         "nrc_permute_train_data": [vp, vp, vp, u64, u32, i32, vp, vp, u32, vp],
+        "nrc_accumulate_render_radiance_factored_padded": [vp, vp, vp, vp, u32, ctypes.c_int, u32, vp],
+        "nrc_copy_radiance_to_output_factored_padded": [vp, vp, vp, u32, vp],
+        "nrc_propagate_train_radiance_factored_padded": [vp, vp, vp, u32, vp, vp, vp, u32, vp],
+        "nrc_permute_train_data_padded": [vp, vp, vp, u64, u32, i32, vp, vp, u32, vp],
         "nrc_process_frame": [vp, ctypes.POINTER(NrcFrameBuffers), ctypes.POINTER(NrcFrameParams),
                               ctypes.POINTER(ctypes.c_float)],
         "nrc_process_frame_shard": [vp, ctypes.POINTER(NrcFrameBuffers), ctypes.POINTER(NrcFrameParams), u32, u32,
@@ -126,20 +130,21 @@ def accumulate_render_radiance(radiance, throughput, output_rgba, num_pixels: in
 
 
 def accumulate_render_radiance_factored(radiance, queries, throughput, output_rgba, num_pixels: int, mode: RenderMode,
-                                        iteration_index: int, stream=None) -> None:
-    """USE_REFLECTANCE_FACTORING 1 form (frame.h): the radiance times the render query's reflectance."""
-    check(_sigs().nrc_accumulate_render_radiance_factored(
-        _ptr(radiance, "radiance"), _ptr(queries, "queries"), _ptr(throughput, "throughput"),
-        _ptr(output_rgba, "output_rgba"), int(num_pixels), int(mode), int(iteration_index), _stream(stream)))
+                                        iteration_index: int, stream=None, padded: bool = False) -> None:
+    """USE_REFLECTANCE_FACTORING 1 form (frame.h): the radiance times the render query's reflectance (padded: the
+    queries are 16-float records, USE_COMPACT_RADIANCE_QUERY 0)."""
+    fn = _sigs().nrc_accumulate_render_radiance_factored_padded if padded else _sigs().nrc_accumulate_render_radiance_factored
+    check(fn(_ptr(radiance, "radiance"), _ptr(queries, "queries"), _ptr(throughput, "throughput"),
+             _ptr(output_rgba, "output_rgba"), int(num_pixels), int(mode), int(iteration_index), _stream(stream)))
 
 
 def propagate_train_radiance_factored(end_vertices, end_radiance, end_queries, num_tiles: int, records, targets,
-                                      train_queries, num_records: int, stream=None) -> None:
+                                      train_queries, num_records: int, stream=None, padded: bool = False) -> None:
     """USE_REFLECTANCE_FACTORING 1 form of propagate_train_radiance (frame.h): targets hold radiance / reflectance."""
-    check(_sigs().nrc_propagate_train_radiance_factored(
-        _ptr(end_vertices, "end_vertices"), _ptr(end_radiance, "end_radiance"), _ptr(end_queries, "end_queries"),
-        int(num_tiles), _ptr(records, "records"), _ptr(targets, "targets"), _ptr(train_queries, "train_queries"),
-        int(num_records), _stream(stream)))
+    fn = _sigs().nrc_propagate_train_radiance_factored_padded if padded else _sigs().nrc_propagate_train_radiance_factored
+    check(fn(_ptr(end_vertices, "end_vertices"), _ptr(end_radiance, "end_radiance"), _ptr(end_queries, "end_queries"),
+             int(num_tiles), _ptr(records, "records"), _ptr(targets, "targets"), _ptr(train_queries, "train_queries"),
+             int(num_records), _stream(stream)))
 
 
 def infer_accumulate(net, queries, results, n: int, throughput, output_rgba, num_pixels: int, mode: RenderMode,
@@ -169,11 +174,12 @@ def generate_train_permutation(seed: int, frame_index: int, permutation, n: int,
 
 
 def permute_train_data(queries_src, targets_src, permutation, seed: int, frame_index: int, num_records: int,
-                       queries_dst, targets_dst, n_out: int = NUM_TRAINING_RECORDS_PER_FRAME, stream=None) -> None:
-    check(_sigs().nrc_permute_train_data(_ptr(queries_src, "queries_src"), _ptr(targets_src, "targets_src"),
-                                         _ptr(permutation, "permutation"), int(seed), int(frame_index),
-                                         int(num_records), _ptr(queries_dst, "queries_dst"),
-                                         _ptr(targets_dst, "targets_dst"), int(n_out), _stream(stream)))
+                       queries_dst, targets_dst, n_out: int = NUM_TRAINING_RECORDS_PER_FRAME, stream=None,
+                       padded: bool = False) -> None:
+    fn = _sigs().nrc_permute_train_data_padded if padded else _sigs().nrc_permute_train_data
+    check(fn(_ptr(queries_src, "queries_src"), _ptr(targets_src, "targets_src"), _ptr(permutation, "permutation"),
+             int(seed), int(frame_index), int(num_records), _ptr(queries_dst, "queries_dst"),
+             _ptr(targets_dst, "targets_dst"), int(n_out), _stream(stream)))
 
 
 def records_to_device(arr: np.ndarray, device):

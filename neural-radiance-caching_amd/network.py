@@ -31,8 +31,8 @@ from enum import IntEnum
 import numpy as np
 
 from . import _lib
-from ._lib import (BATCH_SIZE, GRAD_FLOATS, HASH_GRID_PARAMS, NUM_PARAMS, NrcConfig, NrcError, NrcHyperParams, check,
-                   lib)
+from ._lib import (BATCH_SIZE, GRAD_FLOATS, HASH_GRID_PARAMS, NUM_PARAMS, QUERY_PADDED, NrcConfig, NrcError,
+                   NrcHyperParams, check, lib)
 
 NRC_ERR_DESTROYED = 2
 
@@ -100,6 +100,7 @@ class Network:
         check(lib().nrc_create(ctypes.byref(h)))
         self._h = h
         self._lib = lib()
+        self.query_dims = 15
 
     # ---- lifecycle ---------------------------------------------------------------------------
     def init(self, stream=None, encoding: InputEncoding = InputEncoding.Frequency, verbose: bool = False,
@@ -108,6 +109,8 @@ class Network:
         cfg = ctypes.byref(config) if config is not None else None
         check(self._lib.nrc_init(self._h, s, int(encoding), cfg, int(bool(verbose))))
         self.encoding = InputEncoding(int(encoding))
+        # floats per RadianceQuery record (nrc_config.query_layout: compact 15, padded 16)
+        self.query_dims = 16 if config is not None and int(config.query_layout) == QUERY_PADDED else 15
 
     def destroy(self) -> None:
         check(self._lib.nrc_destroy(self._h))
@@ -124,7 +127,7 @@ class Network:
     # ---- hot path ----------------------------------------------------------------------------
     def train(self, inputs, targets, stream=None, loss: bool = False):
         """One training step on BATCH_SIZE samples; returns the batch loss if loss=True (blocking)."""
-        pi = _dev_ptr(inputs, "inputs", BATCH_SIZE * 15 if hasattr(inputs, "numel") else None)
+        pi = _dev_ptr(inputs, "inputs", BATCH_SIZE * self.query_dims if hasattr(inputs, "numel") else None)
         pt = _dev_ptr(targets, "targets", BATCH_SIZE * 3 if hasattr(targets, "numel") else None)
         lh = ctypes.c_float(float("nan"))
         lp = ctypes.byref(lh) if loss else None
@@ -141,7 +144,7 @@ class Network:
         n = int(numInputs)
         if n < 0 or n > 0xFFFFFFFF:
             raise ValueError("numInputs out of range")
-        pi = _dev_ptr(inputs, "inputs", n * 15 if hasattr(inputs, "numel") else None)
+        pi = _dev_ptr(inputs, "inputs", n * self.query_dims if hasattr(inputs, "numel") else None)
         po = _dev_ptr(outputs, "outputs", n * 3 if hasattr(outputs, "numel") else None)
         if stream is None:
             st = self._lib.nrc_infer(self._h, pi, po, n)
@@ -155,7 +158,7 @@ class Network:
         """Width-128 network: inference through the f16 (0) or FP8 (1) weight image, whatever infer_precision the
         handle was configured with (A/B timing, parity tests)."""
         n = int(numInputs)
-        pi = _dev_ptr(inputs, "inputs", n * 15 if hasattr(inputs, "numel") else None)
+        pi = _dev_ptr(inputs, "inputs", n * self.query_dims if hasattr(inputs, "numel") else None)
         po = _dev_ptr(outputs, "outputs", n * 3 if hasattr(outputs, "numel") else None)
         check(self._lib.nrc_debug_infer_precision(self._h, int(precision), pi, po, n, _stream_ptr(stream)))
 
@@ -192,14 +195,14 @@ class Network:
     def train_batch(self, inputs, targets, b: int, loss: bool = False):
         lh = ctypes.c_float(float("nan"))
         b = int(b)
-        check(self._lib.nrc_train_batch(self._h, _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None),
+        check(self._lib.nrc_train_batch(self._h, _dev_ptr(inputs, "inputs", b * self.query_dims if hasattr(inputs, "numel") else None),
                                         _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None), b,
                                         ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
     def train_grad(self, inputs, targets, b: int, global_b: int, grad) -> None:
         b = int(b)
-        check(self._lib.nrc_train_grad(self._h, _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None) if b else None,
+        check(self._lib.nrc_train_grad(self._h, _dev_ptr(inputs, "inputs", b * self.query_dims if hasattr(inputs, "numel") else None) if b else None,
                                        _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None,
                                        b, int(global_b),
                                        _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None)))
@@ -215,7 +218,7 @@ class Network:
         HASH_GRID_PARAMS; sum it over ranks as int64) and the grid part of grad left unwritten."""
         b = int(b)
         check(self._lib.nrc_train_grad_fixed(
-            self._h, _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None) if b else None,
+            self._h, _dev_ptr(inputs, "inputs", b * self.query_dims if hasattr(inputs, "numel") else None) if b else None,
             _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None, b, int(global_b),
             _dev_ptr(grad, "grad", self.grad_floats if hasattr(grad, "numel") else None),
             _dev_ptr(grid_fixed, "grid_fixed", HASH_GRID_PARAMS if hasattr(grid_fixed, "numel") else None,
@@ -248,7 +251,7 @@ class Network:
         all-reduced over the attached communicator inside the library, then the identical Adam + EMA step."""
         lh = ctypes.c_float(float("nan"))
         b = int(b_local)
-        pi = _dev_ptr(inputs, "inputs", b * 15 if hasattr(inputs, "numel") else None) if b else None
+        pi = _dev_ptr(inputs, "inputs", b * self.query_dims if hasattr(inputs, "numel") else None) if b else None
         pt = _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None
         check(self._lib.nrc_train_dp(self._h, pi, pt, b, int(global_b), ctypes.byref(lh) if loss else None))
         return lh.value if loss else None

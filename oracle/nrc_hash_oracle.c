@@ -92,8 +92,8 @@ static float* grid_view(const float* grid, int mode) {
     return t;
 }
 
-/* enc[64] of one query; table = grid_view() */
-static void encode_one(const float* table, const float* q, int mode, float* enc) {
+/* enc[64] of one query (padq: a non-compact 16-float record); table = grid_view() */
+static void encode_one(const float* table, const float* q, int mode, float* enc, int padq) {
     for (int l = 0; l < HL; ++l) {
         uint32_t idx[8];
         float w[8];
@@ -112,8 +112,15 @@ static void encode_one(const float* table, const float* q, int mode, float* enc)
             }
         }
     }
-    /* OneBlob(dims 3-8) and Identity(dims 9-14): the Frequency composite's features 36..65 */
+    /* OneBlob(dims 3-8) and Identity(dims 9-14): the Frequency composite's features 36..65 (padded records: pad_,
+     * then the padded composite's 37..66, NRCNetworkConfigs.h:106-111) */
     float full[NRC_ENC_WIDTH];
+    if (padq) {
+        orc_encode_padded(q, 1, full);
+        for (int k = 0; k < 31; ++k) enc[32 + k] = (mode == ORC_FP32) ? full[36 + k] : orc_f16_round(full[36 + k]);
+        enc[63] = 1.0f;
+        return;
+    }
     orc_encode(q, 1, full);
     for (int k = 0; k < 30; ++k) enc[32 + k] = (mode == ORC_FP32) ? full[36 + k] : orc_f16_round(full[36 + k]);
     enc[62] = enc[63] = 1.0f; /* Composite padding to the FullyFusedMLP width [M] */
@@ -121,7 +128,7 @@ static void encode_one(const float* table, const float* q, int mode, float* enc)
 
 void orc_hash_encode(const float* params, const float* queries, int64_t n, int mode, float* enc) {
     float* table = grid_view(params + NRC_HASH_GRID_OFFSET, mode);
-    for (int64_t s = 0; s < n; ++s) encode_one(table, queries + s * NRC_INPUT_DIMS, mode, enc + s * ENC);
+    for (int64_t s = 0; s < n; ++s) encode_one(table, queries + s * NRC_INPUT_DIMS, mode, enc + s * ENC, 0);
     free(table);
 }
 
@@ -170,8 +177,8 @@ typedef struct {
 
 static float rnd(float v, int mode) { return mode == ORC_FP32 ? v : orc_f16_round(v); }
 
-static void forward_one(const float* w, const float* table, const float* q, int mode, acts_t* A) {
-    encode_one(table, q, mode, A->enc);
+static void forward_one(const float* w, const float* table, const float* q, int mode, acts_t* A, int padq) {
+    encode_one(table, q, mode, A->enc, padq);
     const float* in = A->enc;
     for (int l = 0; l < 5; ++l) {
         float z[64];
@@ -188,6 +195,7 @@ typedef struct {
     const float *w, *table, *queries, *targets;
     int64_t begin, end;
     int mode;
+    int padq; /* non-compact 16-float records */
     float* out;
     double n_total;
     float loss_scale;
@@ -198,7 +206,8 @@ static void* fwd_job(void* arg) {
     job_t* J = (job_t*)arg;
     acts_t A;
     for (int64_t s = J->begin; s < J->end; ++s) {
-        forward_one(J->w, J->table, J->queries + s * NRC_INPUT_DIMS, J->mode, &A);
+        forward_one(J->w, J->table, J->queries + s * (J->padq ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS), J->mode, &A,
+                    J->padq);
         for (int c = 0; c < 3; ++c) J->out[s * 3 + c] = A.y[c];
     }
     return NULL;
@@ -218,6 +227,11 @@ static int nthr(int t, int64_t n) {
 }
 
 void orc_hash_forward(const float* params, const float* queries, int64_t n, int mode, float* out, int nthreads) {
+    orc_hash_forward_layout(NRC_QUERY_COMPACT, params, queries, n, mode, out, nthreads);
+}
+
+void orc_hash_forward_layout(int layout, const float* params, const float* queries, int64_t n, int mode, float* out,
+                             int nthreads) {
     if (n <= 0) return;
     float* w = mlp_view(params, mode);
     float* table = grid_view(params + NRC_HASH_GRID_OFFSET, mode);
@@ -232,6 +246,7 @@ void orc_hash_forward(const float* params, const float* queries, int64_t n, int 
         jobs[t].begin = n * t / nthreads;
         jobs[t].end = n * (t + 1) / nthreads;
         jobs[t].mode = mode;
+        jobs[t].padq = layout == NRC_QUERY_PADDED;
         jobs[t].out = out;
         if (nthreads > 1) pthread_create(&th[t], NULL, fwd_job, &jobs[t]);
         else fwd_job(&jobs[t]);
@@ -249,8 +264,8 @@ static void* grad_job(void* arg) {
     acts_t A;
     const float n_total = (float)J->n_total;
     for (int64_t s = J->begin; s < J->end; ++s) {
-        const float* q = J->queries + s * NRC_INPUT_DIMS;
-        forward_one(J->w, J->table, q, mode, &A);
+        const float* q = J->queries + s * (J->padq ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS);
+        forward_one(J->w, J->table, q, mode, &A, J->padq);
         const float* t = J->targets + s * 3;
         const float lum = 0.299f * A.y[0] + 0.587f * A.y[1] + 0.114f * A.y[2];
         const float denom = lum * lum + NRC_LUM_EPS;
@@ -301,6 +316,12 @@ static void* grad_job(void* arg) {
 
 double orc_hash_grad(const float* params, const float* queries, const float* targets, int64_t b, double n_total,
                      float loss_scale, int mode, float* grad, int nthreads) {
+    return orc_hash_grad_layout(NRC_QUERY_COMPACT, params, queries, targets, b, n_total, loss_scale, mode, grad,
+                                nthreads);
+}
+
+double orc_hash_grad_layout(int layout, const float* params, const float* queries, const float* targets, int64_t b,
+                            double n_total, float loss_scale, int mode, float* grad, int nthreads) {
     for (int i = 0; i < NRC_HASH_NUM_PARAMS; ++i) grad[i] = 0.0f;
     if (b <= 0) return 0.0;
     float* w = mlp_view(params, mode);
@@ -316,6 +337,7 @@ double orc_hash_grad(const float* params, const float* queries, const float* tar
         jobs[t].begin = b * t / nthreads;
         jobs[t].end = b * (t + 1) / nthreads;
         jobs[t].mode = mode;
+        jobs[t].padq = layout == NRC_QUERY_PADDED;
         jobs[t].n_total = n_total;
         jobs[t].loss_scale = loss_scale;
         jobs[t].grad = (double*)calloc(NRC_HASH_NUM_PARAMS, sizeof(double));

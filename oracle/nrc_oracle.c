@@ -124,6 +124,23 @@ void orc_encode(const float* queries, int64_t n, float* enc) {
     }
 }
 
+/* Non-compact RadianceQuery (USE_COMPACT_RADIANCE_QUERY 0; neural_radiance_caching.h:38-40, :107-111): 16 floats,
+ * pad_ after the position; the Composite gains an Identity(1) of pad_ after the TriangleWave (NRCNetworkConfigs.h:61-67):
+ * [0,36) TriangleWave | 36 pad_ | [37,61) OneBlob | [61,67) Identity | [67,80) padding 1.0 (tcnn's Composite pads the
+ * 67 features to the FullyFusedMLP's input width 80 [M]). */
+void orc_encode_padded(const float* queries, int64_t n, float* enc) {
+    for (int64_t s = 0; s < n; ++s) {
+        const float* q = queries + s * NRC_INPUT_DIMS_PADDED;
+        float* e = enc + s * NRC_ENC_WIDTH;
+        for (int d = 0; d < NRC_TRI_DIMS; ++d)
+            for (int k = 0; k < NRC_TRI_FREQS; ++k) e[d * NRC_TRI_FREQS + k] = tri_wave(q[d], k);
+        e[36] = q[3];
+        for (int d = 0; d < NRC_BLOB_DIMS; ++d) one_blob(q[4 + d], e + 37 + d * NRC_BLOB_BINS);
+        for (int d = 0; d < NRC_IDENT_DIMS; ++d) e[61 + d] = q[10 + d];
+        for (int f = 67; f < NRC_ENC_WIDTH; ++f) e[f] = 1.0f;
+    }
+}
+
 /* Extension encoding NRC_ENCODING_FREQUENCY_SH (not in the reference; BASELINE.json north_star "frequency +
  * one-blob + spherical-harmonics"): TriangleWave(pos) 36 | SphericalHarmonics degree 4 of the direction 16 |
  * OneBlob(normal theta/phi, roughness x/y) 16 | Identity(albedos) 6 | pad 1.0 x 6 = 80. The direction is the unit
@@ -165,9 +182,12 @@ void orc_encode_sh(const float* queries, int64_t n, float* enc) {
 }
 
 static void encode_kind(int kind, const float* q, float* enc) {
-    if (kind == NRC_ENCODING_FREQUENCY_SH) orc_encode_sh(q, 1, enc);
+    if (kind & ORC_KIND_PADDED) orc_encode_padded(q, 1, enc);
+    else if (kind == NRC_ENCODING_FREQUENCY_SH) orc_encode_sh(q, 1, enc);
     else orc_encode(q, 1, enc);
 }
+/* floats per RadianceQuery record of an encoding kind */
+static int64_t kind_qdims(int kind) { return (kind & ORC_KIND_PADDED) ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS; }
 
 /* ------------------------------------------------------------------------------------------ */
 /* Network                                                                                     */
@@ -274,7 +294,7 @@ static void* forward_job(void* arg) {
     job_t* J = (job_t*)arg;
     sample_acts A;
     for (int64_t s = J->begin; s < J->end; ++s) {
-        forward_one(J->w, J->queries + s * NRC_INPUT_DIMS, J->mode, J->kind, &A);
+        forward_one(J->w, J->queries + s * kind_qdims(J->kind), J->mode, J->kind, &A);
         for (int c = 0; c < NRC_OUTPUT_DIMS; ++c) J->out[s * NRC_OUTPUT_DIMS + c] = A.y[c];
     }
     return NULL;
@@ -327,7 +347,7 @@ static void* grad_job(void* arg) {
     sample_acts A;
     const float n_total = (float)J->n_total;
     for (int64_t s = J->begin; s < J->end; ++s) {
-        forward_one(w, J->queries + s * NRC_INPUT_DIMS, mode, J->kind, &A);
+        forward_one(w, J->queries + s * kind_qdims(J->kind), mode, J->kind, &A);
         const float* t = J->targets + s * NRC_OUTPUT_DIMS;
         const float lum = 0.299f * A.y[0] + 0.587f * A.y[1] + 0.114f * A.y[2];
         const float denom = lum * lum + NRC_LUM_EPS;

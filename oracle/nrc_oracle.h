@@ -51,7 +51,13 @@ double orc_grad(const float* params, const float* queries, const float* targets,
 
 /* Extension encoding NRC_ENCODING_FREQUENCY_SH (see nrc_oracle.c): 80-wide, same MLP shape as Frequency. */
 void orc_encode_sh(const float* queries, int64_t n, float* enc);
-/* orc_forward / orc_grad for an encoding kind (NRC_ENCODING_FREQUENCY or NRC_ENCODING_FREQUENCY_SH) */
+/* Non-compact RadianceQuery (16 f32, USE_COMPACT_RADIANCE_QUERY 0) into n x 80 in the reference's padded order:
+ * [0,36) TriangleWave, 36 pad_, [37,61) OneBlob, [61,67) Identity, [67,80) 1.0. */
+void orc_encode_padded(const float* queries, int64_t n, float* enc);
+/* kind flag: the queries are non-compact 16-float records (orc_encode_padded; Frequency only here, Hash: the
+ * orc_hash_*_layout functions) */
+#define ORC_KIND_PADDED 16
+/* orc_forward / orc_grad for an encoding kind (NRC_ENCODING_FREQUENCY or NRC_ENCODING_FREQUENCY_SH, | ORC_KIND_PADDED) */
 void orc_forward_enc(int kind, const float* params, const float* queries, int64_t n, int mode, float* out,
                      int nthreads);
 double orc_grad_enc(int kind, const float* params, const float* queries, const float* targets, int64_t b,
@@ -105,6 +111,12 @@ void orc_hash_encode(const float* params, const float* queries, int64_t n, int m
 void orc_hash_forward(const float* params, const float* queries, int64_t n, int mode, float* out, int nthreads);
 double orc_hash_grad(const float* params, const float* queries, const float* targets, int64_t b, double n_total,
                      float loss_scale, int mode, float* grad, int nthreads);
+/* the same for a query layout (NRC_QUERY_COMPACT / NRC_QUERY_PADDED: the padded encoding is HashGrid 0..31 | pad_ 32 |
+ * OneBlob 33..56 | Identity 57..62 | 1.0) */
+void orc_hash_forward_layout(int layout, const float* params, const float* queries, int64_t n, int mode, float* out,
+                             int nthreads);
+double orc_hash_grad_layout(int layout, const float* params, const float* queries, const float* targets, int64_t b,
+                            double n_total, float loss_scale, int mode, float* grad, int nthreads);
 void orc_hash_adam_ema(float* params, float* m, float* v, float* ema, float* infer_params, uint32_t* grid_steps,
                        uint32_t step, const float* grad, float loss_scale, float lr, float beta1, float beta2,
                        float eps, float l2_reg, float ema_decay);

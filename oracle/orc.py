@@ -46,6 +46,7 @@ def lib() -> ctypes.CDLL:
                                    ctypes.c_float, ctypes.c_float, ctypes.c_int64]
         L.orc_init_params.argtypes = [fp, ctypes.c_uint64]
         L.orc_encode_sh.argtypes = [fp, ctypes.c_int64, fp]
+        L.orc_encode_padded.argtypes = [fp, ctypes.c_int64, fp]
         L.orc_forward_enc.argtypes = [ctypes.c_int, fp, fp, ctypes.c_int64, ctypes.c_int, fp, ctypes.c_int]
         L.orc_grad_enc.restype = ctypes.c_double
         L.orc_grad_enc.argtypes = [ctypes.c_int, fp, fp, fp, ctypes.c_int64, ctypes.c_double, ctypes.c_float,
@@ -62,6 +63,10 @@ def lib() -> ctypes.CDLL:
         L.orc_hash_forward.argtypes = [vp, vp, i64, ctypes.c_int, vp, ctypes.c_int]
         L.orc_hash_grad.restype = ctypes.c_double
         L.orc_hash_grad.argtypes = [vp, vp, vp, i64, ctypes.c_double, ctypes.c_float, ctypes.c_int, vp, ctypes.c_int]
+        L.orc_hash_forward_layout.argtypes = [ctypes.c_int, vp, vp, i64, ctypes.c_int, vp, ctypes.c_int]
+        L.orc_hash_grad_layout.restype = ctypes.c_double
+        L.orc_hash_grad_layout.argtypes = [ctypes.c_int, vp, vp, vp, i64, ctypes.c_double, ctypes.c_float, ctypes.c_int,
+                                           vp, ctypes.c_int]
         L.orc_hash_adam_ema.argtypes = [vp, vp, vp, vp, vp, vp, u32, vp] + [ctypes.c_float] * 7
         L.orc_hash_init_params.argtypes = [vp, u64]
         L.orc_hash_corners.argtypes = [vp, ctypes.c_int, vp, vp]
@@ -127,6 +132,17 @@ def encode(queries: np.ndarray) -> np.ndarray:
 
 
 FREQUENCY, HASH, FREQUENCY_SH = 0, 1, 2
+# encoding kind flag: non-compact 16-float RadianceQuery records (USE_COMPACT_RADIANCE_QUERY 0; ORC_KIND_PADDED)
+PADDED = 16
+
+
+def encode_padded(queries: np.ndarray) -> np.ndarray:
+    """[n][16] non-compact queries -> [n][80] in the reference's padded order (nrc_oracle.c orc_encode_padded)."""
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    out = np.empty((q.shape[0], 80), dtype=np.float32)
+    if q.shape[0]:
+        lib().orc_encode_padded(_p(q), q.shape[0], _p(out))
+    return out
 
 
 def encode_sh(queries: np.ndarray) -> np.ndarray:
@@ -278,20 +294,20 @@ def hash_encode(params, queries, mode: int = MIXED) -> np.ndarray:
     return out
 
 
-def hash_forward(params, queries, mode: int = MIXED, threads: int | None = None) -> np.ndarray:
+def hash_forward(params, queries, mode: int = MIXED, threads: int | None = None, padded: bool = False) -> np.ndarray:
     q, p = _f32(queries), _f32(params)
     out = np.zeros((q.shape[0], 3), np.float32)
     if q.shape[0]:
-        lib().orc_hash_forward(_v(p), _v(q), q.shape[0], mode, _v(out), threads or default_threads())
+        lib().orc_hash_forward_layout(int(padded), _v(p), _v(q), q.shape[0], mode, _v(out), threads or default_threads())
     return out
 
 
-def hash_grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, threads=None):
+def hash_grad(params, queries, targets, n_total=None, loss_scale=128.0, mode=MIXED, threads=None, padded: bool = False):
     q, t, p = _f32(queries), _f32(targets), _f32(params)
     b = q.shape[0]
     g = np.zeros(HASH_NUM_PARAMS, np.float32)
-    loss = lib().orc_hash_grad(_v(p), _v(q), _v(t), b, float(3.0 * b if n_total is None else n_total),
-                               float(loss_scale), mode, _v(g), threads or default_threads())
+    loss = lib().orc_hash_grad_layout(int(padded), _v(p), _v(q), _v(t), b, float(3.0 * b if n_total is None else n_total),
+                                      float(loss_scale), mode, _v(g), threads or default_threads())
     return g, float(loss)
 
 

@@ -202,18 +202,19 @@ def test_two_ranks_on_one_gpu_gloo_hash_exact(tmp_path, nrc, torch, dev):
     ref.destroy()
 
 
-@pytest.mark.parametrize("B", [16384, 4096])
-def test_two_ranks_on_one_gpu_peer_exchange(tmp_path, nrc, torch, dev, golden, B):
+@pytest.mark.parametrize("B,path", [(16384, "peer"), (4096, "peer"), (4096, "peer_push")])
+def test_two_ranks_on_one_gpu_peer_exchange(tmp_path, nrc, torch, dev, golden, B, path):
     """The one-shot peer exchange (nrc_peer_exchange_*): two processes on cuda:0, IPC handles
     all-gathered over gloo, nrc_train_dp pushing each rank's gradient into the other's receive buffer and summing in
-    rank order. Replicas bit-identical, and bitwise the single-process step that sums the two shards' gradients
+    rank order -- fused into the reduction ("peer", production) or as reduce / push / apply launches ("peer_push").
+    Replicas bit-identical, and bitwise the single-process step that sums the two shards' gradients
     (g0 + g1, one f32 addition -- also what a 2-rank RCCL all-reduce computes) and applies them with nrc_train_apply."""
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
     np.save(tmp_path / "params.npy", golden["params_b"])
     steps = 3
     procs = [subprocess.Popen([sys.executable, str(ROOT / "tools" / "dp_rank_worker.py"), str(tmp_path), str(B),
-                               "Frequency", str(steps), "peer"], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                               "Frequency", str(steps), path], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
     logs = [p.communicate(timeout=240)[0] for p in procs]
     assert all(p.returncode == 0 for p in procs), logs
@@ -236,11 +237,37 @@ def test_two_ranks_on_one_gpu_peer_exchange(tmp_path, nrc, torch, dev, golden, B
     ref.destroy()
 
 
+@pytest.mark.parametrize("B", [16384, 2048, 0])
+def test_peer_exchange_world_1_is_the_fused_step(nrc, torch, dev, golden, B):
+    """A world-1 peer exchange (what bench.py's per-rank leg runs): nrc_train_dp through the fused reduce + exchange
+    launch stores each block's partials into its own buffer, waits for its own flags and applies the one-rank sum --
+    bitwise the state and loss of nrc_train's reduce + Adam (the same slab sums, a sum over one rank is the value).
+    B = 0: a rank without samples takes part with a zero gradient (loss 0; Adam's l2 term still steps the weights)."""
+    a, b = nrc.Network(), nrc.Network()
+    for n in (a, b):
+        n.init(stream=torch.cuda.current_stream())
+        n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+    h = a.peer_exchange_handle(1)
+    a.peer_exchange_open(0, 1, h)
+    zero_g = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
+    for it in range(3):
+        q_np, t_np = nrc.synthetic.cornell_batch(max(B, 1), seed=90 + it)
+        q, t = to_dev(torch, dev, q_np), to_dev(torch, dev, t_np)
+        la = a.train_dp(q, t, B, max(B, 1), loss=True)
+        lb = b.train_batch(q, t, B, loss=True) if B else b.train_apply(zero_g, loss=True)
+        assert la == lb
+    for slot in ("PARAMS", "INFER", "EMA", "ADAM_M", "ADAM_V"):
+        np.testing.assert_array_equal(a.get_state(getattr(nrc.StateSlot, slot)), b.get_state(getattr(nrc.StateSlot, slot)))
+    a.peer_exchange_close()
+    a.destroy()
+    b.destroy()
+
+
 def test_peer_exchange_argument_checks(nrc, torch, dev):
     net = nrc.Network()
     net.init(stream=torch.cuda.current_stream())
     with pytest.raises(nrc.NrcError):
-        net.peer_exchange_handle(1)  # world >= 2
+        net.peer_exchange_handle(0)  # world >= 1
     with pytest.raises(nrc.NrcError):
         net.peer_exchange_open(0, 2, bytes(128))  # no buffer allocated yet
     h = net.peer_exchange_handle(2)

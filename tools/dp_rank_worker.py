@@ -7,7 +7,8 @@ nrc_train_grad / nrc_train_apply through nrc_amd.dp.DataParallelTrainer, every r
 global_batch (default 16,384) is split over the ranks; 4,096 gives configs[3]'s per-rank slice of 2,048 samples.
 encoding Hash: the exact grid exchange (DataParallelTrainer with an int64 grid_fixed buffer).
 exchange "peer": the library's one-shot peer exchange (nrc_peer_exchange_*, handles all-gathered over gloo) through
-nrc_train_dp instead of the Python all-reduce.
+nrc_train_dp instead of the Python all-reduce, fused into the reduction (the production path); "peer_push": the same
+exchange as separate reduce / push / apply launches (knob peer_path = 0).
 """
 import os
 import sys
@@ -28,10 +29,12 @@ def main() -> None:
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     encoding = sys.argv[3] if len(sys.argv) > 3 else "Frequency"
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
-    peer = len(sys.argv) > 5 and sys.argv[5] == "peer"
+    peer = len(sys.argv) > 5 and sys.argv[5] in ("peer", "peer_push")
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     nrc = nrc_loader.load()
+    if len(sys.argv) > 5 and sys.argv[5] == "peer_push":
+        nrc._lib.set_knob("peer_path", 0)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     net = nrc.Network()

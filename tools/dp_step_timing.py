@@ -1,5 +1,5 @@
 """Per-step time of data-parallel training on one GPU shared by the ranks: the library's one-shot
-peer exchange (nrc_peer_exchange_* + nrc_train_dp) against the Python all-reduce over gloo (DataParallelTrainer), for
+peer exchange (nrc_peer_exchange_* + nrc_train_dp; fused into the reduction, and as separate launches) against the Python all-reduce over gloo (DataParallelTrainer), for
 the reference's per-step minibatch split over the ranks (b_local = 16,384 / world) and weak-scaled (b_local = 16,384).
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P \\
@@ -46,13 +46,15 @@ def main() -> None:
         global_b = B if split else B * world
         s0 = rank * b_local if split else 0
         qs, ts = q[s0:s0 + b_local], t[s0:s0 + b_local]
-        for mode in ("peer", "gloo"):
+        for mode in ("peer", "peer_push", "gloo"):
+            # peer: the exchange fused into the reduction (production); peer_push: reduce / push / apply launches
+            nrc._lib.set_knob("peer_path", 0 if mode == "peer_push" else -1)
             net = nrc.Network()
             net.init(stream=stream)
             grad = torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev)
             trainer = nrc.dp.DataParallelTrainer(net, grad)
             trainer.broadcast_state(net, dev)
-            if mode == "peer":
+            if mode.startswith("peer"):
                 nrc.dp.open_peer_exchange(net)
                 step = lambda: net.train_dp(qs, ts, b_local, global_b)  # noqa: E731
             else:
@@ -74,7 +76,7 @@ def main() -> None:
             same = all(torch.equal(ps[0], x) for x in ps[1:])
             res[f"{mode}_{'split' if split else 'weak'}"] = {"b_local": b_local, "global_b": global_b,
                                                             "us_per_step": float(worst.item()), "replicas_equal": same}
-            if mode == "peer":
+            if mode.startswith("peer"):
                 dist.barrier()
                 net.peer_exchange_close()
             net.destroy()
