@@ -346,6 +346,7 @@ struct nrc_net {
     int px_world = 0, px_rank = -1;
     uint32_t px_seq = 0;
     bool px_open = false;
+    bool px_shared = false;  // a peer's buffer lives on this rank's device (ranks sharing a GPU): split exchange
     void peer_close() {
         if (px_open)
             for (int r = 0; r < px_world; ++r)
@@ -357,6 +358,7 @@ struct nrc_net {
         px_rank = -1;
         px_seq = 0;
         px_open = false;
+        px_shared = false;
     }
     void alloc_loss_slots() {
         HIP_CHECK(hipMalloc(&work_queue, kInferPoolBytes));
@@ -771,7 +773,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobHashFeatAbl: return v >= -1 && v <= 36;
         case kKnobT16Groups: return v == -1 || v == 1 || v == 2;
         case kKnobHashFeatP: return v == -1 || (v >= 8 && v <= 256 && v % 8 == 0);
-        case kKnobPeerPath: return v >= -1 && v <= 1;
+        case kKnobPeerPath: return v >= -1 && v <= 2;
         default: return false;
     }
 }
@@ -1202,9 +1204,12 @@ void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_loc
     if (net->px_open) {
         net->px_seq = net->px_seq + 1u ? net->px_seq + 1u : 1u;
         const int nfl = (int)net->grad_floats();
-        if (knob(kKnobPeerPath) != 0) {
+        const int kp = knob(kKnobPeerPath);
+        if (kp != 0) {
             // the exchange fused into the reduction: gradient pass -> one launch that reduces the slabs, pushes each
             // block's partials to every rank, waits for the same block of every rank, sums in rank order, Adam/EMA
+            // (split: the wait + sum + Adam as a second, small launch -- ranks sharing this device)
+            const bool split = kp == 2 || (kp == -1 && net->px_shared);
             if (global_b < b_local || global_b == 0)
                 throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
             int blocks = 1;
@@ -1223,7 +1228,7 @@ void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_loc
             HIP_CHECK(launch_reduce_exchange(net->slabs, blocks, net->loss_partials, net->px_peers, net->px_rank,
                                              net->px_world, nfl, net->px_seq, net->proto_err_dev(),
                                              loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step),
-                                             net->stream));
+                                             net->stream, split));
         } else {
             // round 4's first version (knob peer_path = 0; world >= 2): reduce to a gradient -> push the gradient to
             // every peer's receive slot -> wait + rank-order sum + Adam/EMA
@@ -1443,6 +1448,14 @@ nrc_status nrc_peer_exchange_open(nrc_net* net, int rank, int world, const void*
             }
             p.p[r] = static_cast<float*>(ptr);
         }
+        // ranks on one device (tests; oversubscription): the exchange's waits go to the split path's small apply grid
+        bool shared = false;
+        for (int r = 0; r < world; ++r) {
+            if (r == rank) continue;
+            hipPointerAttribute_t a{};
+            if (hipPointerGetAttributes(&a, p.p[r]) == hipSuccess && a.device == net->device) shared = true;
+        }
+        net->px_shared = shared;
         net->px_peers = p;
         net->px_rank = rank;
         net->px_seq = 0;

@@ -326,8 +326,9 @@ enum Knob : int {
     kKnobHashFeatAbl = 6,  // debug library: hash_feature_kernel ablation (1 no gathers, 2 no position loads, 4 no stores)
     kKnobT16Groups = 7,    // role-split t16 training kernel: 16-sample groups per chain wave (1: 64-sample blocks; -1 = 2)
     kKnobHashFeatP = 8,    // Hash feature pass: query ranges per level (multiple of 8; -1 = 16 above 2^19 queries, else 8)
-    kKnobPeerPath = 9,     // nrc_train_dp over the peer exchange: -1 / 1 the exchange fused into the reduction, 0 the
-                           // reduce + push + apply launches (round 4's first version)
+    kKnobPeerPath = 9,     // nrc_train_dp over the peer exchange: -1 automatic (fused, or split when a peer shares this
+                           // rank's device), 0 the reduce + push + apply launches (round 4's first version), 1 fused,
+                           // 2 split (reduce + push, then wait + sum + Adam)
     kKnobCount = 10
 };
 int knob(Knob k);
@@ -393,10 +394,11 @@ hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int
                             hipStream_t s);
 hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
                              const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s);
-// reduce + peer exchange + rank-order sum + Adam/EMA in one launch after the gradient pass (world 1..16)
+// reduce + peer exchange + rank-order sum + Adam/EMA in one launch after the gradient pass (world 1..16); split: as
+// two launches (reduce + push, then wait + sum + Adam in a small grid) for ranks that share a device
 hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
                                   int rank, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
-                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s);
+                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, bool split = false);
 
 // ---- per-handle scratch used by the frame driver (nrc_capi.cpp): NRC_NUM_BATCHES loss slots on the device and a
 // pinned host mirror

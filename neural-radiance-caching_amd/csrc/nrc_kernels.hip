@@ -4068,7 +4068,52 @@ size_t peer_buffer_bytes(int world, int nfl, int n_slab) {
            sizeof(uint32_t) * (size_t)2 * nblk * kPeerMaxRanks;
 }
 
-template <bool H, int WMAX>
+// Wave-level second half of the exchange for chunk blk (64 slab positions, one per lane; this wave's lane = position
+// blk * 64 + lane): wait for every rank's flag of the chunk, sum the world's partials in rank order, Adam/EMA. ain: the
+// position's Adam state, loaded before the wait. Shared by the fused kernel and the split path's apply kernel.
+template <int WMAX>
+__device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, int blk, int nblk, int par, int world,
+                                                    int xstride, int pp, uint32_t seq, uint32_t* err, float* loss_out,
+                                                    const AdamIn& ain, const ModelBuffers& mb, const OptimArgs& oa,
+                                                    float lr_t, float ema_debias) {
+#pragma clang fp contract(off)
+    const int64_t flag_base = (int64_t)2 * world * xstride;
+    const int mypos = blk * kRedParams * kRedVec + lane;
+    // one flag per lane (lanes past the world re-read flag 0); wave-uniform loop, no store
+    const uint32_t* const fw = reinterpret_cast<const uint32_t*>(own) + flag_base +
+                               ((int64_t)par * nblk + blk) * kPeerMaxRanks + (lane < world ? lane : 0);
+    int i = 0;
+    for (; i < (1 << 21); ++i) {
+        const bool ready = __hip_atomic_load(fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
+        if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;
+        if (i < 4096) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(127);
+    }
+    if (i == (1 << 21) && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the world sum in rank order (branch-free: a rank past the world re-reads rank 0 and is not added)
+    const float* const xb = reinterpret_cast<const float*>(own) + (int64_t)par * world * xstride;
+    auto world_sum = [&](int pos) {
+        float w8[WMAX];
+#pragma unroll
+        for (int r = 0; r < WMAX; ++r)
+            w8[r] = __hip_atomic_load(xb + (int64_t)(r < world ? r : 0) * xstride + pos, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+        float g = w8[0];
+#pragma unroll
+        for (int r = 1; r < WMAX; ++r) g = r < world ? g + w8[r] : g;
+        return g;
+    };
+    const float gsum = world_sum(mypos);
+    if (blk == 0 && lane == 0 && loss_out) loss_out[0] = world_sum(mb.n_slab);
+    if (pp < 0) return;  // padding position (dummy layer-0 K slots)
+    adam_pack_pre(pp, gsum, ain, mb, oa, lr_t, ema_debias);
+}
+
+// WAIT: the fused form (push, then wait + sum + Adam in the same wave); !WAIT: the split path's first kernel (reduce +
+// push only, Adam state not loaded), for ranks that share a device (nrc_peer_exchange_open): a wave that waits inside
+// the reduction holds CU resources the co-located rank's gradient pass may need before it can push (a 2-process test
+// on one GPU timed out that way), while the split apply kernel waits in a small grid.
+template <bool H, int WMAX, bool WAIT>
 __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const float* __restrict__ slabs, int nslabs,
                                                                       const float* __restrict__ loss_partials,
                                                                       PeerPtrs dst, size_t region, int rank, int world,
@@ -4106,7 +4151,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const floa
     auto ldc = [&](int k) -> f4 { return ld(min(grp + k * kRedGroups, nslabs - 1)); };
     const int pp = threadIdx.x < kRedParams * kRedVec ? pp_raw : -1;
     AdamIn ain{};
-    if (pp >= 0) ain = adam_load(pp, mb);
+    if (WAIT && pp >= 0) ain = adam_load(pp, mb);
     f4 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = ldc(u);
@@ -4147,52 +4192,58 @@ __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const floa
                             ((int64_t)par * nblk + blk) * kPeerMaxRanks + rank;
         if (lane == 0) __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // wait for every rank's block blk (one flag per lane; lanes past the world re-read flag 0); wave-uniform, no store
-    const char* const own = reinterpret_cast<const char*>(dst.p[rank]) + region;
-    const uint32_t* const fw = reinterpret_cast<const uint32_t*>(own) + flag_base +
-                               ((int64_t)par * nblk + blk) * kPeerMaxRanks + (lane < world ? lane : 0);
-    int i = 0;
-    for (; i < (1 << 21); ++i) {
-        const bool ready = __hip_atomic_load(fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
-        if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;
-        if (i < 4096) __builtin_amdgcn_s_sleep(1);
-        else __builtin_amdgcn_s_sleep(127);
-    }
-    if (i == (1 << 21) && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // the world sum in rank order (branch-free: a rank past the world re-reads rank 0 and is not added)
-    const float* const xb = reinterpret_cast<const float*>(own) + (int64_t)par * world * xstride;
-    auto world_sum = [&](int pos) {
-        float w8[WMAX];
-#pragma unroll
-        for (int r = 0; r < WMAX; ++r)
-            w8[r] = __hip_atomic_load(xb + (int64_t)(r < world ? r : 0) * xstride + pos, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-        float g = w8[0];
-#pragma unroll
-        for (int r = 1; r < WMAX; ++r) g = r < world ? g + w8[r] : g;
-        return g;
-    };
-    const float gsum = world_sum(mypos);
-    if (blk == 0 && lane == 0 && loss_out) loss_out[0] = world_sum(mb.n_slab);
-    if (pp < 0) return;  // padding position (dummy layer-0 K slots)
-    adam_pack_pre(pp, gsum, ain, mb, oa, lr_t, ema_debias);
+    if constexpr (WAIT)
+        exchange_wait_apply<WMAX>(reinterpret_cast<const char*>(dst.p[rank]) + region, lane, blk, nblk, par, world,
+                                  xstride, pp, seq, err, loss_out, ain, mb, oa, lr_t, ema_debias);
+}
+
+// The split path's second kernel: 4 waves per block, wave w of block b takes chunk 4b + w (the fused kernel's second
+// half): 92 blocks of 256 threads for the Frequency slab, the footprint of round 4's first apply kernel.
+template <bool H, int WMAX>
+__global__ __launch_bounds__(256) void exchange_apply_kernel(const char* __restrict__ own, int nblk, int world,
+                                                             uint32_t seq, uint32_t* err, float* loss_out,
+                                                             ModelBuffers mb, OptimArgs oa, float lr_t,
+                                                             float ema_debias) {
+    const int lane = threadIdx.x & 63;
+    const int blk = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (blk >= nblk) return;  // wave-uniform
+    const int mypos = blk * kRedParams * kRedVec + lane;
+    int pp;
+    if constexpr (H) pp = t16_slab_param(mypos);
+    else pp = mb.slab_param[mypos];
+    AdamIn ain{};
+    if (pp >= 0) ain = adam_load(pp, mb);
+    exchange_wait_apply<WMAX>(own, lane, blk, nblk, (int)(seq & 1u), world, px_stride(mb.n_slab), pp, seq, err, loss_out,
+                              ain, mb, oa, lr_t, ema_debias);
 }
 
 hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
                                   int rank, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
-                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
+                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, bool split) {
     if (world < 1 || world > kPeerMaxRanks || rank < 0 || rank >= world || !err || nslabs < 1) return hipErrorInvalidValue;
     for (int r = 0; r < world; ++r)
         if (!dst.p[r]) return hipErrorInvalidValue;
     float lr_t, ema_debias;
     adam_host_factors(oa, lr_t, ema_debias);
-    const dim3 grid(mb.n_slab / (kRedParams * kRedVec));
+    const int nblk = mb.n_slab / (kRedParams * kRedVec);
     const size_t region = px_region_offset(world, nfl);
+    const char* own = reinterpret_cast<const char*>(dst.p[rank]) + region;
 #define NRC_RX(HH, W)                                                                                                   \
-    hipLaunchKernelGGL((reduce_exchange_kernel<HH, W>), grid, dim3(kRedThreads), 0, s, slabs, nslabs, loss_partials,    \
-                       dst, region, rank, world, seq, err, loss_out, mb, oa, lr_t, ema_debias)
-#define NRC_RXW(HH)            \
-    if (world <= 2) NRC_RX(HH, 2); \
+    do {                                                                                                                \
+        if (split) {                                                                                                    \
+            hipLaunchKernelGGL((reduce_exchange_kernel<HH, W, false>), dim3(nblk), dim3(kRedThreads), 0, s, slabs,      \
+                               nslabs, loss_partials, dst, region, rank, world, seq, err, loss_out, mb, oa, lr_t,       \
+                               ema_debias);                                                                             \
+            hipLaunchKernelGGL((exchange_apply_kernel<HH, W>), dim3((nblk + 3) / 4), dim3(256), 0, s, own, nblk, world, \
+                               seq, err, loss_out, mb, oa, lr_t, ema_debias);                                           \
+        } else {                                                                                                        \
+            hipLaunchKernelGGL((reduce_exchange_kernel<HH, W, true>), dim3(nblk), dim3(kRedThreads), 0, s, slabs,       \
+                               nslabs, loss_partials, dst, region, rank, world, seq, err, loss_out, mb, oa, lr_t,       \
+                               ema_debias);                                                                             \
+        }                                                                                                               \
+    } while (0)
+#define NRC_RXW(HH)                     \
+    if (world <= 2) NRC_RX(HH, 2);      \
     else if (world <= 4) NRC_RX(HH, 4); \
     else if (world <= 8) NRC_RX(HH, 8); \
     else NRC_RX(HH, 16)

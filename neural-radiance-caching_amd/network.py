@@ -58,6 +58,9 @@ class HyperParams:
     learningRate: float
 
 
+_DTYPE_OK: dict = {}  # dtype objects already checked against each dtype name
+
+
 def _dev_ptr(x, what: str, min_elems: int | None = None, dtype: str = "torch.float32") -> int:
     if x is None:
         raise ValueError(f"{what}: null buffer")
@@ -67,8 +70,11 @@ def _dev_ptr(x, what: str, min_elems: int | None = None, dtype: str = "torch.flo
     if hasattr(x, "data_ptr"):
         if not x.is_cuda:
             raise ValueError(f"{what}: tensor must live on the GPU")
-        if str(x.dtype) != dtype:
-            raise ValueError(f"{what}: tensor must be {dtype.split('.')[-1]}")
+        dt = x.dtype
+        if dt not in _DTYPE_OK.get(dtype, ()):  # the string compare only once per dtype (a hot-path call)
+            if str(dt) != dtype:
+                raise ValueError(f"{what}: tensor must be {dtype.split('.')[-1]}")
+            _DTYPE_OK.setdefault(dtype, set()).add(dt)
         if not x.is_contiguous():
             raise ValueError(f"{what}: tensor must be contiguous")
         if min_elems is not None and x.numel() < min_elems:

@@ -206,7 +206,9 @@ def test_two_ranks_on_one_gpu_gloo_hash_exact(tmp_path, nrc, torch, dev):
 def test_two_ranks_on_one_gpu_peer_exchange(tmp_path, nrc, torch, dev, golden, B, path):
     """The one-shot peer exchange (nrc_peer_exchange_*): two processes on cuda:0, IPC handles
     all-gathered over gloo, nrc_train_dp pushing each rank's gradient into the other's receive buffer and summing in
-    rank order -- fused into the reduction ("peer", production) or as reduce / push / apply launches ("peer_push").
+    rank order -- "peer": the production choice, which for ranks sharing a device is the split form of the exchange
+    fused into the reduction (reduce + push, then wait + sum + Adam; the fused single launch is exercised by the world-1
+    test below), "peer_push": round 4's first version (reduce / push / apply launches).
     Replicas bit-identical, and bitwise the single-process step that sums the two shards' gradients
     (g0 + g1, one f32 addition -- also what a 2-rank RCCL all-reduce computes) and applies them with nrc_train_apply."""
     port = _free_port()

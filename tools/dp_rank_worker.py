@@ -8,7 +8,8 @@ global_batch (default 16,384) is split over the ranks; 4,096 gives configs[3]'s 
 encoding Hash: the exact grid exchange (DataParallelTrainer with an int64 grid_fixed buffer).
 exchange "peer": the library's one-shot peer exchange (nrc_peer_exchange_*, handles all-gathered over gloo) through
 nrc_train_dp instead of the Python all-reduce, fused into the reduction (the production path); "peer_push": the same
-exchange as separate reduce / push / apply launches (knob peer_path = 0).
+exchange as separate reduce / push / apply launches (knob peer_path = 0). Both ranks share cuda:0, so "peer" runs
+the split form of the fused exchange (nrc_peer_exchange_open detects the shared device).
 """
 import os
 import sys
