@@ -4048,71 +4048,74 @@ __global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict
 // The exchange fused into the reduction (round 4): one launch after the gradient pass replaces reduce (kReduceOnly) +
 // peer_push_kernel + peer_apply_kernel. Block i of every rank reduces the same 64 slab positions (the slab map is the
 // same on every rank), so the exchange runs per block: wave 0 of block i stores its 64 reduced partials -- slab order,
-// one contiguous 256-B store per destination -- into slot [par][rank] of every rank's buffer, waits for those stores
-// (uncached memory: acknowledged = in memory), raises flag [par][i][rank] in each of them, then polls its own buffer's
-// flags [par][i][0..world) and sums the world's partials in rank order before the same Adam/EMA as kReduceFused.
-// A block waits only for the blocks of the same index on the other ranks, which store before they wait: no cycle,
-// whatever the residency. The Adam state is loaded with the slab loads, before the wait. Buffer layout after the
-// push/apply region's (peer_buffer_bytes): data [2][world][xstride] f32 (slab order, the loss at n_slab), flags
-// [2][nblk][kPeerMaxRanks] u32. The parity argument of the push/apply pair holds per block: a rank's step k kernel
-// starts after all its blocks of step k - 1 saw every peer's step k - 1 flags, which those peers raised after their
-// step k - 2 kernels (and reads) had ended.
+// one contiguous 512-B store per destination -- into slot [par][rank] of every rank's buffer, then polls its own
+// buffer's slots [par][0..world) at its positions and sums the world's partials in rank order before the same
+// Adam/EMA as kReduceFused. Every element is a tagged 8-byte word (f32 value | step sequence number << 32), written
+// with one 64-bit store and read with one 64-bit load (single-copy atomic; RCCL's LL protocol rests on the same
+// property of xGMI): a reader that sees the tag sees the value, so there is no flag, no store acknowledgement to wait
+// for before a flag and no second load after it -- one memory round trip where the flag protocol took three (the
+// first fused version: 10.8 us per world-1 step, profiles/r04_fused/). A block waits only for the blocks of the same
+// index on the other ranks, which store before they wait: no cycle, whatever the residency (ranks sharing a device
+// take the split form below). The Adam state is loaded with the slab loads, before the wait. Buffer layout after the
+// push/apply region's (peer_buffer_bytes): [2][world][xstride] tagged words (slab order, the loss at n_slab). Two
+// parities suffice as for the push/apply pair: a rank's step k kernel starts after all its blocks of step k - 1 saw
+// every peer's step k - 1 words, which those peers stored after their step k - 2 kernels (and reads) had ended.
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ constexpr int px_stride(int n_slab) { return (n_slab + 1 + 63) / 64 * 64; }
 size_t px_region_offset(int world, int nfl) {
     return sizeof(float) * ((size_t)2 * world * peer_stride(nfl)) + sizeof(uint32_t) * 2 * world * kPeerSplit * kPeerFlagStride;
 }
 size_t peer_buffer_bytes(int world, int nfl, int n_slab) {
-    const int nblk = n_slab / (kRedParams * kRedVec);
-    return px_region_offset(world, nfl) + sizeof(float) * (size_t)2 * world * px_stride(n_slab) +
-           sizeof(uint32_t) * (size_t)2 * nblk * kPeerMaxRanks;
+    return px_region_offset(world, nfl) + sizeof(uint64_t) * (size_t)2 * world * px_stride(n_slab);
+}
+__device__ __forceinline__ uint64_t px_word(float v, uint32_t seq) {
+    return ((uint64_t)seq << 32) | (uint64_t)__builtin_bit_cast(uint32_t, v);
 }
 
 // Wave-level second half of the exchange for chunk blk (64 slab positions, one per lane; this wave's lane = position
-// blk * 64 + lane): wait for every rank's flag of the chunk, sum the world's partials in rank order, Adam/EMA. ain: the
-// position's Adam state, loaded before the wait. Shared by the fused kernel and the split path's apply kernel.
+// blk * 64 + lane): wait until every rank's word at the lane's position (and, for chunk 0, the loss) carries this step's
+// tag, sum the world's partials in rank order, Adam/EMA. ain: the position's Adam state, loaded before the wait.
+// Shared by the fused kernel and the split path's apply kernel.
 template <int WMAX>
-__device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, int blk, int nblk, int par, int world,
+__device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, int blk, int par, int world,
                                                     int xstride, int pp, uint32_t seq, uint32_t* err, float* loss_out,
                                                     const AdamIn& ain, const ModelBuffers& mb, const OptimArgs& oa,
                                                     float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
-    const int64_t flag_base = (int64_t)2 * world * xstride;
     const int mypos = blk * kRedParams * kRedVec + lane;
-    // one flag per lane (lanes past the world re-read flag 0); wave-uniform loop, no store
-    const uint32_t* const fw = reinterpret_cast<const uint32_t*>(own) + flag_base +
-                               ((int64_t)par * nblk + blk) * kPeerMaxRanks + (lane < world ? lane : 0);
+    // lane 0 of chunk 0 also waits for the loss words (position n_slab), every other lane re-reads its own position
+    const bool has_loss = blk == 0 && lane == 0 && loss_out;
+    const uint64_t* const xb = reinterpret_cast<const uint64_t*>(own) + (int64_t)par * world * xstride;
+    uint64_t w[WMAX], wl[WMAX];
     int i = 0;
     for (; i < (1 << 21); ++i) {
-        const bool ready = __hip_atomic_load(fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
-        if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;
+        bool ready = true;
+#pragma unroll
+        for (int r = 0; r < WMAX; ++r) {
+            const int64_t row = (int64_t)(r < world ? r : 0) * xstride;  // a rank past the world re-reads rank 0
+            w[r] = __hip_atomic_load(xb + row + mypos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            wl[r] = __hip_atomic_load(xb + row + (has_loss ? mb.n_slab : mypos), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+            ready = ready && (uint32_t)(w[r] >> 32) == seq && (uint32_t)(wl[r] >> 32) == seq;
+        }
+        if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;  // wave-uniform, no store in the loop
         if (i < 4096) __builtin_amdgcn_s_sleep(1);
         else __builtin_amdgcn_s_sleep(127);
     }
     if (i == (1 << 21) && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // the world sum in rank order (branch-free: a rank past the world re-reads rank 0 and is not added)
-    const float* const xb = reinterpret_cast<const float*>(own) + (int64_t)par * world * xstride;
-    auto world_sum = [&](int pos) {
-        float w8[WMAX];
+    // the world sum in rank order (branch-free: a rank past the world is not added)
+    auto world_sum = [&](const uint64_t (&v)[WMAX]) {
+        float g = __builtin_bit_cast(float, (uint32_t)v[0]);
 #pragma unroll
-        for (int r = 0; r < WMAX; ++r)
-            w8[r] = __hip_atomic_load(xb + (int64_t)(r < world ? r : 0) * xstride + pos, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-        float g = w8[0];
-#pragma unroll
-        for (int r = 1; r < WMAX; ++r) g = r < world ? g + w8[r] : g;
+        for (int r = 1; r < WMAX; ++r) g = r < world ? g + __builtin_bit_cast(float, (uint32_t)v[r]) : g;
         return g;
     };
-    const float gsum = world_sum(mypos);
-    if (blk == 0 && lane == 0 && loss_out) loss_out[0] = world_sum(mb.n_slab);
+    const float gsum = world_sum(w);
+    if (has_loss) loss_out[0] = world_sum(wl);
     if (pp < 0) return;  // padding position (dummy layer-0 K slots)
     adam_pack_pre(pp, gsum, ain, mb, oa, lr_t, ema_debias);
 }
 
-// WAIT: the fused form (push, then wait + sum + Adam in the same wave); !WAIT: the split path's first kernel (reduce +
-// push only, Adam state not loaded), for ranks that share a device (nrc_peer_exchange_open): a wave that waits inside
-// the reduction holds CU resources the co-located rank's gradient pass may need before it can push (a 2-process test
-// on one GPU timed out that way), while the split apply kernel waits in a small grid.
 template <bool H, int WMAX, bool WAIT>
 __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const float* __restrict__ slabs, int nslabs,
                                                                       const float* __restrict__ loss_partials,
@@ -4177,24 +4180,20 @@ __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const floa
 #pragma unroll
     for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][lp][comp] + part[2 * u + 1][lp][comp];
     const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
-    // push: slot [par][rank] of every rank (own buffer included), then the loss (block 0)
+    // push: slot [par][rank] of every rank (own buffer included) as tagged words, then the loss (block 0); no wait,
+    // no flag (px_word). dst.p is indexed by a wave-uniform rank: a per-lane index into the kernel-argument array
+    // would go through scratch.
+    const uint64_t word = px_word(g1, seq), lword = px_word(L, seq);
     for (int r = 0; r < world; ++r) {
-        float* const d = reinterpret_cast<float*>(reinterpret_cast<char*>(dst.p[r]) + region) +
-                         ((int64_t)par * world + rank) * xstride;
-        d[mypos] = g1;
-        if (blk == 0 && lane == 0) d[mb.n_slab] = L;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int64_t flag_base = (int64_t)2 * world * xstride;  // u32 index of flag [0][0][0] in the region
-    // (dst.p indexed by a wave-uniform rank: a per-lane index into the kernel-argument array would go through scratch)
-    for (int r = 0; r < world; ++r) {
-        uint32_t* const f = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(dst.p[r]) + region) + flag_base +
-                            ((int64_t)par * nblk + blk) * kPeerMaxRanks + rank;
-        if (lane == 0) __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint64_t* const d = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(dst.p[r]) + region) +
+                            ((int64_t)par * world + rank) * xstride;
+        __hip_atomic_store(d + mypos, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (blk == 0 && lane == 0) __hip_atomic_store(d + mb.n_slab, lword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if constexpr (WAIT)
-        exchange_wait_apply<WMAX>(reinterpret_cast<const char*>(dst.p[rank]) + region, lane, blk, nblk, par, world,
-                                  xstride, pp, seq, err, loss_out, ain, mb, oa, lr_t, ema_debias);
+        exchange_wait_apply<WMAX>(reinterpret_cast<const char*>(dst.p[rank]) + region, lane, blk, par, world, xstride,
+                                  pp, seq, err, loss_out, ain, mb, oa, lr_t, ema_debias);
+    (void)nblk;
 }
 
 // The split path's second kernel: 4 waves per block, wave w of block b takes chunk 4b + w (the fused kernel's second
@@ -4213,8 +4212,8 @@ __global__ __launch_bounds__(256) void exchange_apply_kernel(const char* __restr
     else pp = mb.slab_param[mypos];
     AdamIn ain{};
     if (pp >= 0) ain = adam_load(pp, mb);
-    exchange_wait_apply<WMAX>(own, lane, blk, nblk, (int)(seq & 1u), world, px_stride(mb.n_slab), pp, seq, err, loss_out,
-                              ain, mb, oa, lr_t, ema_debias);
+    exchange_wait_apply<WMAX>(own, lane, blk, (int)(seq & 1u), world, px_stride(mb.n_slab), pp, seq, err, loss_out, ain,
+                              mb, oa, lr_t, ema_debias);
 }
 
 hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
