@@ -366,15 +366,18 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
 
 def dp_exchange_bench(nrc, net, dev, world: int, rank: int, frames_q, frames_t, b0: int, bn: int, frames: int,
                       barrier, max_over_ranks) -> dict:
-    """N > 1: the same training frames through the library's one-shot peer exchange (nrc_peer_exchange_*: each rank
-    stores its gradient into every peer's receive buffer over xGMI, the Adam kernel sums them in rank order) instead of
+    """N > 1: the same training frames through the library's one-shot peer exchange (nrc_peer_exchange_*: each rank's
+    slab reduction stores its partials into every peer's receive buffer over xGMI and sums the world's in rank order
+    before Adam) instead of
     the RCCL all-reduce -- per step for configs[3]'s split minibatch (b_local = 16,384 / N) and weak-scaled (16,384 per
     rank, global batch N x 16,384). A setup or exchange failure is recorded, not raised (the inference line stands)."""
     import torch
     import torch.distributed as dist
 
     B = nrc.BATCH_SIZE
-    res = {"exchange": "peer (IPC-mapped uncached receive buffers, xGMI stores, rank-order sum fused into Adam)"}
+    res = {"exchange": "peer exchange inside the slab reduction (IPC-mapped uncached receive buffers, xGMI stores of "
+                       "tagged 8-byte words, rank-order sum + Adam in the same launch; the split form when ranks share "
+                       "a device)"}
     ok = torch.ones(1, dtype=torch.int32, device=dev)
     try:
         nrc.dp.open_peer_exchange(net)
