@@ -309,8 +309,9 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
     step0 = net.step
     tq, tt = frames_q[0], frames_t[0]
     k = 4 * iters
-    # the production data-parallel path: the one-shot peer exchange fused into the reduction, at world 1 (the rank's
-    # own buffer: every store, flag and poll of the N-rank step, without the xGMI hop)
+    # the production data-parallel path: the peer exchange fused into the reduction, at world 1. A rank keeps its own
+    # partials in registers, so at world 1 nothing crosses memory: this is the per-rank gradient pass + reduction +
+    # Adam of the N-rank step; the wait for the other ranks' words is the prediction's assumed xGMI term below.
     peer_ms = None
     try:
         net.peer_exchange_open(0, 1, net.peer_exchange_handle(1))
@@ -355,8 +356,8 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
                 "xgmi_us_assumed": xgmi_assumed_us,
                 "train_step_ms_8gpu": dp_step + xgmi_assumed_us * 1e-3,
                 "train_speedup": step16k_ms / (dp_step + xgmi_assumed_us * 1e-3),
-                "train_what": "1-GPU 16384-sample step / (per-rank world-1 peer-exchange step + an ASSUMED xGMI "
-                              "store + flag latency; unmeasured on 8 GPUs)",
+                "train_what": "1-GPU 16384-sample step / (per-rank world-1 peer-exchange step + an ASSUMED wait for "
+                              "the other ranks' words over xGMI; unmeasured on 8 GPUs)",
                 "allreduce_us_assumed": allreduce_assumed_us,
                 "train_step_ms_8gpu_rccl": grad_ms + apply_ms + allreduce_assumed_us * 1e-3,
                 "train_speedup_rccl": step16k_ms / (grad_ms + apply_ms + allreduce_assumed_us * 1e-3),

@@ -4075,12 +4075,13 @@ __device__ __forceinline__ uint64_t px_word(float v, uint32_t seq) {
 // Wave-level second half of the exchange for chunk blk (64 slab positions, one per lane; this wave's lane = position
 // blk * 64 + lane): wait until every rank's word at the lane's position (and, for chunk 0, the loss) carries this step's
 // tag, sum the world's partials in rank order, Adam/EMA. ain: the position's Adam state, loaded before the wait.
-// Shared by the fused kernel and the split path's apply kernel.
-template <int WMAX>
-__device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, int blk, int par, int world,
+// Shared by the fused kernel and the split path's apply kernel. OWNREG (fused): this rank's own partial and loss are
+// the registers mine / mine_l (never stored to nor read back from memory), so only the other ranks' words are awaited.
+template <int WMAX, bool OWNREG>
+__device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, int blk, int par, int rank, int world,
                                                     int xstride, int pp, uint32_t seq, uint32_t* err, float* loss_out,
-                                                    const AdamIn& ain, const ModelBuffers& mb, const OptimArgs& oa,
-                                                    float lr_t, float ema_debias) {
+                                                    float mine, float mine_l, const AdamIn& ain, const ModelBuffers& mb,
+                                                    const OptimArgs& oa, float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
     const int mypos = blk * kRedParams * kRedVec + lane;
     // lane 0 of chunk 0 also waits for the loss words (position n_slab), every other lane re-reads its own position
@@ -4088,21 +4089,33 @@ __device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, i
     const uint64_t* const xb = reinterpret_cast<const uint64_t*>(own) + (int64_t)par * world * xstride;
     uint64_t w[WMAX], wl[WMAX];
     int i = 0;
-    for (; i < (1 << 21); ++i) {
+    // OWNREG at world 1: nothing to wait for (the loop would only re-read a row that is never awaited)
+    for (; i < (1 << 21) && !(OWNREG && world == 1); ++i) {
         bool ready = true;
 #pragma unroll
         for (int r = 0; r < WMAX; ++r) {
-            const int64_t row = (int64_t)(r < world ? r : 0) * xstride;  // a rank past the world re-reads rank 0
+            // a rank past the world (and, OWNREG, this rank) re-reads a row that is never awaited: the other rank's, so
+            // that the loads stay branch-free
+            const bool skip = r >= world || (OWNREG && r == rank);
+            const int64_t row = (int64_t)(r < world ? r : 0) * xstride;
             w[r] = __hip_atomic_load(xb + row + mypos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             wl[r] = __hip_atomic_load(xb + row + (has_loss ? mb.n_slab : mypos), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_SYSTEM);
-            ready = ready && (uint32_t)(w[r] >> 32) == seq && (uint32_t)(wl[r] >> 32) == seq;
+            ready = ready && (skip || ((uint32_t)(w[r] >> 32) == seq && (uint32_t)(wl[r] >> 32) == seq));
         }
         if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;  // wave-uniform, no store in the loop
         if (i < 4096) __builtin_amdgcn_s_sleep(1);
         else __builtin_amdgcn_s_sleep(127);
     }
     if (i == (1 << 21) && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if constexpr (OWNREG) {
+#pragma unroll
+        for (int r = 0; r < WMAX; ++r)
+            if (r == rank) {
+                w[r] = px_word(mine, seq);
+                wl[r] = px_word(mine_l, seq);
+            }
+    }
     // the world sum in rank order (branch-free: a rank past the world is not added)
     auto world_sum = [&](const uint64_t (&v)[WMAX]) {
         float g = __builtin_bit_cast(float, (uint32_t)v[0]);
@@ -4180,19 +4193,21 @@ __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const floa
 #pragma unroll
     for (int u = 0; u < 8; ++u) t8[u] = part[2 * u][lp][comp] + part[2 * u + 1][lp][comp];
     const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
-    // push: slot [par][rank] of every rank (own buffer included) as tagged words, then the loss (block 0); no wait,
-    // no flag (px_word). dst.p is indexed by a wave-uniform rank: a per-lane index into the kernel-argument array
-    // would go through scratch.
+    // push: slot [par][rank] of every rank as tagged words, then the loss (block 0); no wait, no flag (px_word). The
+    // fused form keeps its own partials in registers (no own slot written or read); the split form's apply kernel
+    // reads them back. dst.p is indexed by a wave-uniform rank: a per-lane index into the kernel-argument array would
+    // go through scratch.
     const uint64_t word = px_word(g1, seq), lword = px_word(L, seq);
     for (int r = 0; r < world; ++r) {
+        if (WAIT && r == rank) continue;
         uint64_t* const d = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(dst.p[r]) + region) +
                             ((int64_t)par * world + rank) * xstride;
         __hip_atomic_store(d + mypos, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (blk == 0 && lane == 0) __hip_atomic_store(d + mb.n_slab, lword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if constexpr (WAIT)
-        exchange_wait_apply<WMAX>(reinterpret_cast<const char*>(dst.p[rank]) + region, lane, blk, par, world, xstride,
-                                  pp, seq, err, loss_out, ain, mb, oa, lr_t, ema_debias);
+        exchange_wait_apply<WMAX, true>(reinterpret_cast<const char*>(dst.p[rank]) + region, lane, blk, par, rank, world,
+                                        xstride, pp, seq, err, loss_out, g1, L, ain, mb, oa, lr_t, ema_debias);
     (void)nblk;
 }
 
@@ -4212,8 +4227,8 @@ __global__ __launch_bounds__(256) void exchange_apply_kernel(const char* __restr
     else pp = mb.slab_param[mypos];
     AdamIn ain{};
     if (pp >= 0) ain = adam_load(pp, mb);
-    exchange_wait_apply<WMAX>(own, lane, blk, (int)(seq & 1u), world, px_stride(mb.n_slab), pp, seq, err, loss_out, ain,
-                              mb, oa, lr_t, ema_debias);
+    exchange_wait_apply<WMAX, false>(own, lane, blk, (int)(seq & 1u), 0, world, px_stride(mb.n_slab), pp, seq, err,
+                                     loss_out, 0.0f, 0.0f, ain, mb, oa, lr_t, ema_debias);
 }
 
 hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
