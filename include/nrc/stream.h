@@ -9,7 +9,8 @@
  * samples) plus the trace outputs the post-trace kernels read (Device.cpp:1382-1469).
  *
  * Layout (little-endian, no padding, sizes in bytes):
- *   file header   64: "NRCSTRM\0", u32 version (1), u32 header_bytes (64), u32 query_bytes (60),
+ *   file header   64: "NRCSTRM\0", u32 version (1), u32 header_bytes (64), u32 query_bytes (60, or 64 for a stream
+ *                     of padded RadianceQuery records: nrc_stream_create_layout),
  *                     u32 record_bytes (28), u32 end_vertex_bytes (16), u32 float3_bytes (12),
  *                     u32 width, u32 height, u32 capacity (65536), u32 reserved, u64 reserved[2]
  *   per frame:    "FRME" + nrc_stream_frame_header (48) + 12 reserved bytes = 64, then every present
@@ -50,7 +51,8 @@ typedef struct nrc_stream_frame_header {
     uint32_t num_tiles;
     int32_t num_training_records; /* raw trace counter (may exceed capacity) */
     uint32_t sections;            /* bit i set <=> section i present */
-    uint32_t reserved0;
+    uint32_t query_layout;        /* the stream's RadianceQuery layout (NRC_QUERY_COMPACT / NRC_QUERY_PADDED): set by
+                                   * the writer and the reader from the file header; sizes the query sections */
     uint64_t shuffle_seed;
     uint64_t payload_bytes;       /* bytes of all sections that follow; filled in by the writer */
 } nrc_stream_frame_header;
@@ -62,6 +64,12 @@ uint64_t nrc_stream_section_bytes(const nrc_stream_frame_header* hdr, int sectio
 
 /* Create a stream file for writing (truncates). width/height are informational (0 = unknown). */
 nrc_status nrc_stream_create(const char* path, uint32_t width, uint32_t height, nrc_stream** out);
+/* The same for a RadianceQuery layout (nrc_config.query_layout: NRC_QUERY_COMPACT 60-byte or NRC_QUERY_PADDED 64-byte
+ * records in the query sections); nrc_stream_create is the compact layout. */
+nrc_status nrc_stream_create_layout(const char* path, uint32_t width, uint32_t height, uint32_t query_layout,
+                                    nrc_stream** out);
+/* The query layout of an open stream. */
+nrc_status nrc_stream_query_layout(const nrc_stream* s, uint32_t* query_layout);
 /* Open a stream file for reading; width/height may be NULL. */
 nrc_status nrc_stream_open(const char* path, nrc_stream** out, uint32_t* width, uint32_t* height);
 nrc_status nrc_stream_close(nrc_stream* s);

@@ -57,7 +57,8 @@ EXPORTS = [
     "nrc_propagate_train_radiance_factored_padded", "nrc_permute_train_data_padded",
     "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
     # include/nrc/stream.h (bound in stream.py)
-    "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_open", "nrc_stream_close",
+    "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_create_layout", "nrc_stream_query_layout",
+    "nrc_stream_open", "nrc_stream_close",
     "nrc_stream_write_frame", "nrc_stream_next_frame", "nrc_stream_read_section",
 ]
 

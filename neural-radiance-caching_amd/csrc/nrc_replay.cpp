@@ -174,6 +174,8 @@ int main(int argc, char** argv) {
     nrc_stream_frame_header h{};
     int eos = 0;
     uint32_t max_screen = 0, max_tiles = 0;
+    uint32_t query_layout = NRC_QUERY_COMPACT;  // the stream's RadianceQuery records: the handle is made to match
+    NRC(nrc_stream_query_layout(s, &query_layout));
     long frames = 0;
     for (;;) {
         NRC(nrc_stream_next_frame(s, &h, &eos));
@@ -193,16 +195,17 @@ int main(int argc, char** argv) {
     HIP(hipStreamCreate(&stream));
     const size_t cap = NRC_NUM_TRAINING_RECORDS_PER_FRAME;
     const size_t nq = (size_t)max_screen + max_tiles;
+    const size_t QD = query_layout == NRC_QUERY_PADDED ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS;
     nrc_frame_buffers fb{};
-    float* queries_inference = dalloc<float>(nq * NRC_INPUT_DIMS);
+    float* queries_inference = dalloc<float>(nq * QD);
     nrc_float3* results_inference = dalloc<nrc_float3>(nq);
     nrc_float3* throughput = dalloc<nrc_float3>(max_screen);
     float* output = dalloc<float>((size_t)max_screen * 4);
-    float* queries_vis = dalloc<float>((size_t)max_screen * NRC_INPUT_DIMS);
+    float* queries_vis = dalloc<float>((size_t)max_screen * QD);
     nrc_float3* results_vis = dalloc<nrc_float3>(max_screen);
     nrc_train_suffix_end_vertex* ends = dalloc<nrc_train_suffix_end_vertex>(max_tiles);
     nrc_training_record* records = dalloc<nrc_training_record>(cap);
-    float* tq[2] = {dalloc<float>(cap * NRC_INPUT_DIMS), dalloc<float>(cap * NRC_INPUT_DIMS)};
+    float* tq[2] = {dalloc<float>(cap * QD), dalloc<float>(cap * QD)};
     nrc_float3* tt[2] = {dalloc<nrc_float3>(cap), dalloc<nrc_float3>(cap)};
     int32_t* perm = dalloc<int32_t>(cap);
     fb.queries_inference_d = queries_inference;
@@ -222,7 +225,9 @@ int main(int argc, char** argv) {
 
     nrc_net* net = nullptr;
     NRC(nrc_create(&net));
-    NRC(nrc_init(net, stream, NRC_ENCODING_FREQUENCY, nullptr, 0));
+    nrc_config cfg = nrc_default_config(NRC_ENCODING_FREQUENCY);
+    cfg.query_layout = query_layout;
+    NRC(nrc_init(net, stream, NRC_ENCODING_FREQUENCY, &cfg, 0));
     void* comm = nullptr;
     if (dp) {
         unsigned char id[NRC_COMM_UNIQUE_ID_BYTES];

@@ -49,6 +49,7 @@ struct nrc_stream {
     FILE* f = nullptr;
     bool writing = false;
     uint32_t width = 0, height = 0;
+    uint32_t query_layout = NRC_QUERY_COMPACT;  // of the query sections (file header query_bytes 60 / 64)
     bool have_frame = false;
     nrc_stream_frame_header cur{};
     int64_t payload_start = 0;
@@ -112,7 +113,8 @@ uint64_t nrc_stream_section_bytes(const nrc_stream_frame_header* h, int section)
     const uint64_t screen = h->screen_size, tiles = h->num_tiles;
     const uint64_t nrec =
         (uint64_t)std::clamp<int64_t>(h->num_training_records, 0, NRC_NUM_TRAINING_RECORDS_PER_FRAME);
-    const uint64_t q = sizeof(float) * NRC_INPUT_DIMS, f3 = sizeof(nrc_float3);
+    const uint64_t q = sizeof(float) * (h->query_layout == NRC_QUERY_PADDED ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS);
+    const uint64_t f3 = sizeof(nrc_float3);
     switch (section) {
     case NRC_SEC_QUERIES_INFERENCE: return (screen + tiles) * q;
     case NRC_SEC_LAST_RENDER_THROUGHPUT: return screen * f3;
@@ -130,8 +132,14 @@ uint64_t nrc_stream_section_bytes(const nrc_stream_frame_header* h, int section)
 }
 
 nrc_status nrc_stream_create(const char* path, uint32_t width, uint32_t height, nrc_stream** out) {
+    return nrc_stream_create_layout(path, width, height, NRC_QUERY_COMPACT, out);
+}
+
+nrc_status nrc_stream_create_layout(const char* path, uint32_t width, uint32_t height, uint32_t query_layout,
+                                    nrc_stream** out) {
     return guarded([&] {
         require(path && out, "NULL argument");
+        require(query_layout == NRC_QUERY_COMPACT || query_layout == NRC_QUERY_PADDED, "unknown query_layout");
         *out = nullptr;
         auto s = std::make_unique<nrc_stream>();
         s->f = fopen(path, "wb");
@@ -139,11 +147,12 @@ nrc_status nrc_stream_create(const char* path, uint32_t width, uint32_t height, 
         s->writing = true;
         s->width = width;
         s->height = height;
+        s->query_layout = query_layout;
         FileHeader fh{};
         std::memcpy(fh.magic, kMagic, 8);
         fh.version = NRC_STREAM_VERSION;
         fh.header_bytes = kHeaderBytes;
-        fh.query_bytes = sizeof(float) * NRC_INPUT_DIMS;
+        fh.query_bytes = sizeof(float) * (query_layout == NRC_QUERY_PADDED ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS);
         fh.record_bytes = sizeof(nrc_training_record);
         fh.end_vertex_bytes = sizeof(nrc_train_suffix_end_vertex);
         fh.float3_bytes = sizeof(nrc_float3);
@@ -166,10 +175,11 @@ nrc_status nrc_stream_open(const char* path, nrc_stream** out, uint32_t* width, 
         require(fread(&fh, 1, sizeof fh, s->f) == sizeof fh, "not an NRC stream (short header)");
         require(std::memcmp(fh.magic, kMagic, 8) == 0, "not an NRC stream (bad magic)");
         require(fh.version == NRC_STREAM_VERSION, "unsupported stream version " + std::to_string(fh.version));
-        require(fh.header_bytes == kHeaderBytes && fh.query_bytes == 60 && fh.record_bytes == 28 &&
-                    fh.end_vertex_bytes == 16 && fh.float3_bytes == 12,
+        require(fh.header_bytes == kHeaderBytes && (fh.query_bytes == 60 || fh.query_bytes == 64) &&
+                    fh.record_bytes == 28 && fh.end_vertex_bytes == 16 && fh.float3_bytes == 12,
                 "stream record sizes do not match this build");
         require(fh.capacity == NRC_NUM_TRAINING_RECORDS_PER_FRAME, "stream capacity does not match this build");
+        s->query_layout = fh.query_bytes == 64 ? NRC_QUERY_PADDED : NRC_QUERY_COMPACT;
         s->width = fh.width;
         s->height = fh.height;
         if (width) *width = fh.width;
@@ -195,7 +205,7 @@ nrc_status nrc_stream_write_frame(nrc_stream* s, const nrc_stream_frame_header* 
         nrc_stream_frame_header h = *hdr;
         h.sections = 0;
         h.payload_bytes = 0;
-        h.reserved0 = 0;
+        h.query_layout = s->query_layout;
         for (int i = 0; i < NRC_SEC_COUNT; ++i)
             if (sections && sections[i]) {
                 h.sections |= 1u << i;
@@ -230,6 +240,7 @@ nrc_status nrc_stream_next_frame(nrc_stream* s, nrc_stream_frame_header* hdr, in
         char pad[kFrameHeaderBytes - 4 - sizeof h];
         require(fread(&h, 1, sizeof h, s->f) == sizeof h && fread(pad, 1, sizeof pad, s->f) == sizeof pad,
                 "truncated stream (frame header)");
+        h.query_layout = s->query_layout;  // the file header's record size decides
         uint64_t need = 0;
         for (int i = 0; i < NRC_SEC_COUNT; ++i)
             if (h.sections & (1u << i)) need += nrc_stream_section_bytes(&h, i);
@@ -250,6 +261,13 @@ nrc_status nrc_stream_read_section(nrc_stream* s, int section, void* dst, hipStr
         const uint64_t off = section_offset(s->cur, section);
         require(fseeko(s->f, (off_t)(s->payload_start + (int64_t)off), SEEK_SET) == 0, "seek failed");
         read_bytes(s, dst, nrc_stream_section_bytes(&s->cur, section), stream);
+    });
+}
+
+nrc_status nrc_stream_query_layout(const nrc_stream* s, uint32_t* query_layout) {
+    return guarded([&] {
+        require(s && query_layout, "NULL argument");
+        *query_layout = s->query_layout;
     });
 }
 

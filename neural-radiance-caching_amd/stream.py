@@ -55,13 +55,13 @@ class FrameHeader:
         return max(0, min(self.num_training_records, CAPACITY))
 
 
-def section_shape(h: FrameHeader, sec: int):
-    """(count, dtype, row shape) of a section."""
-    s, t, n = h.screen_size, h.num_tiles, h.nrec
+def section_shape(h: FrameHeader, sec: int, query_dims: int = 15):
+    """(count, dtype, row shape) of a section (query_dims: 15 compact / 16 padded RadianceQuery records)."""
+    s, t, n, qd = h.screen_size, h.num_tiles, h.nrec, int(query_dims)
     return {
-        QUERIES_INFERENCE: (s + t, np.float32, (15,)), LAST_RENDER_THROUGHPUT: (s, np.float32, (3,)),
-        QUERIES_CACHE_VIS: (s, np.float32, (15,)), END_VERTICES: (t, END_VERTEX_DTYPE, ()),
-        TRAIN_RECORDS: (n, TRAINING_RECORD_DTYPE, ()), TRAIN_QUERIES: (n, np.float32, (15,)),
+        QUERIES_INFERENCE: (s + t, np.float32, (qd,)), LAST_RENDER_THROUGHPUT: (s, np.float32, (3,)),
+        QUERIES_CACHE_VIS: (s, np.float32, (qd,)), END_VERTICES: (t, END_VERTEX_DTYPE, ()),
+        TRAIN_RECORDS: (n, TRAINING_RECORD_DTYPE, ()), TRAIN_QUERIES: (n, np.float32, (qd,)),
         TRAIN_TARGETS: (n, np.float32, (3,)), PERMUTATION: (CAPACITY, np.int32, ()),
         RESULTS_INFERENCE: (s + t, np.float32, (3,)), OUTPUT_RGBA: (s, np.float32, (4,)),
         LOSSES: (NUM_BATCHES, np.float32, ()),
@@ -140,7 +140,7 @@ class _CHeader(ctypes.Structure):
     _fields_ = [("frame_index", ctypes.c_uint32), ("iteration_index", ctypes.c_uint32),
                 ("render_mode", ctypes.c_int32), ("screen_size", ctypes.c_uint32), ("num_tiles", ctypes.c_uint32),
                 ("num_training_records", ctypes.c_int32), ("sections", ctypes.c_uint32),
-                ("reserved0", ctypes.c_uint32), ("shuffle_seed", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64)]
+                ("query_layout", ctypes.c_uint32), ("shuffle_seed", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64)]
 
 
 def _sigs():
@@ -152,6 +152,8 @@ def _sigs():
     L.nrc_stream_section_bytes.argtypes = [ctypes.POINTER(_CHeader), ctypes.c_int]
     for name, args in {
         "nrc_stream_create": [ctypes.c_char_p, u32, u32, ctypes.POINTER(vp)],
+        "nrc_stream_create_layout": [ctypes.c_char_p, u32, u32, u32, ctypes.POINTER(vp)],
+        "nrc_stream_query_layout": [vp, ctypes.POINTER(u32)],
         "nrc_stream_open": [ctypes.c_char_p, ctypes.POINTER(vp), ctypes.POINTER(u32), ctypes.POINTER(u32)],
         "nrc_stream_close": [vp],
         "nrc_stream_write_frame": [vp, ctypes.POINTER(_CHeader), ctypes.POINTER(vp), vp],
@@ -185,18 +187,25 @@ def _from_c(c: _CHeader) -> FrameHeader:
 
 
 class CStream:
-    """The C-ABI stream (csrc/nrc_stream.cpp). Buffers may be numpy arrays or device tensors / addresses."""
+    """The C-ABI stream (csrc/nrc_stream.cpp). Buffers may be numpy arrays or device tensors / addresses.
+    query_layout (writing): 0 compact (15-float records), 1 padded (16-float, USE_COMPACT_RADIANCE_QUERY 0); a reader
+    takes it from the file."""
 
-    def __init__(self, path, mode: str = "r", width: int = 0, height: int = 0):
+    def __init__(self, path, mode: str = "r", width: int = 0, height: int = 0, query_layout: int = 0):
         L = _sigs()
         self._h = ctypes.c_void_p()
         if mode == "w":
-            check(L.nrc_stream_create(str(path).encode(), width, height, ctypes.byref(self._h)))
+            check(L.nrc_stream_create_layout(str(path).encode(), width, height, int(query_layout),
+                                             ctypes.byref(self._h)))
             self.width, self.height = width, height
         else:
             w, h = ctypes.c_uint32(), ctypes.c_uint32()
             check(L.nrc_stream_open(str(path).encode(), ctypes.byref(self._h), ctypes.byref(w), ctypes.byref(h)))
             self.width, self.height = w.value, h.value
+        ql = ctypes.c_uint32()
+        check(L.nrc_stream_query_layout(self._h, ctypes.byref(ql)))
+        self.query_layout = ql.value
+        self.query_dims = 16 if ql.value == 1 else 15
         self._cur = None
 
     def write_frame(self, header: FrameHeader, sections: dict, stream=None) -> None:
@@ -216,7 +225,7 @@ class CStream:
     def read_section(self, sec: int, dst=None, stream=None):
         """Into dst (numpy array / device tensor / address); with dst None a new numpy array is returned."""
         if dst is None:
-            n, dt, row = section_shape(self._cur, sec)
+            n, dt, row = section_shape(self._cur, sec, self.query_dims)
             dst = np.empty((n,) + row, dtype=dt)
         s = None if stream is None else int(getattr(stream, "cuda_stream", stream))
         check(_sigs().nrc_stream_read_section(self._h, sec, _addr(dst), s))

@@ -120,3 +120,26 @@ def test_record_synthetic_stream(nrc, tmp_path):
     h, secs = frames[1]
     np.testing.assert_array_equal(secs[S.QUERIES_INFERENCE], f1.queries_inference)
     assert secs[S.TRAIN_RECORDS].tobytes() == f1.train_records[: h.nrec].tobytes()
+
+
+def test_padded_query_layout_roundtrip(nrc, tmp_path):
+    """A stream of padded RadianceQuery records (nrc_stream_create_layout, USE_COMPACT_RADIANCE_QUERY 0): the file header
+    says 64-byte queries, the query sections are 16 floats wide, the reader reports the layout and returns the bytes."""
+    S = nrc.stream
+    p = tmp_path / "padded.nrcs"
+    h, secs = _frame(nrc, seed=3, frame_index=1)
+    for k in (S.QUERIES_INFERENCE, S.QUERIES_CACHE_VIS, S.TRAIN_QUERIES):
+        q = np.asarray(secs[k], np.float32)
+        secs[k] = np.ascontiguousarray(np.insert(q, 3, np.arange(len(q), dtype=np.float32), axis=1))
+    with S.CStream(p, "w", 48, 32, query_layout=1) as cs:
+        assert cs.query_layout == 1
+        cs.write_frame(h, secs)
+    assert int.from_bytes(p.read_bytes()[16:20], "little") == 64  # query_bytes in the file header
+    with S.CStream(p) as cs:
+        assert cs.query_layout == 1 and cs.query_dims == 16
+        got = cs.next_frame()
+        assert got.sections == sum(1 << k for k in secs)
+        for k in secs:
+            assert cs.read_section(k).tobytes() == np.ascontiguousarray(secs[k]).tobytes(), S.SECTION_NAMES[k]
+    with pytest.raises(nrc.NrcError):
+        S.CStream(tmp_path / "x.nrcs", "w", query_layout=2)
