@@ -145,3 +145,33 @@ def test_replay_ranks1_rccl_matches_plain_replay(nrc, dev, tmp_path):
         outs[mode] = ([x["loss"] for x in lines if "frame" in x], out_f.read_bytes(), res_f.read_bytes())
     assert outs["plain"][0] == outs["ranks1"][0]
     assert outs["plain"][1] == outs["ranks1"][1] and outs["plain"][2] == outs["ranks1"][2]
+
+
+def test_cpp_replayer_padded_stream_equals_compact(nrc, dev, tmp_path):
+    """A stream of padded RadianceQuery records (USE_COMPACT_RADIANCE_QUERY 0, pad_ = 1.0 in every record) replays
+    through nrc_replay -- which sizes its buffers and makes its handle from the stream's query layout -- with losses,
+    radiance and frame buffer bitwise those of the compact stream of the same frames: a padded handle with pad_ = 1
+    computes what a compact handle computes (tests/test_gpu_padded.py), and both start from the same seeded weights."""
+    assert REPLAY_BIN.exists(), "nrc_replay not built (make -C neural-radiance-caching_amd)"
+    S = nrc.stream
+    p, q = tmp_path / "compact.nrcs", tmp_path / "padded.nrcs"
+    S.record_synthetic(p, 3, 160, 120, seed=4)
+    with S.CStream(q, "w", 160, 120, query_layout=1) as cs:
+        for h, secs in S.read_stream(p):
+            for k in (S.QUERIES_INFERENCE, S.QUERIES_CACHE_VIS, S.TRAIN_QUERIES):
+                if k in secs:
+                    a = np.asarray(secs[k], np.float32)
+                    secs[k] = np.ascontiguousarray(np.insert(a, 3, np.float32(1.0), axis=1))
+            cs.write_frame(h, {k: np.ascontiguousarray(v) for k, v in secs.items()})
+    outs = []
+    for path in (p, q):
+        out_f, res_f = tmp_path / (path.stem + ".out"), tmp_path / (path.stem + ".res")
+        r = subprocess.run([str(REPLAY_BIN), str(path), "--dump-output", str(out_f), "--dump-results", str(res_f)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        losses = [json.loads(x)["loss"] for x in r.stdout.splitlines() if '"frame"' in x]
+        outs.append((losses, np.fromfile(out_f, np.float32), np.fromfile(res_f, np.float32)))
+    assert len(outs[0][0]) == 3 and all(np.isfinite(outs[0][0]))
+    assert outs[0][0] == outs[1][0]
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_array_equal(outs[0][2], outs[1][2])
