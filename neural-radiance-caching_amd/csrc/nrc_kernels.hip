@@ -3198,6 +3198,11 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         case 57: return launch_persistent_infer(infer_kernel_v2<2, 2, 512, true, 48 | 1024 | 2048>, 512, bpc[57], (ntiles + 1) / 2, queries, out, n, wf, s);
         case 58: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, false, 48 | 1024 | 2048 | 65536 | 262144>, 768, bpc[58], (ntiles + 1) / 2, queries, out, n, wf, s);
         case 59: return launch_persistent_infer(infer_kernel_v2<2, 3, 768, true, 48 | 1024 | 2048>, 768, bpc[59], (ntiles + 1) / 2, queries, out, n, wf, s);
+        // round 4 (the C4 per-rank shard's one-tile tail): 47's body with fewer waves per CU, one persistent block per
+        // CU -- 61: 512 threads (2 waves per SIMD), 62: 768 threads (3 per SIMD) -- so that the last tile of a CU takes
+        // about half / three quarters of the 4-wave tile time
+        case 61: bpc[61] = 1; return launch_persistent_infer(infer_kernel_v2<1, 2, 512, false, 48 | 1024 | 2048 | 8192 | 65536>, 512, bpc[61], ntiles, queries, out, n, wf, s);
+        case 62: bpc[62] = 1; return launch_persistent_infer(infer_kernel_v2<1, 3, 768, false, 48 | 1024 | 2048 | 8192 | 65536>, 768, bpc[62], ntiles, queries, out, n, wf, s);
         // 60: energy probe (wrong outputs): 47 with 12 of the 14 pad slots of layer 0 fed as zeros
         case 60: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | 524288>, 1024, bpc[60], ntiles, queries, out, n, wf, s);
 #endif
