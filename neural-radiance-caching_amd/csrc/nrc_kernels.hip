@@ -3233,13 +3233,28 @@ hipError_t launch_infer_stamped(const float*, float*, int64_t, const _Float16*, 
 }
 #endif
 
+// Launches of at most kInferSmallN queries (a data-parallel rank's shard: 2^19 at 8 ranks) run variant 47's body with
+// 768-thread blocks, one per CU (3 waves per SIMD): the CU's last tile then takes three quarters of the 4-wave tile
+// time, and the tail after the queue runs dry is the per-launch cost that dominates a small launch (DESIGN.md §8:
+// 22.6 vs 24.1 us at 2^19 in-process; 79.7 vs 78.9 us at 2^21, where the 4-wave shape stays).
+constexpr int64_t kInferSmallN = (int64_t)1 << 20;
+
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s, uint32_t* pools,
                         int* parity, bool padq) {
+    if (n <= 0) return hipSuccess;
+    constexpr int A47 = 48 | 1024 | 2048 | 8192 | 65536;
+    const int64_t ntiles = (n + 31) / 32;
+    if (n <= kInferSmallN) {
+        static int bpc = 1, bpc_p = 1;  // one persistent block per CU
+        if (padq)
+            return launch_persistent_infer(infer_kernel_v2<1, 3, 768, false, A47 | kAblPadQ>, 768, bpc_p, ntiles, queries,
+                                           out, n, wf, s);
+        return launch_persistent_infer(infer_kernel_v2<1, 3, 768, false, A47>, 768, bpc, ntiles, queries, out, n, wf, s);
+    }
     if (padq) {  // variant 47 over padded RadianceQuery records
-        if (n <= 0) return hipSuccess;
         static int bpc = 0;
-        return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | kAblPadQ>, 1024,
-                                       bpc, (n + 31) / 32, queries, out, n, wf, s);
+        return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, A47 | kAblPadQ>, 1024, bpc, ntiles, queries, out,
+                                       n, wf, s);
     }
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, pools, parity);
 }

@@ -87,7 +87,7 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40, 41, 42, 47, 48])
+@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40, 41, 42, 47, 48, 61, 62])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every kernel variant kept for A/B at sizes
     that exercise partial tiles / single blocks. The product library holds variant 47 only; the A/B variants are
