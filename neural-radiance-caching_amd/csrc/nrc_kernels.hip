@@ -3236,8 +3236,9 @@ hipError_t launch_infer_stamped(const float*, float*, int64_t, const _Float16*, 
 // Launches of at most kInferSmallN queries (a data-parallel rank's shard: 2^19 at 8 ranks) run variant 47's body with
 // 768-thread blocks, one per CU (3 waves per SIMD): the CU's last tile then takes three quarters of the 4-wave tile
 // time, and the tail after the queue runs dry is the per-launch cost that dominates a small launch (DESIGN.md §8:
-// 22.6 vs 24.1 us at 2^19 in-process; 79.7 vs 78.9 us at 2^21, where the 4-wave shape stays).
-constexpr int64_t kInferSmallN = (int64_t)1 << 20;
+// 22.6 vs 24.1 us at 2^19 in-process, 33.9 vs 34.9 at 3 * 2^18; 44.6 vs 43.2 at 2^20 and 79.7 vs 78.9 at 2^21, where
+// the 4-wave shape stays: profiles/r04_tail/).
+constexpr int64_t kInferSmallN = (int64_t)3 << 18;
 
 hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Float16* wf, hipStream_t s, uint32_t* pools,
                         int* parity, bool padq) {
