@@ -42,6 +42,8 @@ def main() -> None:
     ap.add_argument("--seconds", type=float, default=1.5)
     ap.add_argument("--settle", type=float, default=0.4)
     ap.add_argument("--paths", default="f64,wide_f16,wide_fp8,hash")
+    ap.add_argument("--hash-knob", default=None,
+                    help="name=v1,v2,...: one more Hash path per value of a knob (debug library for the ablations)")
     args = ap.parse_args()
     import torch
 
@@ -75,6 +77,10 @@ def main() -> None:
         net.init(stream=stream, encoding=nrc.InputEncoding.Hash)
         net = trained(net)
         runners["hash"] = (n21, lambda net=net: net.infer(q21, o21, n21))
+        if args.hash_knob:
+            kname, vals = args.hash_knob.split("=")
+            for v in vals.split(","):
+                runners[f"hash@{kname}={v}"] = (n21, lambda net=net: net.infer(q21, o21, n21), (kname, int(v)))
     if "wide_f16" in paths or "wide_fp8" in paths:
         q23 = torch.from_numpy(nrc.synthetic.cornell_queries(n23, seed=seed + 1000)).to(dev)
         o23 = torch.empty((n23, 3), device=dev)
@@ -108,7 +114,10 @@ def main() -> None:
         return launches, us, t0, time.perf_counter()
 
     for _ in range(args.rounds):
-        for p, (n, fn) in runners.items():
+        for p, (n, fn, *knob) in runners.items():
+            if args.hash_knob:
+                kname = args.hash_knob.split("=")[0]
+                nrc._lib.set_knob(kname, knob[0][1] if knob else -1)
             chunk = 50 if n == n21 else 12
             run_for(fn, args.settle, chunk)
             launches, us, t0, t1 = run_for(fn, args.seconds, chunk)
