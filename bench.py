@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-hash", action="store_true", help="skip the InputEncoding::Hash line")
     ap.add_argument("--no-c4", action="store_true", help="N = 1: skip the configs[3] per-rank measurement")
     ap.add_argument("--no-peer", action="store_true", help="N > 1: skip the one-shot peer-exchange training leg")
-    ap.add_argument("--sustained", type=int, default=1000,
+    ap.add_argument("--sustained", type=int, default=4000,
                     help="N = 1: sustained-inference launches timed after as many untimed ones (0: skip)")
     ap.add_argument("--settle-ms", type=float, default=60.0,
                     help="untimed inference launches before the warmup steps until this much GPU time has passed: the "
@@ -423,6 +423,40 @@ def dp_exchange_bench(nrc, net, dev, world: int, rank: int, frames_q, frames_t, 
     return res
 
 
+PEAK_CLOCK_MHZ = 2400.0  # the clock the 2.5 PF dense f16 peak is quoted at (1,024 SIMDs x 1,024 FLOP per cycle)
+
+
+def power_sampler(torch, dev):
+    """tools/energy_ab.py's amdsmi sampler (read-only gpu_metrics: socket power, gfx clock) on this rank's device, or
+    None where amdsmi is unavailable: the power figures are context for the roofline, never required."""
+    try:
+        sys.path.insert(0, str(ROOT / "tools"))
+        from energy_ab import Sampler
+
+        props = torch.cuda.get_device_properties(dev)
+        smp = Sampler(f"{props.pci_bus_id:02x}:{props.pci_device_id:02x}", period=0.01)
+        smp.start()
+        return smp
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def power_window(smp, t0: float, t1: float, achieved_tflops: float) -> dict | None:
+    """Mean socket power and gfx clock over [t0, t1] (the sustained launches), and the achieved MFMA rate against the
+    dense f16 peak at the sampled clock: the package power limit sets the clock."""
+    if smp is None:
+        return None
+    try:
+        w = smp.window(t0, t1)
+    finally:
+        smp.stop()
+    res = {"samples": w.get("samples"), "socket_w": w.get("power_w"), "gfx_mhz": w.get("gfx_mhz")}
+    if w.get("gfx_mhz"):
+        peak = PEAK_F16_TFLOPS * w["gfx_mhz"] / PEAK_CLOCK_MHZ
+        res.update({"peak_at_clock_tflops": peak, "frac_at_clock": achieved_tflops / peak})
+    return res
+
+
 def pmc_traffic() -> float | None:
     f = ROOT / "profiles" / f"pmc_infer_{ROUND}.json"
     if f.exists():
@@ -604,6 +638,7 @@ def main() -> None:
     # launches is lower than in a short burst; the average of the last `sustained` of 2 x `sustained` launches
     sustained = None
     if args.sustained > 0:
+        sampler = power_sampler(torch, dev)
         for _ in range(args.sustained):
             net.infer(q, out, nq)
         ev2, ev3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -611,12 +646,18 @@ def main() -> None:
         for _ in range(args.sustained):
             net.infer(q, out, nq)
         ev3.record(stream)
+        # the sampled window is the timed half: from the moment the GPU reaches ev2 to the end
+        while not ev2.query():
+            time.sleep(0.0005)
+        t_s0 = time.perf_counter()
         torch.cuda.synchronize()
+        t_s1 = time.perf_counter()
         s_ms = ev2.elapsed_time(ev3) / args.sustained
         s_tf = FLOP_PER_QUERY * nq / (s_ms * 1e-3) / 1e12
         sustained = {"launches": 2 * args.sustained, "timed": args.sustained, "infer_kernel_ms": s_ms,
                      "achieved": s_tf, "frac": s_tf / PEAK_F16_TFLOPS,
-                     "M_queries_per_s": nq / (s_ms * 1e-3) / 1e6}
+                     "M_queries_per_s": nq / (s_ms * 1e-3) / 1e6,
+                     "power": power_window(sampler, t_s0, t_s1, s_tf)}
 
     # ---- configs[3] per-rank work on one GPU (C4): 2^19-query shard + 2048-sample slices through nrc_train_dp
     c4_per_rank = None
