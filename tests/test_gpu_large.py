@@ -10,10 +10,14 @@ and write nothing past n. The base block's own outputs are checked against the o
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+# NRC_TEST_LARGE=0 skips these (≈10 GB of device buffers, ≈20 s)
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("NRC_TEST_LARGE", "0") == "0", reason="NRC_TEST_LARGE=1 runs them")]
 
 BASE = 1 << 20
 N = 72_000_123  # 68 copies of BASE + a ragged tail of 697,387 rows; 60 N > 2^32
