@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-# NRC_TEST_LARGE=0 skips these (≈10 GB of device buffers, ≈20 s)
+# opt-in (NRC_TEST_LARGE=1): ≈10 GB of device buffers, ≈20 s
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(os.environ.get("NRC_TEST_LARGE", "0") == "0", reason="NRC_TEST_LARGE=1 runs them")]
 
