@@ -15,9 +15,9 @@ import os
 import numpy as np
 import pytest
 
-# opt-in (NRC_TEST_LARGE=1): ≈10 GB of device buffers, ≈20 s
+# ≈10 GB of device buffers, a few seconds (profiles/r04_end/pytest_gpu_large.log); NRC_TEST_LARGE=0 skips them
 pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("NRC_TEST_LARGE", "0") == "0", reason="NRC_TEST_LARGE=1 runs them")]
+              pytest.mark.skipif(os.environ.get("NRC_TEST_LARGE", "1") == "0", reason="NRC_TEST_LARGE=0")]
 
 BASE = 1 << 20
 N = 72_000_123  # 68 copies of BASE + a ragged tail of 697,387 rows; 60 N > 2^32
