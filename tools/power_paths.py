@@ -2,7 +2,8 @@
 at the package power limit (the 64-wide kernel is) or limited by something else?
 
 Paths: the 64-wide Frequency network (2^21 queries, the product launch), the width-128 network in f16 and FP8
-(2^23 queries, BASELINE configs[4]) and InputEncoding::Hash (2^21 queries: feature pass + MLP pass). Each runs back to
+(2^23 queries, BASELINE configs[4]), InputEncoding::Hash (2^21 queries: feature pass + MLP pass) and, with --paths
+train, the 16,384-sample training step (eager calls; "queries" = samples). Each runs back to
 back for --seconds after --settle of the same launches, event-timed per chunk, while tools/energy_ab.py's Sampler reads
 the GPU's gpu_metrics through amdsmi (read-only). For the MFMA kernels the MFMA-pipe share of the issue cycles at the
 sampled clock follows from their per-tile MFMA cycles (MI355X_MICROARCH.md cycle constants).
@@ -72,6 +73,19 @@ def main() -> None:
         net.init(stream=stream)
         net = trained(net)
         runners["f64"] = (n21, lambda net=net: net.infer(q21, o21, n21))
+    if "train" in paths:
+        # the 16,384-sample training step (bench.py's minibatches), per step: queries = samples
+        net = nrc.Network()
+        net.init(stream=stream)
+        net = trained(net)
+        B = nrc.BATCH_SIZE
+        ctr = [0]
+
+        def step(net=net):
+            b = ctr[0] % 4
+            ctr[0] += 1
+            net.train(tq[b * B:], tt[b * B:])
+        runners["train"] = (B, step)
     if "hash" in paths:
         net = nrc.Network()
         net.init(stream=stream, encoding=nrc.InputEncoding.Hash)
@@ -118,7 +132,7 @@ def main() -> None:
             if args.hash_knob:
                 kname = args.hash_knob.split("=")[0]
                 nrc._lib.set_knob(kname, knob[0][1] if knob else -1)
-            chunk = 50 if n == n21 else 12
+            chunk = 50 if n == n21 else 200 if n == nrc.BATCH_SIZE else 12
             run_for(fn, args.settle, chunk)
             launches, us, t0, t1 = run_for(fn, args.seconds, chunk)
             w = smp.window(t0, t1)
