@@ -184,3 +184,34 @@ def test_training_full_batch_deterministic_every_slot(nrc, dev, width):
     finally:
         for n in nets:
             n.destroy()
+
+
+@pytest.mark.parametrize("layout", ["compact", "padded"])
+def test_small_and_large_launch_shapes_agree_bitwise(nrc, orc, dev, layout):
+    """launch_infer runs launches of <= 3 * 2^18 queries on the 3-waves-per-SIMD shape (nrc_kernels.hip kInferSmallN)
+    and larger ones on variant 47's 4-wave shape: the same per-query arithmetic, so a query's output must not depend on
+    the launch size -- rows of small launches (1, 33, 70,001 and exactly 3 * 2^18 queries) equal, bit for bit, the same
+    rows of one launch past the threshold."""
+    import torch
+    cfg = nrc.default_config(nrc.InputEncoding.Frequency)
+    cfg.query_layout = nrc.QUERY_PADDED if layout == "padded" else nrc.QUERY_COMPACT
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream(), config=cfg)
+    try:
+        net.set_state(nrc.StateSlot.INFER, orc.init_params(1337) * np.float32(1.6))
+        small = 3 << 18
+        nb = small + 4097
+        q_np = nrc.synthetic.cornell_queries(nb, seed=35)
+        if layout == "padded":
+            q_np = np.insert(q_np, 3, np.random.default_rng(3).uniform(-1, 1, nb).astype(np.float32), axis=1)
+        q = _t(q_np, dev)
+        big = torch.full((nb, 3), 777.0, device=dev)
+        net.infer(q, big, nb)
+        for n in (1, 33, 70_001, small):
+            o = torch.full((n + 8, 3), 777.0, device=dev)
+            net.infer(q, o, n)
+            torch.cuda.synchronize()
+            assert torch.equal(o[:n], big[:n]), f"n={n}: {int((o[:n] != big[:n]).any(dim=1).sum())} rows differ"
+            assert bool((o[n:] == 777.0).all())
+    finally:
+        net.destroy()
