@@ -204,6 +204,14 @@ nrc_status nrc_train_dp(nrc_net* net, const float* inputs_d, const float* target
 nrc_status nrc_peer_exchange_handle(nrc_net* net, int world, void* handle_out);
 nrc_status nrc_peer_exchange_open(nrc_net* net, int rank, int world, const void* handles);
 nrc_status nrc_peer_exchange_close(nrc_net* net);
+/* In-process setup (round 5): one process driving several handles -- one per device, as the reference's multi-device
+ * renderer keeps one Device per GPU in one process, or several on one device. nets[r] becomes rank r; each
+ * handle's receive buffer is allocated on its own device and the others store into it through plain device pointers
+ * (peer access enabled between the devices; no IPC). Replaces any exchange the handles had open. The handles share
+ * each other's buffers: close every one of them (after its last step) before destroying any. Handles on one device
+ * take the split form of the exchange (nrc_train_dp of each must then run on its own stream, since a rank's wait
+ * completes only after its peers have pushed); on separate devices the fused form. */
+nrc_status nrc_peer_exchange_open_local(nrc_net* const* nets, int world);
 
 /* ---- state access (host buffers of nrc_get_num_params() f32; synchronous) ----
  * Frequency: NRC_NUM_PARAMS (layout.h canonical blob). Hash: NRC_HASH_NUM_PARAMS = MLP blob then the grid table
@@ -219,12 +227,18 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
  * nrc_init: -1/0 decoupled chain, 1 / 2 round-2 t16 role-split / 4-wave, 32 round-1 32x32x16), "train_shape" (decoupled
  * chain block shape 0..7, -1 = by batch size), "scatter_min" / "scatter_max" (Hash grid-scatter slice plan), "hash_infer"
  * (Hash inference: 1 = the round-2 gather kernel instead of the LDS-table feature pass), "t16_groups" (1 = 64-sample blocks
- * of the role-split kernel, debug library); debug library only: "dc_dw0_delay", "hash_feat_abl". -1 restores the
- * production choice. A value outside a knob's range (train_kernel -1/0/1/2/32, train_shape -1..7, scatter_* -1 or
- * 16..2^20, hash_infer -1..1, t16_groups -1/1/2, dc_dw0_delay -1..2^20, hash_feat_abl -1..36, hash_feat_p -1 or a multiple of 8 in 8..256) is
+ * of the role-split kernel, debug library), "peer_path" (nrc_train_dp over a peer exchange: 0 reduce / push / apply
+ * launches, 1 fused, 2 split; tests: 3 the split form's gradient pass + push alone, 4 its wait + sum + Adam alone),
+ * "px_polls" (bound of the exchange's wait loops, -1 = 2^21 polls, about 10 s); debug library only: "dc_dw0_delay",
+ * "hash_feat_abl". -1 restores the production choice. A value outside a knob's range (train_kernel -1/0/1/2/32,
+ * train_shape -1..7, scatter_* -1 or 16..2^20, hash_infer -1..1, t16_groups -1/1/2, dc_dw0_delay -1..2^20, hash_feat_abl
+ * -1..36, hash_feat_p -1 or a multiple of 8 in 8..256, peer_path -1..4, px_polls -1 or 1..2^21) is
  * NRC_ERR_INVALID_ARGUMENT and leaves the knob unchanged. */
 nrc_status nrc_debug_set_knob(const char* name, int value);
 nrc_status nrc_debug_get_knob(const char* name, int* value);
+/* Test entry: set the peer exchange's sequence number (the tag of the last step; the next step uses seq + 1, and
+ * 0xFFFFFFFF is followed by 2 so that the buffer parity keeps alternating). Between steps, the same value on every rank. */
+nrc_status nrc_debug_set_peer_seq(nrc_net* net, uint32_t seq);
 /* Inference through a specific kernel variant for in-process A/B timing; results are identical in meaning to
  * nrc_infer_stream. The product library has variant 47 (the production kernel) only; the debug library
  * (libnrc_amd_debug.so) also has 0, 23, 30, 39 (47 with the 32x32x16 output layer), 40 / 48 (39 / 47 + in-kernel

@@ -46,10 +46,10 @@ EXPORTS = [
     "nrc_train_grad", "nrc_train_apply", "nrc_train_grad_fixed", "nrc_train_apply_fixed", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
     "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp",
-    "nrc_peer_exchange_handle", "nrc_peer_exchange_open", "nrc_peer_exchange_close",
+    "nrc_peer_exchange_handle", "nrc_peer_exchange_open", "nrc_peer_exchange_close", "nrc_peer_exchange_open_local",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_hash_scatter_inputs", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
     "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert", "nrc_debug_set_knob",
-    "nrc_debug_get_knob",
+    "nrc_debug_get_knob", "nrc_debug_set_peer_seq",
     # include/nrc/frame.h (bound in frame.py)
     "nrc_accumulate_render_radiance", "nrc_infer_accumulate", "nrc_copy_radiance_to_output", "nrc_propagate_train_radiance",
     "nrc_accumulate_render_radiance_factored", "nrc_copy_radiance_to_output_factored", "nrc_propagate_train_radiance_factored",
@@ -137,6 +137,8 @@ def lib() -> ctypes.CDLL:
         "nrc_peer_exchange_handle": (st, [vp, ctypes.c_int, vp]),
         "nrc_peer_exchange_open": (st, [vp, ctypes.c_int, ctypes.c_int, vp]),
         "nrc_peer_exchange_close": (st, [vp]),
+        "nrc_peer_exchange_open_local": (st, [ctypes.POINTER(vp), ctypes.c_int]),
+        "nrc_debug_set_peer_seq": (st, [vp, u32]),
         "nrc_encode": (st, [fp, fp, u32, vp]),
         "nrc_debug_infer_variant": (st, [vp, ctypes.c_int, fp, fp, u32, vp]),
         "nrc_debug_read_infer_clock": (st, [vp, u32, ctypes.POINTER(u32)]),

@@ -235,9 +235,11 @@ std::vector<int> build_t16_slab_map() {
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
 bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
-                                            "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path"};
+                                            "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path",
+                                            "px_polls"};
+static_assert(kKnobCount == 11, "one initial value and one name per knob");
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -340,15 +342,17 @@ struct nrc_net {
                            "derived from it are invalid; re-initialise the network)");
     }
     // one-shot peer gradient exchange (nrc_peer_exchange_*; round 4): own receive buffer, the IPC-mapped buffers of
-    // the peers (px_peers.p[px_rank] = px_buf), the step sequence number
+    // the peers (px_peers.p[px_rank] = px_buf), the step sequence number (the tag of the last step's words)
     float* px_buf = nullptr;
     PeerPtrs px_peers{};
     int px_world = 0, px_rank = -1;
     uint32_t px_seq = 0;
     bool px_open = false;
-    bool px_shared = false;  // a peer's buffer lives on this rank's device (ranks sharing a GPU): split exchange
+    bool px_shared = false;   // a peer's buffer lives on this rank's device (ranks sharing a GPU): split exchange
+    bool px_local = false;    // nrc_peer_exchange_open_local: the peers' buffers are other handles' own (no IPC)
+    bool px_pending = false;  // knob peer_path 3 pushed a step whose wait + sum + Adam (peer_path 4) is still to run
     void peer_close() {
-        if (px_open)
+        if (px_open && !px_local)
             for (int r = 0; r < px_world; ++r)
                 if (r != px_rank && px_peers.p[r]) (void)hipIpcCloseMemHandle(px_peers.p[r]);
         px_peers = PeerPtrs{};
@@ -359,6 +363,8 @@ struct nrc_net {
         px_seq = 0;
         px_open = false;
         px_shared = false;
+        px_local = false;
+        px_pending = false;
     }
     void alloc_loss_slots() {
         HIP_CHECK(hipMalloc(&work_queue, kInferPoolBytes));
@@ -748,6 +754,16 @@ bool nrc_amd::net_comm(nrc_net* net, int* rank, int* world) {
     return net->comm != nullptr;
 }
 
+bool nrc_amd::net_infer_fusable(nrc_net* net) {
+    check_live(net);
+    return net->cfg.infer_precision != NRC_PRECISION_F16_ACC16;
+}
+
+void nrc_amd::net_check_protocol(nrc_net* net) {
+    check_live(net);
+    net->check_protocol();
+}
+
 bool nrc_amd::net_padq(nrc_net* net) {
     check_live(net);
     return net->padq();
@@ -773,7 +789,8 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobHashFeatAbl: return v >= -1 && v <= 36;
         case kKnobT16Groups: return v == -1 || v == 1 || v == 2;
         case kKnobHashFeatP: return v == -1 || (v >= 8 && v <= 256 && v % 8 == 0);
-        case kKnobPeerPath: return v >= -1 && v <= 2;
+        case kKnobPeerPath: return v >= -1 && v <= 4;
+        case kKnobPxPolls: return v == -1 || (v >= 1 && v <= kPeerPolls);
         default: return false;
     }
 }
@@ -1195,26 +1212,57 @@ void nccl_check(ncclResult_t r, const char* what) {
         throw ApiError(NRC_ERR_HIP, std::string(what) + " failed: " + ncclGetErrorString(r));
 }
 
-void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b, float* loss_h,
-                 float* loss_d) {
-    check_live(net);
-    if (!net->comm && !net->px_open)
-        throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm / nrc_peer_exchange_open)");
-    if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
-    if (net->px_open) {
-        net->px_seq = net->px_seq + 1u ? net->px_seq + 1u : 1u;
-        const int nfl = (int)net->grad_floats();
-        const int kp = knob(kKnobPeerPath);
-        if (kp != 0) {
+// Sequence number of the peer exchange's next step: never 0 (the tag of a zeroed receive buffer), and its parity (the
+// buffer half a step uses) alternates across the wrap, 0xFFFFFFFF -> 2, as the two-parity protocol requires.
+uint32_t px_next(uint32_t seq) { return seq == 0xFFFFFFFFu ? 2u : seq + 1u; }
+
+int px_polls() {
+    const int k = knob(kKnobPxPolls);
+    return k > 0 ? k : kPeerPolls;
+}
+
+// nrc_train_dp over an open peer exchange. Every argument is checked and the protocol state read before anything is
+// launched, and the handle's sequence number advances only once the exchange launch has been issued: a call rejected
+// on one rank leaves that rank's sequence where its peers expect it, so the next step still pairs up.
+void do_peer_step(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b, float* loss_h,
+                  float* loss_d) {
+    const int kp = knob(kKnobPeerPath);
+    const int nfl = (int)net->grad_floats();
+    const int polls = px_polls();
+    if (kp != 4) {
+        if (global_b < b_local || global_b == 0)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
+        if (b_local > 0 && (!in || !tgt)) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
+    }
+    if ((kp == 4) != net->px_pending)
+        throw ApiError(NRC_ERR_INVALID_ARGUMENT, net->px_pending
+                                                     ? "peer exchange: a pushed step awaits its apply (knob peer_path 4)"
+                                                     : "peer exchange: no pushed step to apply (knob peer_path 3 first)");
+    net->check_protocol();
+    if (kp == 3 && loss_h) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "peer_path 3 pushes only: no loss to return");
+    const int form = kp == -1 ? (net->px_shared ? kPxSplit : kPxFused)
+                     : kp == 1 ? kPxFused
+                     : kp == 2 ? kPxSplit
+                     : kp == 3 ? kPxPushOnly
+                     : kp == 4 ? kPxApplyOnly
+                               : -1;  // 0: the reduce + push + apply launches
+    float* const ld = loss_d ? loss_d : net->loss_dev;
+    const uint32_t st = net->step + 1;
+    if (form == kPxApplyOnly) {
+        // the pushed step's sequence number is already committed; a slab count of 1 is a placeholder (no reduce runs)
+        HIP_CHECK(launch_reduce_exchange(net->slabs, 1, net->loss_partials, net->px_peers, net->px_rank, net->px_world,
+                                         nfl, net->px_seq, net->proto_err_dev(), ld, net->buffers(), net->optim(st),
+                                         net->stream, kPxApplyOnly, polls));
+        net->step = st;
+        net->px_pending = false;
+    } else {
+        const uint32_t seq = px_next(net->px_seq);
+        if (form >= 0) {
             // the exchange fused into the reduction: gradient pass -> one launch that reduces the slabs, pushes each
             // block's partials to every rank, waits for the same block of every rank, sums in rank order, Adam/EMA
             // (split: the wait + sum + Adam as a second, small launch -- ranks sharing this device)
-            const bool split = kp == 2 || (kp == -1 && net->px_shared);
-            if (global_b < b_local || global_b == 0)
-                throw ApiError(NRC_ERR_INVALID_ARGUMENT, "global_b must be >= b and >= 1");
             int blocks = 1;
             if (b_local > 0) {
-                if (!in || !tgt) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/target pointer");
                 blocks = train_block_count(net, b_local);
                 net->ensure_slabs(blocks);
                 train_partials(net, in, tgt, b_local, 3.0f * (float)global_b);
@@ -1224,33 +1272,43 @@ void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_loc
                 HIP_CHECK(hipMemsetAsync(net->slabs, 0, (mb.slab_f16 ? 2 : 4) * (size_t)mb.n_slab, net->stream));
                 HIP_CHECK(hipMemsetAsync(net->loss_partials, 0, sizeof(float), net->stream));
             }
-            net->step += 1;
             HIP_CHECK(launch_reduce_exchange(net->slabs, blocks, net->loss_partials, net->px_peers, net->px_rank,
-                                             net->px_world, nfl, net->px_seq, net->proto_err_dev(),
-                                             loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step),
-                                             net->stream, split));
+                                             net->px_world, nfl, seq, net->proto_err_dev(), ld, net->buffers(),
+                                             net->optim(st), net->stream, form, polls));
         } else {
             // round 4's first version (knob peer_path = 0; world >= 2): reduce to a gradient -> push the gradient to
             // every peer's receive slot -> wait + rank-order sum + Adam/EMA
+            if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
             do_train_grad(net, in, tgt, b_local, global_b, net->dp_grad);
-            HIP_CHECK(launch_peer_push(net->dp_grad, nfl, net->px_peers, net->px_rank, net->px_world, net->px_seq,
-                                       net->stream));
-            net->step += 1;
-            HIP_CHECK(launch_peer_apply(net->px_buf, net->px_world, nfl, net->px_seq, net->proto_err_dev(),
-                                        loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step),
-                                        net->stream));
+            HIP_CHECK(launch_peer_push(net->dp_grad, nfl, net->px_peers, net->px_rank, net->px_world, seq, net->stream));
+            HIP_CHECK(launch_peer_apply(net->px_buf, net->px_world, nfl, seq, net->proto_err_dev(), ld, net->buffers(),
+                                        net->optim(st), net->stream, polls));
         }
-        if (loss_h) {
-            if (loss_d) {
-                HIP_CHECK(hipStreamSynchronize(net->stream));
-                net->check_protocol();
-                HIP_CHECK(hipMemcpy(loss_h, loss_d, sizeof(float), hipMemcpyDeviceToHost));
-            } else {
-                *loss_h = net->read_loss();
-            }
+        net->px_seq = seq;
+        if (form == kPxPushOnly) net->px_pending = true;
+        else net->step = st;
+    }
+    if (loss_h) {
+        if (loss_d) {
+            HIP_CHECK(hipStreamSynchronize(net->stream));
+            net->check_protocol();
+            HIP_CHECK(hipMemcpy(loss_h, loss_d, sizeof(float), hipMemcpyDeviceToHost));
+        } else {
+            *loss_h = net->read_loss();
         }
+    }
+}
+
+void do_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b, float* loss_h,
+                 float* loss_d) {
+    check_live(net);
+    if (!net->comm && !net->px_open)
+        throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no communicator attached (nrc_set_comm / nrc_peer_exchange_open)");
+    if (net->px_open) {
+        do_peer_step(net, in, tgt, b_local, global_b, loss_h, loss_d);
         return;
     }
+    if (!net->dp_grad) HIP_CHECK(hipMalloc(&net->dp_grad, sizeof(float) * net->grad_floats()));
     if (net->hash()) {
         // exact grid exchange: each rank's fixed-point sums, exchange-encoded in place in the handle's accumulator,
         // summed as int64 beside the f32 MLP gradient and loss (one RCCL group on the handle's stream), then rounded
@@ -1468,6 +1526,80 @@ nrc_status nrc_peer_exchange_close(nrc_net* net) {
         check_live(net);
         HIP_CHECK(hipStreamSynchronize(net->stream));
         net->peer_close();
+    });
+}
+
+nrc_status nrc_peer_exchange_open_local(nrc_net* const* nets, int world) {
+    return guarded([&] {
+        if (!nets) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null handle array");
+        if (world < 1 || world > kPeerMaxRanks) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "world must be 1..16");
+        for (int r = 0; r < world; ++r) {
+            check_live(nets[r]);
+            if (nets[r]->hash() || nets[r]->wide())
+                throw ApiError(NRC_ERR_UNSUPPORTED, "the peer exchange is implemented for the width-64 Frequency / "
+                                                    "FrequencySH networks (Hash and width 128 use the RCCL path)");
+            if (nets[r]->encoding != nets[0]->encoding)
+                throw ApiError(NRC_ERR_INVALID_ARGUMENT, "every handle of one exchange must have the same encoding");
+            for (int q = 0; q < r; ++q)
+                if (nets[q] == nets[r]) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "a handle appears twice");
+        }
+        int cur = 0;
+        HIP_CHECK(hipGetDevice(&cur));
+        struct Restore {
+            int dev;
+            ~Restore() { (void)hipSetDevice(dev); }
+        } restore{cur};
+        for (int r = 0; r < world; ++r) {
+            HIP_CHECK(hipStreamSynchronize(nets[r]->stream));
+            nets[r]->peer_close();
+        }
+        // each rank's receive buffer on its own device (uncached, as for the IPC form); the peers store into it
+        // through plain device pointers, over xGMI when the devices differ (peer access enabled both ways)
+        for (int r = 0; r < world; ++r) {
+            nrc_net* n = nets[r];
+            HIP_CHECK(hipSetDevice(n->device));
+            const size_t bytes = peer_buffer_bytes(world, (int)n->grad_floats(), n->buffers().n_slab);
+            const hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&n->px_buf), bytes, hipDeviceMallocUncached);
+            if (e != hipSuccess) {
+                for (int q = 0; q <= r; ++q) nets[q]->peer_close();
+                throw ApiError(e == hipErrorOutOfMemory ? NRC_ERR_OUT_OF_MEMORY : NRC_ERR_HIP,
+                               std::string("hipExtMallocWithFlags: ") + hipGetErrorString(e));
+            }
+            HIP_CHECK(hipMemset(n->px_buf, 0, bytes));
+            for (int q = 0; q < world; ++q) {
+                if (nets[q]->device == n->device) continue;
+                const hipError_t pe = hipDeviceEnablePeerAccess(nets[q]->device, 0);
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+                    throw ApiError(NRC_ERR_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(pe));
+                (void)hipGetLastError();
+            }
+            HIP_CHECK(hipDeviceSynchronize());
+        }
+        PeerPtrs p{};
+        for (int r = 0; r < world; ++r) p.p[r] = nets[r]->px_buf;
+        for (int r = 0; r < world; ++r) {
+            nrc_net* n = nets[r];
+            bool shared = false;
+            for (int q = 0; q < world; ++q) shared = shared || (q != r && nets[q]->device == n->device);
+            n->px_peers = p;
+            n->px_world = world;
+            n->px_rank = r;
+            n->px_seq = 0;
+            n->px_shared = shared;
+            n->px_local = true;
+            n->px_pending = false;
+            n->px_open = true;
+        }
+    });
+}
+
+nrc_status nrc_debug_set_peer_seq(nrc_net* net, uint32_t seq) {
+    return guarded([&] {
+        check_live(net);
+        if (!net->px_open || net->px_pending)
+            throw ApiError(NRC_ERR_INVALID_ARGUMENT, "no open peer exchange between steps");
+        if (seq == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "sequence number 0 is the tag of an empty buffer");
+        net->px_seq = seq;
     });
 }
 

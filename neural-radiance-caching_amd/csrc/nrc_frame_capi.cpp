@@ -209,7 +209,8 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     // Full / CacheOnly: accumulate_render_radiance runs in the inference epilogue (row 4 fusion); with reflectance
     // factoring the separate (factored) accumulation kernel runs instead
     const bool rf = p->reflectance_factoring != 0;
-    const bool fuse = !skip_render && !p->keep_render_results && !rf &&
+    // (a handle inferring with tcnn's f16 accumulation has no fused form: it takes infer + accumulate)
+    const bool fuse = !skip_render && !p->keep_render_results && !rf && net_infer_fusable(net) &&
                       (mode == NRC_RENDER_FULL || mode == NRC_RENDER_CACHE_ONLY);
     if ((uint64_t)screen + tiles > 0) require(qi && ri, "inference buffers are NULL");
     auto infer_range = [&](uint32_t first, uint32_t count, uint32_t acc_pixels) {
@@ -289,6 +290,7 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     }
     if (loss_h) {
         HIP_CHECK(hipStreamSynchronize(s));  // the slots are host-mapped: the kernels wrote them directly
+        net_check_protocol(net);  // a timed-out exchange wait or LDS protocol wait invalidates the losses
         float total = 0.0f;
         for (int b = 0; b < NRC_NUM_BATCHES; ++b) total += slots.host[b];
         *loss_h = total * (1.0f / NRC_NUM_BATCHES);

@@ -325,11 +325,13 @@ enum Knob : int {
     kKnobHashInfer = 5,   // Hash inference: -1 / 0 LDS-table feature pass + MLP kernel (round 3), 1 the gather kernel
     kKnobHashFeatAbl = 6,  // debug library: hash_feature_kernel ablation (1 no gathers, 2 no position loads, 4 no stores)
     kKnobT16Groups = 7,    // role-split t16 training kernel: 16-sample groups per chain wave (1: 64-sample blocks; -1 = 2)
-    kKnobHashFeatP = 8,    // Hash feature pass: query ranges per level (multiple of 8; -1 = 16 above 2^19 queries, else 8)
+    kKnobHashFeatP = 8,    // Hash feature pass: query ranges per level (multiple of 8; -1 = 32 above 2^19 queries, else 8)
     kKnobPeerPath = 9,     // nrc_train_dp over the peer exchange: -1 automatic (fused, or split when a peer shares this
                            // rank's device), 0 the reduce + push + apply launches (round 4's first version), 1 fused,
-                           // 2 split (reduce + push, then wait + sum + Adam)
-    kKnobCount = 10
+                           // 2 split (reduce + push, then wait + sum + Adam); tests: 3 the split form's gradient pass +
+                           // push alone (no optimizer step), 4 its wait + sum + Adam alone (the step the last 3 pushed)
+    kKnobPxPolls = 10,     // bound of the peer exchange's wait loops (-1 = kPeerPolls, about 10 s; 1..2^21)
+    kKnobCount = 11
 };
 int knob(Knob k);
 
@@ -392,13 +394,19 @@ hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const fl
                               hipStream_t s);
 hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int rank, int world, uint32_t seq,
                             hipStream_t s);
+// polls: bound of every wait loop (kPeerPolls in production, about 10 s; knob "px_polls" for tests)
+constexpr int kPeerPolls = 1 << 21;
 hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
-                             const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s);
-// reduce + peer exchange + rank-order sum + Adam/EMA in one launch after the gradient pass (world 1..16); split: as
-// two launches (reduce + push, then wait + sum + Adam in a small grid) for ranks that share a device
+                             const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, int polls = kPeerPolls);
+// Forms of the exchange inside the reduction: kPxFused -- reduce + push + wait + rank-order sum + Adam/EMA in one launch
+// after the gradient pass (world 1..16, ranks on separate devices); kPxSplit -- the same as two launches (reduce + push,
+// then wait + sum + Adam in a small grid) for ranks that share a device; kPxPushOnly / kPxApplyOnly -- the split form's
+// first / second launch on its own (sequenced single-process tests, knob peer_path 3 / 4)
+enum PxForm { kPxFused = 0, kPxSplit = 1, kPxPushOnly = 2, kPxApplyOnly = 3 };
 hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
                                   int rank, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
-                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, bool split = false);
+                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, int form,
+                                  int polls = kPeerPolls);
 
 // ---- per-handle scratch used by the frame driver (nrc_capi.cpp): NRC_NUM_BATCHES loss slots on the device and a
 // pinned host mirror
@@ -414,6 +422,10 @@ nrc_loss_slots net_loss_slots(nrc_net* net);
 bool net_comm(nrc_net* net, int* rank, int* world);
 // the handle's RadianceQuery records are padded (nrc_config.query_layout = NRC_QUERY_PADDED)
 bool net_padq(nrc_net* net);
+// inference can take the fused accumulation epilogue (not with NRC_PRECISION_F16_ACC16)
+bool net_infer_fusable(nrc_net* net);
+// throws NRC_ERR_INTERNAL if a training kernel or a peer-exchange wait reported a timeout (after a stream sync)
+void net_check_protocol(nrc_net* net);
 // nrc_train_dp with the loss left in a device slot (frame driver)
 void net_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
                         float* loss_d);

@@ -4018,8 +4018,8 @@ __global__ __launch_bounds__(1024) void peer_push_kernel(const float* __restrict
 
 template <int WMAX>  // the world's bucket (2, 4, 8, 16): the rank-order sum is unrolled over WMAX ranks
 __global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict__ xbuf, int world, int stride, uint32_t seq,
-                                                         uint32_t* err, float* __restrict__ loss_out, ModelBuffers mb,
-                                                         OptimArgs oa, float lr_t, float ema_debias) {
+                                                         int polls, uint32_t* err, float* __restrict__ loss_out,
+                                                         ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
     const int par = (int)(seq & 1u);
     const int nflags = world * kPeerSplit;
     __shared__ uint32_t timed_out;
@@ -4028,18 +4028,18 @@ __global__ __launch_bounds__(256) void peer_apply_kernel(const float* __restrict
         // wave-uniform (ballot) and holds no store (tests/test_asm_hazards.py rule 3). Relaxed system-scope polls of
         // uncached memory (no L2 invalidate per poll); the data loads below are issued after the flags have returned
         // (the barrier follows the loop) and read memory, not a cache. Fast polls first (~0.1 ms), then ~4 us apart:
-        // about 10 s in all.
+        // about 10 s in all (polls = 2^21; the px_polls knob shortens it for tests).
         const int lane = threadIdx.x;
         const uint32_t* f = reinterpret_cast<const uint32_t*>(xbuf + (int64_t)2 * world * stride) +
                             (par * nflags + (lane < nflags ? lane : 0)) * kPeerFlagStride;
         int i = 0;
-        for (; i < (1 << 21); ++i) {
+        for (; i < polls; ++i) {
             const bool ready = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq;
             if (__builtin_amdgcn_readfirstlane(__ballot(!ready) == 0ull)) break;
             if (i < 4096) __builtin_amdgcn_s_sleep(1);
             else __builtin_amdgcn_s_sleep(127);
         }
-        if (lane == 0) timed_out = i == (1 << 21) ? 1u : 0u;
+        if (lane == 0) timed_out = i == polls ? 1u : 0u;
     }
     __syncthreads();
     if (timed_out && blockIdx.x == 0 && threadIdx.x == 0)
@@ -4100,7 +4100,8 @@ __device__ __forceinline__ uint64_t px_word(float v, uint32_t seq) {
 // the registers mine / mine_l (never stored to nor read back from memory), so only the other ranks' words are awaited.
 template <int WMAX, bool OWNREG>
 __device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, int blk, int par, int rank, int world,
-                                                    int xstride, int pp, uint32_t seq, uint32_t* err, float* loss_out,
+                                                    int xstride, int pp, uint32_t seq, int polls, uint32_t* err,
+                                                    float* loss_out,
                                                     float mine, float mine_l, const AdamIn& ain, const ModelBuffers& mb,
                                                     const OptimArgs& oa, float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
@@ -4111,7 +4112,7 @@ __device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, i
     uint64_t w[WMAX], wl[WMAX];
     int i = 0;
     // OWNREG at world 1: nothing to wait for (the loop would only re-read a row that is never awaited)
-    for (; i < (1 << 21) && !(OWNREG && world == 1); ++i) {
+    for (; i < polls && !(OWNREG && world == 1); ++i) {
         bool ready = true;
 #pragma unroll
         for (int r = 0; r < WMAX; ++r) {
@@ -4128,7 +4129,7 @@ __device__ __forceinline__ void exchange_wait_apply(const char* own, int lane, i
         if (i < 4096) __builtin_amdgcn_s_sleep(1);
         else __builtin_amdgcn_s_sleep(127);
     }
-    if (i == (1 << 21) && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (i == polls && lane == 0) __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if constexpr (OWNREG) {
 #pragma unroll
         for (int r = 0; r < WMAX; ++r)
@@ -4154,9 +4155,9 @@ template <bool H, int WMAX, bool WAIT>
 __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const float* __restrict__ slabs, int nslabs,
                                                                       const float* __restrict__ loss_partials,
                                                                       PeerPtrs dst, size_t region, int rank, int world,
-                                                                      uint32_t seq, uint32_t* err, float* loss_out,
-                                                                      ModelBuffers mb, OptimArgs oa, float lr_t,
-                                                                      float ema_debias) {
+                                                                      uint32_t seq, int polls, uint32_t* err,
+                                                                      float* loss_out, ModelBuffers mb, OptimArgs oa,
+                                                                      float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ f4 part[kRedGroups][kRedParams];
@@ -4228,7 +4229,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const floa
     }
     if constexpr (WAIT)
         exchange_wait_apply<WMAX, true>(reinterpret_cast<const char*>(dst.p[rank]) + region, lane, blk, par, rank, world,
-                                        xstride, pp, seq, err, loss_out, g1, L, ain, mb, oa, lr_t, ema_debias);
+                                        xstride, pp, seq, polls, err, loss_out, g1, L, ain, mb, oa, lr_t, ema_debias);
     (void)nblk;
 }
 
@@ -4236,9 +4237,9 @@ __global__ __launch_bounds__(kRedThreads) void reduce_exchange_kernel(const floa
 // half): 92 blocks of 256 threads for the Frequency slab, the footprint of round 4's first apply kernel.
 template <bool H, int WMAX>
 __global__ __launch_bounds__(256) void exchange_apply_kernel(const char* __restrict__ own, int nblk, int world,
-                                                             uint32_t seq, uint32_t* err, float* loss_out,
-                                                             ModelBuffers mb, OptimArgs oa, float lr_t,
-                                                             float ema_debias) {
+                                                             uint32_t seq, int polls, uint32_t* err,
+                                                             float* loss_out, ModelBuffers mb, OptimArgs oa,
+                                                             float lr_t, float ema_debias) {
     const int lane = threadIdx.x & 63;
     const int blk = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
     if (blk >= nblk) return;  // wave-uniform
@@ -4248,14 +4249,16 @@ __global__ __launch_bounds__(256) void exchange_apply_kernel(const char* __restr
     else pp = mb.slab_param[mypos];
     AdamIn ain{};
     if (pp >= 0) ain = adam_load(pp, mb);
-    exchange_wait_apply<WMAX, false>(own, lane, blk, (int)(seq & 1u), 0, world, px_stride(mb.n_slab), pp, seq, err,
-                                     loss_out, 0.0f, 0.0f, ain, mb, oa, lr_t, ema_debias);
+    exchange_wait_apply<WMAX, false>(own, lane, blk, (int)(seq & 1u), 0, world, px_stride(mb.n_slab), pp, seq, polls,
+                                     err, loss_out, 0.0f, 0.0f, ain, mb, oa, lr_t, ema_debias);
 }
 
 hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* loss_partials, const PeerPtrs& dst,
                                   int rank, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
-                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, bool split) {
-    if (world < 1 || world > kPeerMaxRanks || rank < 0 || rank >= world || !err || nslabs < 1) return hipErrorInvalidValue;
+                                  const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, int form, int polls) {
+    if (world < 1 || world > kPeerMaxRanks || rank < 0 || rank >= world || !err || nslabs < 1 || polls < 1 ||
+        form < kPxFused || form > kPxApplyOnly)
+        return hipErrorInvalidValue;
     for (int r = 0; r < world; ++r)
         if (!dst.p[r]) return hipErrorInvalidValue;
     float lr_t, ema_debias;
@@ -4263,19 +4266,22 @@ hipError_t launch_reduce_exchange(const float* slabs, int nslabs, const float* l
     const int nblk = mb.n_slab / (kRedParams * kRedVec);
     const size_t region = px_region_offset(world, nfl);
     const char* own = reinterpret_cast<const char*>(dst.p[rank]) + region;
+    const bool push = form != kPxApplyOnly, apply = form == kPxSplit || form == kPxApplyOnly;
 #define NRC_RX(HH, W)                                                                                                   \
     do {                                                                                                                \
-        if (split) {                                                                                                    \
-            hipLaunchKernelGGL((reduce_exchange_kernel<HH, W, false>), dim3(nblk), dim3(kRedThreads), 0, s, slabs,      \
-                               nslabs, loss_partials, dst, region, rank, world, seq, err, loss_out, mb, oa, lr_t,       \
-                               ema_debias);                                                                             \
-            hipLaunchKernelGGL((exchange_apply_kernel<HH, W>), dim3((nblk + 3) / 4), dim3(256), 0, s, own, nblk, world, \
-                               seq, err, loss_out, mb, oa, lr_t, ema_debias);                                           \
-        } else {                                                                                                        \
+        if (form == kPxFused) {                                                                                         \
             hipLaunchKernelGGL((reduce_exchange_kernel<HH, W, true>), dim3(nblk), dim3(kRedThreads), 0, s, slabs,       \
-                               nslabs, loss_partials, dst, region, rank, world, seq, err, loss_out, mb, oa, lr_t,       \
-                               ema_debias);                                                                             \
+                               nslabs, loss_partials, dst, region, rank, world, seq, polls, err, loss_out, mb, oa,      \
+                               lr_t, ema_debias);                                                                       \
+            break;                                                                                                      \
         }                                                                                                               \
+        if (push)                                                                                                       \
+            hipLaunchKernelGGL((reduce_exchange_kernel<HH, W, false>), dim3(nblk), dim3(kRedThreads), 0, s, slabs,      \
+                               nslabs, loss_partials, dst, region, rank, world, seq, polls, err, loss_out, mb, oa,      \
+                               lr_t, ema_debias);                                                                       \
+        if (apply)                                                                                                      \
+            hipLaunchKernelGGL((exchange_apply_kernel<HH, W>), dim3((nblk + 3) / 4), dim3(256), 0, s, own, nblk, world, \
+                               seq, polls, err, loss_out, mb, oa, lr_t, ema_debias);                                    \
     } while (0)
 #define NRC_RXW(HH)                     \
     if (world <= 2) NRC_RX(HH, 2);      \
@@ -4304,20 +4310,20 @@ hipError_t launch_peer_push(const float* grad, int nfl, const PeerPtrs& dst, int
 }
 
 hipError_t launch_peer_apply(const float* xbuf, int world, int nfl, uint32_t seq, uint32_t* err, float* loss_out,
-                             const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
-    if (world < 2 || world > kPeerMaxRanks || !xbuf || !err) return hipErrorInvalidValue;
+                             const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s, int polls) {
+    if (world < 2 || world > kPeerMaxRanks || !xbuf || !err || polls < 1) return hipErrorInvalidValue;
     float lr_t, ema_debias;
     adam_host_factors(oa, lr_t, ema_debias);
     const dim3 grid((mb.n_mlp + 255) / 256);
     const int st = peer_stride(nfl);
     if (world <= 2)
-        hipLaunchKernelGGL(peer_apply_kernel<2>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+        hipLaunchKernelGGL(peer_apply_kernel<2>, grid, dim3(256), 0, s, xbuf, world, st, seq, polls, err, loss_out, mb, oa, lr_t, ema_debias);
     else if (world <= 4)
-        hipLaunchKernelGGL(peer_apply_kernel<4>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+        hipLaunchKernelGGL(peer_apply_kernel<4>, grid, dim3(256), 0, s, xbuf, world, st, seq, polls, err, loss_out, mb, oa, lr_t, ema_debias);
     else if (world <= 8)
-        hipLaunchKernelGGL(peer_apply_kernel<8>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+        hipLaunchKernelGGL(peer_apply_kernel<8>, grid, dim3(256), 0, s, xbuf, world, st, seq, polls, err, loss_out, mb, oa, lr_t, ema_debias);
     else
-        hipLaunchKernelGGL(peer_apply_kernel<16>, grid, dim3(256), 0, s, xbuf, world, st, seq, err, loss_out, mb, oa, lr_t, ema_debias);
+        hipLaunchKernelGGL(peer_apply_kernel<16>, grid, dim3(256), 0, s, xbuf, world, st, seq, polls, err, loss_out, mb, oa, lr_t, ema_debias);
     return hipGetLastError();
 }
 

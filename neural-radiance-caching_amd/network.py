@@ -281,6 +281,19 @@ class Network:
     def peer_exchange_close(self) -> None:
         check(self._lib.nrc_peer_exchange_close(self._h))
 
+    @staticmethod
+    def peer_exchange_open_local(nets) -> None:
+        """In-process peer exchange over several handles of this process (nrc_peer_exchange_open_local): nets[r] is
+        rank r, the receive buffers are reached through plain device pointers. Close every handle before destroying
+        any of them."""
+        nets = list(nets)
+        arr = (ctypes.c_void_p * len(nets))(*[n._h.value for n in nets])
+        check(nets[0]._lib.nrc_peer_exchange_open_local(arr, len(nets)))
+
+    def set_peer_seq(self, seq: int) -> None:
+        """Test entry (nrc_debug_set_peer_seq): the sequence number of the last exchange step, between steps."""
+        check(self._lib.nrc_debug_set_peer_seq(self._h, int(seq)))
+
     @property
     def num_params(self) -> int:
         """Parameter count of the configured model (Frequency 22,528; Hash 21,504 MLP + 991,232 grid)."""

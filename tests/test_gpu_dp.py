@@ -242,7 +242,8 @@ def test_two_ranks_on_one_gpu_peer_exchange(tmp_path, nrc, torch, dev, golden, B
 @pytest.mark.parametrize("B", [16384, 2048, 0])
 def test_peer_exchange_world_1_is_the_fused_step(nrc, torch, dev, golden, B):
     """A world-1 peer exchange (what bench.py's per-rank leg runs): nrc_train_dp through the fused reduce + exchange
-    launch stores each block's partials into its own buffer, waits for its own flags and applies the one-rank sum --
+    launch keeps its own partials in registers -- at world 1 it stores nothing and skips the wait loop, so this covers
+    the reduce + sum + Adam half only (the stores and the wait at world >= 2: the sequenced test below) -- and must be
     bitwise the state and loss of nrc_train's reduce + Adam (the same slab sums, a sum over one rank is the value).
     B = 0: a rank without samples takes part with a zero gradient (loss 0; Adam's l2 term still steps the weights)."""
     a, b = nrc.Network(), nrc.Network()
@@ -284,3 +285,148 @@ def test_peer_exchange_argument_checks(nrc, torch, dev):
         hnet.peer_exchange_handle(2)
     assert e.value.status == 5
     hnet.destroy()
+
+
+SLOTS = ("PARAMS", "INFER", "EMA", "ADAM_M", "ADAM_V")
+
+
+@pytest.fixture()
+def knobs(nrc):
+    yield nrc._lib.set_knob
+    for k in ("peer_path", "px_polls"):
+        nrc._lib.set_knob(k, -1)
+
+
+@pytest.mark.parametrize("world,B", [(2, 16384), (4, 16384), (8, 16384), (8, 4096)])
+def test_sequenced_fused_peer_exchange(nrc, torch, dev, golden, knobs, world, B):
+    """the fused exchange at world >= 2 -- its stores into every peer's buffer and its wait loop
+    (reduce_exchange_kernel<..., WAIT=true>, what every rank runs with one rank per GPU) -- executed in one process
+    without co-residency: world handles on one GPU joined by nrc_peer_exchange_open_local (plain device pointers, no
+    IPC); per step ranks 1..N-1 run the split form's gradient pass + push alone (knob peer_path 3), then rank 0 runs
+    the fused kernel (peer_path 1; every word it awaits is already in its buffer), then ranks 1..N-1 run the split form's
+    wait + sum + Adam alone (peer_path 4; rank 0's words have arrived). Every handle's five state slots and loss must be
+    bitwise those of one handle applying the rank-order sum g0 + g1 + ... of the shards' gradients (nrc_train_grad)
+    with nrc_train_apply. Three steps: both buffer parities; at world 8 the sequence number starts at 0xFFFFFFFE, so the
+    steps carry tags 0xFFFFFFFF, 2, 3 (the wrap keeps the parity alternating). On step 2 rank 1 first makes a rejected
+    call (global_b < b_local), which must not advance its sequence. A slip ends a wait with
+    NRC_ERR_INTERNAL after px_polls polls instead of hanging."""
+    knobs("px_polls", 1 << 14)
+    nets = []
+    for _ in range(world):
+        n = nrc.Network()
+        n.init(stream=torch.cuda.current_stream())
+        n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+        nets.append(n)
+    nrc.Network.peer_exchange_open_local(nets)
+    if world == 8:
+        for n in nets:
+            n.set_peer_seq(0xFFFFFFFE)
+    ref = nrc.Network()
+    ref.init(stream=torch.cuda.current_stream())
+    ref.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+    g = [torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev) for _ in range(world)]
+    try:
+        for it in range(3):
+            q_np, t_np = nrc.synthetic.cornell_batch(B, seed=300 + it)
+            q, t = to_dev(torch, dev, q_np), to_dev(torch, dev, t_np)
+            sh = [nrc.dp.shard_range(B, r, world) for r in range(world)]
+            knobs("peer_path", 3)
+            if it == 1:
+                s1, c1 = sh[1]
+                with pytest.raises(nrc.NrcError) as e:
+                    nets[1].train_dp(q[s1:s1 + c1], t[s1:s1 + c1], c1, c1 - 1)
+                assert e.value.status == 1
+            for r in range(1, world):
+                s, c = sh[r]
+                nets[r].train_dp(q[s:s + c], t[s:s + c], c, B)
+            knobs("peer_path", 1)
+            s, c = sh[0]
+            losses = [nets[0].train_dp(q[s:s + c], t[s:s + c], c, B, loss=True)]
+            knobs("peer_path", 4)
+            for r in range(1, world):
+                losses.append(nets[r].train_dp(None, None, 0, B, loss=True))
+            for r in range(world):
+                s, c = sh[r]
+                ref.train_grad(q[s:s + c], t[s:s + c], c, B, g[r])
+            gs = g[0]
+            for r in range(1, world):
+                gs = gs + g[r]
+            ref_loss = ref.train_apply(gs, loss=True)
+            assert losses == [ref_loss] * world, (it, losses, ref_loss)
+        for slot in SLOTS:
+            want = ref.get_state(getattr(nrc.StateSlot, slot))
+            for r in range(world):
+                np.testing.assert_array_equal(nets[r].get_state(getattr(nrc.StateSlot, slot)), want, err_msg=f"{slot} rank {r}")
+        assert all(n.step == 3 for n in nets)
+    finally:
+        for n in nets:
+            n.peer_exchange_close()
+        for n in nets:
+            n.destroy()
+        ref.destroy()
+
+
+def test_fused_peer_exchange_missing_peer_times_out(nrc, torch, dev, golden, knobs):
+    """VERDICT r04 item 1, negative case: rank 0 of a world-2 exchange runs the fused kernel while rank 1 never pushes.
+    With the wait bounded to 2^13 polls (knob px_polls) the step must end with NRC_ERR_INTERNAL (the sticky protocol
+    error) within seconds, not hang; the handle stays poisoned until nrc_init, and the peer is unaffected."""
+    import time
+
+    knobs("px_polls", 1 << 13)
+    knobs("peer_path", 1)
+    a, b = nrc.Network(), nrc.Network()
+    for n in (a, b):
+        n.init(stream=torch.cuda.current_stream())
+        n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+    nrc.Network.peer_exchange_open_local([a, b])
+    q_np, t_np = nrc.synthetic.cornell_batch(4096, seed=5)
+    q, t = to_dev(torch, dev, q_np), to_dev(torch, dev, t_np)
+    try:
+        t0 = time.perf_counter()
+        with pytest.raises(nrc.NrcError) as e:
+            a.train_dp(q[:2048], t[:2048], 2048, 4096, loss=True)
+        dt = time.perf_counter() - t0
+        assert e.value.status == 7 and "peer" in str(e.value), str(e.value)
+        assert dt < 5.0, dt
+        with pytest.raises(nrc.NrcError) as e:
+            a.train_dp(q[:2048], t[:2048], 2048, 4096)
+        assert e.value.status == 7
+        knobs("peer_path", -1)
+        b_state = b.get_state(nrc.StateSlot.PARAMS)
+        np.testing.assert_array_equal(b_state, golden["params_b"])
+    finally:
+        for n in (a, b):
+            n.peer_exchange_close()
+        for n in (a, b):
+            n.destroy()
+
+
+def test_peer_exchange_local_argument_checks(nrc, torch, dev, knobs):
+    nets = [nrc.Network() for _ in range(2)]
+    for n in nets:
+        n.init(stream=torch.cuda.current_stream())
+    h = nrc.Network()
+    h.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+    try:
+        with pytest.raises(nrc.NrcError) as e:
+            nrc.Network.peer_exchange_open_local([nets[0], h])
+        assert e.value.status == 5
+        with pytest.raises(nrc.NrcError):
+            nrc.Network.peer_exchange_open_local([nets[0], nets[0]])
+        with pytest.raises(nrc.NrcError):
+            nets[0].set_peer_seq(5)  # no exchange open
+        nrc.Network.peer_exchange_open_local(nets)
+        with pytest.raises(nrc.NrcError):
+            nets[0].set_peer_seq(0)
+        knobs("peer_path", 4)
+        with pytest.raises(nrc.NrcError) as e:  # nothing pushed yet
+            nets[1].train_dp(None, None, 0, 16)
+        assert e.value.status == 1
+        for k, v in (("peer_path", 5), ("px_polls", 0), ("px_polls", (1 << 21) + 1)):
+            with pytest.raises(nrc.NrcError):
+                knobs(k, v)
+    finally:
+        for n in nets:
+            n.peer_exchange_close()
+        for n in nets + [h]:
+            n.destroy()

@@ -131,3 +131,29 @@ def test_trained_weights_full_frame(nrc, orc, torch, dev, tnet):
     print(f"trained weights, 2^21 frame, {idx.size} rows: rel-L2 vs ORC_TCNN {r:.2e}")
     assert r <= 1e-3
     assert np.isfinite(y).all()
+
+
+def test_process_frame_on_a_tcnn_numerics_handle(nrc, torch, dev, tnet):
+    """a handle with infer_precision F16_ACC16 has no fused accumulation epilogue, so nrc_process_frame in
+    Full mode (default frame params) takes infer + accumulate_render_radiance instead of failing with UNSUPPORTED; the
+    frame buffer is bitwise that of the same two calls made by hand (training off, so the weights do not move)."""
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(160, 96, (8, 8), seed=11)
+    S, T = f.screen_size, f.num_tiles
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    cap = F.NUM_TRAINING_RECORDS_PER_FRAME
+    fb = F.FrameBuffers(t(f.queries_inference), torch.zeros((S + T, 3), device=dev), t(f.last_render_throughput),
+                        torch.full((S, 4), 0.25, device=dev), F.records_to_device(f.end_vertices, dev),
+                        F.records_to_device(np.zeros(cap, F.TRAINING_RECORD_DTYPE), dev),
+                        [torch.zeros((cap, 15), device=dev), torch.zeros((cap, 15), device=dev)],
+                        [torch.zeros((cap, 3), device=dev), torch.zeros((cap, 3), device=dev)])
+    fp = F.FrameParams(S, T, 0, F.RenderMode.Full, 3, 3, 1, train=False)
+    F.process_frame(tnet, fb, fp, loss=False)
+    rad = torch.zeros((S + T, 3), device=dev)
+    tnet.infer(t(f.queries_inference), rad, S + T)
+    rgba = torch.full((S, 4), 0.25, device=dev)
+    F.accumulate_render_radiance(rad, t(f.last_render_throughput), rgba, S, F.RenderMode.Full, 3,
+                                 stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(fb.output_rgba, rgba)
+    assert torch.equal(fb.results_inference[S:], rad[S:])
