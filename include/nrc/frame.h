@@ -116,6 +116,16 @@ nrc_status nrc_propagate_train_radiance_factored(const nrc_train_suffix_end_vert
 nrc_status nrc_generate_train_permutation(uint64_t seed, uint32_t frame_index, int32_t* permutation_d, uint32_t n,
                                           hipStream_t stream);
 
+/* The reference's shuffle itself (NRCUtil.cu:19-35): cub::DeviceRadixSort::SortPairs(keys, [0, n)) over key bits
+ * [0, 32) -- the permutation a STABLE sort of the caller's 32-bit keys makes of the indices (ascending keys, equal keys in
+ * index order), e.g. of the renderer's 65,536 curand keys or a recorded key section (nrc/stream.h). permutation_d[n]
+ * receives the sorted indices, sorted_keys_d (may be NULL) the sorted keys; no buffer may overlap another. temp_d: device
+ * memory of at least nrc_sort_train_permutation_temp_bytes(n) bytes (4-byte aligned). 1 <= n <= 2^24; n = 0 is a
+ * no-op. An LSD radix sort of 8-bit digits, two launches per digit. */
+size_t nrc_sort_train_permutation_temp_bytes(uint32_t n);
+nrc_status nrc_sort_train_permutation(const uint32_t* keys_d, uint32_t* sorted_keys_d, int32_t* permutation_d,
+                                      uint32_t n, void* temp_d, size_t temp_bytes, hipStream_t stream);
+
 /* permute_train_data (nrc_helpers.cu:226-249): for d in [0, n_out):
  *     s = perm(d) % min(num_records, n_out);  queries_dst[d] = queries_src[s];  targets_dst[d] = targets_src[s]
  * perm(d) = permutation_d[d] if permutation_d != NULL (any caller-made permutation, e.g. the reference's
@@ -160,7 +170,11 @@ typedef struct nrc_frame_buffers {
     const nrc_training_record* train_records_d;   /* [65536] */
     float* train_queries_d[2];                    /* DoubleBuffer<RadianceQuery>: [0] as traced, [1] shuffled */
     nrc_float3* train_targets_d[2];               /* DoubleBuffer<float3>: [0] emission so far (+= propagation) */
-    const int32_t* permutation_d;                 /* NULL: Feistel permutation of (shuffle_seed, frame_index) */
+    const int32_t* permutation_d;                 /* NULL: the key sort below, or the Feistel permutation of
+                                                     (shuffle_seed, frame_index) */
+    const uint32_t* shuffle_keys_d;               /* [65536] keys whose stable sort gives the permutation
+                                                     (nrc_sort_train_permutation; the reference's curand keys); used
+                                                     when permutation_d is NULL; NULL: Feistel */
 } nrc_frame_buffers;
 
 typedef struct nrc_frame_params {

@@ -40,7 +40,9 @@ typedef enum nrc_stream_section {
     NRC_SEC_RESULTS_INFERENCE = 8,      /* (screen + tiles) x float3: recorded infer() outputs (for comparison) */
     NRC_SEC_OUTPUT_RGBA = 9,            /* screen x float4: recorded frame buffer after accumulation */
     NRC_SEC_LOSSES = 10,                /* NUM_BATCHES x f32: recorded minibatch losses */
-    NRC_SEC_COUNT = 11
+    NRC_SEC_SHUFFLE_KEYS = 11,          /* capacity x u32: the frame's shuffle keys (the reference's curand keys,
+                                           NRCUtil.cu:25); the permutation is their stable sort (frame.h) */
+    NRC_SEC_COUNT = 12
 } nrc_stream_section;
 
 typedef struct nrc_stream_frame_header {

@@ -55,7 +55,8 @@ EXPORTS = [
     "nrc_accumulate_render_radiance_factored", "nrc_copy_radiance_to_output_factored", "nrc_propagate_train_radiance_factored",
     "nrc_accumulate_render_radiance_factored_padded", "nrc_copy_radiance_to_output_factored_padded",
     "nrc_propagate_train_radiance_factored_padded", "nrc_permute_train_data_padded",
-    "nrc_generate_train_permutation", "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
+    "nrc_generate_train_permutation", "nrc_sort_train_permutation_temp_bytes", "nrc_sort_train_permutation",
+    "nrc_permute_train_data", "nrc_process_frame", "nrc_process_frame_shard",
     # include/nrc/stream.h (bound in stream.py)
     "nrc_stream_section_bytes", "nrc_stream_create", "nrc_stream_create_layout", "nrc_stream_query_layout",
     "nrc_stream_open", "nrc_stream_close",

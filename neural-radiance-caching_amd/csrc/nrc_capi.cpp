@@ -323,6 +323,8 @@ struct nrc_net {
     ncclComm_t comm = nullptr;       // attached RCCL communicator (not owned), nrc_set_comm
     int comm_rank = 0, comm_world = 1;
     float* dp_grad = nullptr;        // [grad_floats] gradient exchange buffer of nrc_train_dp
+    void* frame_scratch = nullptr;   // frame driver scratch (net_frame_scratch): the key sort's permutation + temp
+    size_t frame_scratch_bytes = 0;
     float* loss_dev = nullptr;   // device view of loss_host
     float* loss_host = nullptr;
     // training-protocol error word (round 4), in the same mapped allocation as the loss slots (index kProtoErrSlot):
@@ -445,6 +447,9 @@ struct nrc_net {
         work_queue = nullptr;
         f(dp_grad);
         dp_grad = nullptr;
+        f(frame_scratch);
+        frame_scratch = nullptr;
+        frame_scratch_bytes = 0;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer); f(hash_feat);
         hash_feat = nullptr;
         if (feat_done) (void)hipEventDestroy(feat_done);
@@ -752,6 +757,21 @@ bool nrc_amd::net_comm(nrc_net* net, int* rank, int* world) {
     *rank = net->comm_rank;
     *world = net->comm_world;
     return net->comm != nullptr;
+}
+
+void* nrc_amd::net_frame_scratch(nrc_net* net, size_t bytes) {
+    check_live(net);
+    if (bytes > net->frame_scratch_bytes) {
+        if (net->frame_scratch) {
+            HIP_CHECK(hipStreamSynchronize(net->stream));  // a queued kernel may still use the old buffer
+            HIP_CHECK(hipFree(net->frame_scratch));
+        }
+        net->frame_scratch = nullptr;
+        net->frame_scratch_bytes = 0;
+        HIP_CHECK(hipMalloc(&net->frame_scratch, bytes));
+        net->frame_scratch_bytes = bytes;
+    }
+    return net->frame_scratch;
 }
 
 bool nrc_amd::net_infer_fusable(nrc_net* net) {

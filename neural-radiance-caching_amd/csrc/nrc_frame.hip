@@ -6,6 +6,8 @@
 // (CMakeLists.txt:256-257), so results are bit-identical to the oracle (oracle/nrc_frame_oracle.c).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "nrc_internal.h"
 
 namespace nrc_amd {
@@ -200,6 +202,89 @@ __global__ __launch_bounds__(256) void permute_kernel(const uint32_t* __restrict
         td[gg] = ts[(size_t)s * 3u + k];
 }
 
+
+// ---- the reference's own shuffle contract (NRCUtil.cu:19-35): cub::DeviceRadixSort::SortPairs of caller-supplied u32
+// keys with the values [0, n), bits [0, 32) -- an LSD radix sort, so equal keys keep index order. Four passes of 8-bit
+// digits; a pass = sort_hist_kernel (per-block digit counts, digit-major [d][block]) + sort_scatter_kernel (each block
+// derives its digits' output bases from the whole count table, then its 4 waves scatter their contiguous ranges in
+// order, 64 keys at a time, ranking equal digits inside the wave by ballot matching). At most kSortBlocks blocks: the
+// reference's 65,536 keys are 64 blocks of 1,024.
+constexpr uint32_t kSortBlocks = 64;
+
+__global__ __launch_bounds__(256) void sort_hist_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t chunk,
+                                                        int shift, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+    for (uint32_t i = b0 + threadIdx.x; i < b1; i += 256u) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+
+// vin == nullptr: the values are the indices (the first pass of SortPairs(keys, iota))
+__global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __restrict__ kin, const int* __restrict__ vin,
+                                                           uint32_t* __restrict__ kout, int* __restrict__ vout,
+                                                           uint32_t n, uint32_t chunk, int shift,
+                                                           const uint32_t* __restrict__ hist) {
+    __shared__ uint32_t tot[256];     // digit totals, then their inclusive scan
+    __shared__ uint32_t cnt[4][256];  // per-wave digit counts, then each wave's next output position per digit
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const uint32_t nblk = gridDim.x, b = blockIdx.x;
+    // digit tid: its count over all blocks and over the blocks before this one
+    uint32_t total = 0u, before = 0u;
+    for (uint32_t q = 0; q < nblk; ++q) {
+        const uint32_t c = hist[tid * nblk + q];
+        total += c;
+        before += q < b ? c : 0u;
+    }
+    tot[tid] = total;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cnt[j][tid] = 0u;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const uint32_t v = tid >= off ? tot[tid - off] : 0u;
+        __syncthreads();
+        tot[tid] += v;
+        __syncthreads();
+    }
+    const uint32_t dbase = tot[tid] - total + before;  // first output slot of digit tid in this block
+    const uint32_t per = chunk / 4u, w0 = b * chunk + (uint32_t)w * per, w1 = min(n, w0 + per);
+    for (uint32_t i = w0 + lane; i < w1; i += 64u) atomicAdd(&cnt[w][(kin[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    uint32_t run = dbase;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t c = cnt[j][tid];
+        cnt[j][tid] = run;
+        run += c;
+    }
+    __syncthreads();
+    // wave w: its range in order, 64 at a time (the loop is wave-uniform); lanes holding the same digit are matched
+    // by 8 ballots, rank = the matching lanes below this one, the lowest of them advances the digit's position
+    for (uint32_t i0 = w0; i0 < w1; i0 += 64u) {
+        const uint32_t i = i0 + lane;
+        const bool valid = i < w1;
+        const uint32_t key = valid ? kin[i] : 0u;
+        const int val = valid ? (vin ? vin[i] : (int)i) : 0;
+        const uint32_t d = (key >> shift) & 255u;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const bool set = (d >> bit) & 1u;
+            const uint64_t bb = __ballot(set);
+            m &= set ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & __lanemask_lt());
+        const uint32_t base = cnt[w][d];
+        if (valid && rank == 0u) cnt[w][d] = base + (uint32_t)__popcll(m);
+        if (valid) {
+            kout[base + rank] = key;
+            vout[base + rank] = val;
+        }
+    }
+}
+
 FeistelKey make_key(uint64_t seed, uint32_t frame, uint32_t n) {
     auto mix = [](uint32_t x) {
         x ^= x >> 16;
@@ -303,6 +388,32 @@ hipError_t launch_permute(const float* qs, const float* ts, const int* perm, uin
                            reinterpret_cast<const uint32_t*>(qs), reinterpret_cast<const uint32_t*>(ts), perm,
                            make_key(seed, frame, n_out), nrec, reinterpret_cast<uint32_t*>(qd),
                            reinterpret_cast<uint32_t*>(td));
+    return hipGetLastError();
+}
+
+// Temporary storage of launch_sort_pairs: ping keys + values, second key buffer, the digit-count table.
+size_t sort_pairs_temp_bytes(uint32_t n) { return sizeof(uint32_t) * (3 * (size_t)n + 256 * kSortBlocks); }
+
+hipError_t launch_sort_pairs(const uint32_t* keys, uint32_t* keys_out, int* vals_out, uint32_t n, void* temp,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (!keys || !vals_out || !temp) return hipErrorInvalidValue;
+    const uint32_t nblk = std::min<uint32_t>(kSortBlocks, (n + 1023u) / 1024u);
+    const uint32_t chunk = ((n + nblk - 1u) / nblk + 255u) / 256u * 256u;  // elements per block, 64 per wave-step
+    uint32_t* kA = static_cast<uint32_t*>(temp);
+    int* vA = reinterpret_cast<int*>(kA + n);
+    uint32_t* kB = kA + 2 * (size_t)n;
+    uint32_t* hist = kA + 3 * (size_t)n;
+    // pass p reads (ki, vi), writes (ko, vo): keys -> A -> B/vals_out -> A -> keys_out/B, vals_out
+    const uint32_t* ki[4] = {keys, kA, kB, kA};
+    const int* vi[4] = {nullptr, vA, vals_out, vA};
+    uint32_t* ko[4] = {kA, kB, kA, keys_out ? keys_out : kB};
+    int* vo[4] = {vA, vals_out, vA, vals_out};
+    for (int p = 0; p < 4; ++p) {
+        hipLaunchKernelGGL(sort_hist_kernel, dim3(nblk), dim3(256), 0, s, ki[p], n, chunk, 8 * p, hist);
+        hipLaunchKernelGGL(sort_scatter_kernel, dim3(nblk), dim3(256), 0, s, ki[p], vi[p], ko[p], vo[p], n, chunk, 8 * p,
+                           hist);
+    }
     return hipGetLastError();
 }
 

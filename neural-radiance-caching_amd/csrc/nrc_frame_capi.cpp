@@ -153,6 +153,22 @@ nrc_status nrc_generate_train_permutation(uint64_t seed, uint32_t frame, int32_t
     });
 }
 
+size_t nrc_sort_train_permutation_temp_bytes(uint32_t n) { return sort_pairs_temp_bytes(n); }
+
+nrc_status nrc_sort_train_permutation(const uint32_t* keys, uint32_t* sorted_keys, int32_t* perm, uint32_t n,
+                                      void* temp, size_t temp_bytes, hipStream_t stream) {
+    return guarded([&] {
+        if (n == 0) return;
+        require(n <= (1u << 24), "n must be <= 2^24");
+        require(keys && aligned(keys, 4), "keys must be non-NULL and 4-byte aligned");
+        require(perm && aligned(perm, 4), "permutation buffer must be non-NULL and 4-byte aligned");
+        require(!sorted_keys || aligned(sorted_keys, 4), "sorted_keys must be 4-byte aligned");
+        require(temp && aligned(temp, 4) && temp_bytes >= sort_pairs_temp_bytes(n),
+                "temp must be 4-byte aligned and hold nrc_sort_train_permutation_temp_bytes(n) bytes");
+        HIP_CHECK(launch_sort_pairs(keys, sorted_keys, perm, n, temp, stream));
+    });
+}
+
 namespace {
 nrc_status permute_train(const float* qs, const nrc_float3* ts, const int32_t* perm, uint64_t seed, uint32_t frame,
                          int32_t num_records, float* qd, nrc_float3* td, uint32_t n_out, hipStream_t stream, bool padq) {
@@ -266,8 +282,17 @@ void process_frame(nrc_net* net, const nrc_frame_buffers* fb, const nrc_frame_pa
     else
         check(nrc_propagate_train_radiance(fb->end_vertices_d, fb->results_inference_d + screen, tiles,
                                            fb->train_records_d, fb->train_targets_d[0], (uint32_t)nrec, s));
-    // Device::nrcShuffleTrainingData (Device.cpp:1427-1469)
-    check(permute_train(fb->train_queries_d[0], fb->train_targets_d[0], fb->permutation_d, p->shuffle_seed,
+    // Device::nrcShuffleTrainingData (Device.cpp:1427-1469). The permutation: the caller's, else the stable sort of the
+    // caller's keys (the reference's curand keys + cub radix sort, NRCUtil.cu:19-35), else the Feistel permutation
+    const int32_t* perm = fb->permutation_d;
+    if (!perm && fb->shuffle_keys_d) {
+        const uint32_t N = NRC_NUM_TRAINING_RECORDS_PER_FRAME;
+        char* scratch = static_cast<char*>(net_frame_scratch(net, sizeof(int32_t) * N + sort_pairs_temp_bytes(N)));
+        int32_t* sorted = reinterpret_cast<int32_t*>(scratch);
+        HIP_CHECK(launch_sort_pairs(fb->shuffle_keys_d, nullptr, sorted, N, scratch + sizeof(int32_t) * N, s));
+        perm = sorted;
+    }
+    check(permute_train(fb->train_queries_d[0], fb->train_targets_d[0], perm, p->shuffle_seed,
                         p->frame_index, nrec, fb->train_queries_d[1], fb->train_targets_d[1],
                         NRC_NUM_TRAINING_RECORDS_PER_FRAME, s, padq));
     // Device::nrcTrainRadiance (Device.cpp:1473-1512): NUM_BATCHES steps, mean loss. The minibatch losses

@@ -420,6 +420,8 @@ namespace nrc_amd {
 nrc_loss_slots net_loss_slots(nrc_net* net);
 // the attached communicator (nrc_set_comm): false if none; rank / world of it
 bool net_comm(nrc_net* net, int* rank, int* world);
+// per-handle device scratch of the frame driver (grown on demand, freed with the handle; stream-ordered use only)
+void* net_frame_scratch(nrc_net* net, size_t bytes);
 // the handle's RadianceQuery records are padded (nrc_config.query_layout = NRC_QUERY_PADDED)
 bool net_padq(nrc_net* net);
 // inference can take the fused accumulation epilogue (not with NRC_PRECISION_F16_ACC16)
@@ -438,6 +440,11 @@ hipError_t launch_propagate(const void* ends, const float* end_rad, uint32_t til
                             float* targets, uint32_t nrec, hipStream_t s, const float* end_queries = nullptr,
                             const float* train_queries = nullptr, bool padq = false);
 hipError_t launch_permutation(uint64_t seed, uint32_t frame, int* perm, uint32_t n, hipStream_t s);
+// the reference's shuffle contract (NRCUtil.cu:19-35): stable LSD radix sort of (keys[i], i) over 32 key bits; vals_out
+// receives the sorted indices, keys_out (may be null) the sorted keys; temp: sort_pairs_temp_bytes(n) bytes
+size_t sort_pairs_temp_bytes(uint32_t n);
+hipError_t launch_sort_pairs(const uint32_t* keys, uint32_t* keys_out, int* vals_out, uint32_t n, void* temp,
+                             hipStream_t s);
 hipError_t launch_permute(const float* qs, const float* ts, const int* perm, uint64_t seed, uint32_t frame,
                           uint32_t nrec, float* qd, float* td, uint32_t n_out, hipStream_t s, bool padq = false);
 

@@ -208,6 +208,7 @@ int main(int argc, char** argv) {
     float* tq[2] = {dalloc<float>(cap * QD), dalloc<float>(cap * QD)};
     nrc_float3* tt[2] = {dalloc<nrc_float3>(cap), dalloc<nrc_float3>(cap)};
     int32_t* perm = dalloc<int32_t>(cap);
+    uint32_t* keys = dalloc<uint32_t>(cap);
     fb.queries_inference_d = queries_inference;
     fb.results_inference_d = results_inference;
     fb.last_render_throughput_d = throughput;
@@ -221,7 +222,7 @@ int main(int argc, char** argv) {
     fb.train_targets_d[0] = tt[0];
     fb.train_targets_d[1] = tt[1];
     void* const dst[NRC_SEC_COUNT] = {queries_inference, throughput, queries_vis, ends, records, tq[0], tt[0], perm,
-                                      nullptr, nullptr, nullptr};
+                                      nullptr, nullptr, nullptr, keys};
 
     nrc_net* net = nullptr;
     NRC(nrc_create(&net));
@@ -249,6 +250,7 @@ int main(int argc, char** argv) {
         for (int sec = 0; sec < NRC_SEC_COUNT; ++sec)
             if (dst[sec] && (h.sections & (1u << sec))) NRC(nrc_stream_read_section(s, sec, dst[sec], stream));
         fb.permutation_d = (h.sections & (1u << NRC_SEC_PERMUTATION)) ? perm : nullptr;
+        fb.shuffle_keys_d = (h.sections & (1u << NRC_SEC_SHUFFLE_KEYS)) ? keys : nullptr;
         nrc_frame_params p{};
         p.screen_size = h.screen_size;
         p.num_tiles = h.num_tiles;

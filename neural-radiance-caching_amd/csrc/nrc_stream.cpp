@@ -127,6 +127,7 @@ uint64_t nrc_stream_section_bytes(const nrc_stream_frame_header* h, int section)
     case NRC_SEC_RESULTS_INFERENCE: return (screen + tiles) * f3;
     case NRC_SEC_OUTPUT_RGBA: return screen * 4 * sizeof(float);
     case NRC_SEC_LOSSES: return NRC_NUM_BATCHES * sizeof(float);
+    case NRC_SEC_SHUFFLE_KEYS: return (uint64_t)NRC_NUM_TRAINING_RECORDS_PER_FRAME * sizeof(uint32_t);
     default: return 0;
     }
 }

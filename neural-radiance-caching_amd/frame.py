@@ -88,6 +88,7 @@ def _sigs():
         "nrc_copy_radiance_to_output_factored": [vp, vp, vp, u32, vp],
         "nrc_propagate_train_radiance_factored": [vp, vp, vp, u32, vp, vp, vp, u32, vp],
         "nrc_generate_train_permutation": [u64, u32, vp, u32, vp],
+        "nrc_sort_train_permutation": [vp, vp, vp, u32, vp, ctypes.c_size_t, vp],
         "nrc_permute_train_data": [vp, vp, vp, u64, u32, i32, vp, vp, u32, vp],
         "nrc_accumulate_render_radiance_factored_padded": [vp, vp, vp, vp, u32, ctypes.c_int, u32, vp],
         "nrc_copy_radiance_to_output_factored_padded": [vp, vp, vp, u32, vp],
@@ -111,7 +112,7 @@ class NrcFrameBuffers(ctypes.Structure):
                 ("queries_cache_vis_d", ctypes.c_void_p), ("results_cache_vis_d", ctypes.c_void_p),
                 ("end_vertices_d", ctypes.c_void_p), ("train_records_d", ctypes.c_void_p),
                 ("train_queries_d", ctypes.c_void_p * 2), ("train_targets_d", ctypes.c_void_p * 2),
-                ("permutation_d", ctypes.c_void_p)]
+                ("permutation_d", ctypes.c_void_p), ("shuffle_keys_d", ctypes.c_void_p)]
 
 
 class NrcFrameParams(ctypes.Structure):
@@ -173,6 +174,26 @@ def generate_train_permutation(seed: int, frame_index: int, permutation, n: int,
                                                  int(n), _stream(stream)))
 
 
+def sort_train_permutation_temp_bytes(n: int) -> int:
+    L = lib()
+    fn = L.nrc_sort_train_permutation_temp_bytes
+    fn.restype, fn.argtypes = ctypes.c_size_t, [ctypes.c_uint32]
+    return int(fn(int(n)))
+
+
+def sort_train_permutation(keys, permutation, n: int, sorted_keys=None, temp=None, stream=None) -> None:
+    """The reference's shuffle (NRCUtil.cu:19-35): permutation[0:n] = the indices of a stable sort of the u32 keys
+    (cub::DeviceRadixSort::SortPairs(keys, iota)); sorted_keys (optional) = the sorted keys. Device tensors of 4-byte
+    elements; temp: a device buffer of sort_train_permutation_temp_bytes(n) bytes (allocated here if None)."""
+    if temp is None:
+        import torch
+        temp = torch.empty(max(1, sort_train_permutation_temp_bytes(n)), dtype=torch.uint8, device=keys.device)
+    nbytes = temp.numel() * temp.element_size() if hasattr(temp, "numel") else sort_train_permutation_temp_bytes(n)
+    check(_sigs().nrc_sort_train_permutation(_ptr(keys, "keys"), _ptr(sorted_keys, "sorted_keys"),
+                                             _ptr(permutation, "permutation"), int(n), _ptr(temp, "temp"), int(nbytes),
+                                             _stream(stream)))
+
+
 def permute_train_data(queries_src, targets_src, permutation, seed: int, frame_index: int, num_records: int,
                        queries_dst, targets_dst, n_out: int = NUM_TRAINING_RECORDS_PER_FRAME, stream=None,
                        padded: bool = False) -> None:
@@ -208,6 +229,7 @@ class FrameBuffers:
     queries_cache_vis: object = None
     results_cache_vis: object = None
     permutation: object = None
+    shuffle_keys: object = None  # u32 keys (any 4-byte dtype) whose stable sort is the permutation (frame.h)
     _keep: list = field(default_factory=list)
 
     def as_struct(self) -> NrcFrameBuffers:
@@ -225,6 +247,7 @@ class FrameBuffers:
         fb.train_targets_d[0] = _ptr(self.train_targets[0], "train_targets[0]")
         fb.train_targets_d[1] = _ptr(self.train_targets[1], "train_targets[1]")
         fb.permutation_d = _ptr(self.permutation, "permutation")
+        fb.shuffle_keys_d = _ptr(self.shuffle_keys, "shuffle_keys")
         return fb
 
 

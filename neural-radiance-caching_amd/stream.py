@@ -26,11 +26,11 @@ FRAME_TAG = b"FRME"
 CAPACITY = NUM_TRAINING_RECORDS_PER_FRAME
 
 (QUERIES_INFERENCE, LAST_RENDER_THROUGHPUT, QUERIES_CACHE_VIS, END_VERTICES, TRAIN_RECORDS, TRAIN_QUERIES,
- TRAIN_TARGETS, PERMUTATION, RESULTS_INFERENCE, OUTPUT_RGBA, LOSSES) = range(11)
-SECTION_COUNT = 11
+ TRAIN_TARGETS, PERMUTATION, RESULTS_INFERENCE, OUTPUT_RGBA, LOSSES, SHUFFLE_KEYS) = range(12)
+SECTION_COUNT = 12
 SECTION_NAMES = ["queries_inference", "last_render_throughput", "queries_cache_vis", "end_vertices",
                  "train_records", "train_queries", "train_targets", "permutation", "results_inference",
-                 "output_rgba", "losses"]
+                 "output_rgba", "losses", "shuffle_keys"]
 
 _FILE_HDR = struct.Struct("<8s10I2Q")       # 64 B
 _FRAME_HDR = struct.Struct("<4s2Ii2IiI4x2Q12x")  # tag + nrc_stream_frame_header (48) + 12 pad = 64 B
@@ -64,7 +64,7 @@ def section_shape(h: FrameHeader, sec: int, query_dims: int = 15):
         TRAIN_RECORDS: (n, TRAINING_RECORD_DTYPE, ()), TRAIN_QUERIES: (n, np.float32, (qd,)),
         TRAIN_TARGETS: (n, np.float32, (3,)), PERMUTATION: (CAPACITY, np.int32, ()),
         RESULTS_INFERENCE: (s + t, np.float32, (3,)), OUTPUT_RGBA: (s, np.float32, (4,)),
-        LOSSES: (NUM_BATCHES, np.float32, ()),
+        LOSSES: (NUM_BATCHES, np.float32, ()), SHUFFLE_KEYS: (CAPACITY, np.uint32, ()),
     }[sec]
 
 
@@ -289,12 +289,13 @@ class Replayer:
         self.train_queries = [z(CAPACITY, 15), z(CAPACITY, 15)]
         self.train_targets = [z(CAPACITY, 3), z(CAPACITY, 3)]
         self.permutation = z(CAPACITY, dtype=torch.int32)
+        self.shuffle_keys = z(CAPACITY, dtype=torch.int32)  # u32 keys, held as int32 bytes
 
-    def buffers(self, has_perm: bool) -> FrameBuffers:
+    def buffers(self, has_perm: bool, has_keys: bool = False) -> FrameBuffers:
         return FrameBuffers(self.queries_inference, self.results_inference, self.last_render_throughput,
                             self.output_rgba, self.end_vertices, self.train_records, self.train_queries,
                             self.train_targets, self.queries_cache_vis, self.results_cache_vis,
-                            self.permutation if has_perm else None)
+                            self.permutation if has_perm else None, self.shuffle_keys if has_keys else None)
 
 
 def replay(path, net, device, keep_outputs: bool = False, loss: bool = True) -> ReplayResult:
@@ -313,7 +314,7 @@ def replay(path, net, device, keep_outputs: bool = False, loss: bool = True) -> 
     targets = {QUERIES_INFERENCE: rp.queries_inference, LAST_RENDER_THROUGHPUT: rp.last_render_throughput,
                QUERIES_CACHE_VIS: rp.queries_cache_vis, END_VERTICES: rp.end_vertices,
                TRAIN_RECORDS: rp.train_records, TRAIN_QUERIES: rp.train_queries[0],
-               TRAIN_TARGETS: rp.train_targets[0], PERMUTATION: rp.permutation}
+               TRAIN_TARGETS: rp.train_targets[0], PERMUTATION: rp.permutation, SHUFFLE_KEYS: rp.shuffle_keys}
     stream = torch.cuda.current_stream()
     with CStream(path) as cs:
         while (h := cs.next_frame()) is not None:
@@ -322,7 +323,7 @@ def replay(path, net, device, keep_outputs: bool = False, loss: bool = True) -> 
             for sec, dst in targets.items():
                 if h.sections & (1 << sec):
                     cs.read_section(sec, dst, stream)
-            l = process_frame(net, rp.buffers(bool(h.sections & (1 << PERMUTATION))),
+            l = process_frame(net, rp.buffers(bool(h.sections & (1 << PERMUTATION)), bool(h.sections & (1 << SHUFFLE_KEYS))),
                               FrameParams(h.screen_size, h.num_tiles, h.num_training_records,
                                           RenderMode(h.render_mode), h.iteration_index, h.frame_index,
                                           h.shuffle_seed), loss=loss)

@@ -16,6 +16,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 typedef struct { float x, y, z; } f3;
@@ -229,6 +230,38 @@ void orc_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n) {
         while (x >= n) x = feistel(x, h, k);
         perm[d] = (int32_t)x;
     }
+}
+
+/* The reference's shuffle contract itself, NRCUtil.cu:19-35: cub::DeviceRadixSort::SortPairs(keys, values = the
+ * indices 0..n-1 (Device.cpp:1187-1192), n, begin_bit 0, end_bit 32). cub (absent from the snapshot; CUDA toolkit
+ * library) documents SortPairs as a stable least-significant-digit radix sort: ascending keys, pairs with equal keys in
+ * their input order. Restated as cub's algorithm: LSD passes over 8-bit digits, each a stable counting sort.
+ * sorted_keys may be NULL. */
+void orc_sort_pairs(const uint32_t* keys, uint32_t* sorted_keys, int32_t* perm, uint32_t n) {
+    if (n == 0) return;
+    uint32_t* ka = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    uint32_t* kb = (uint32_t*)malloc(sizeof(uint32_t) * n);
+    int32_t* va = (int32_t*)malloc(sizeof(int32_t) * n);
+    int32_t* vb = (int32_t*)malloc(sizeof(int32_t) * n);
+    for (uint32_t i = 0; i < n; i++) {
+        ka[i] = keys[i];
+        va[i] = (int32_t)i;
+    }
+    for (int shift = 0; shift < 32; shift += 8) {
+        uint32_t count[257] = {0};
+        for (uint32_t i = 0; i < n; i++) count[((ka[i] >> shift) & 255U) + 1]++;
+        for (int d = 0; d < 256; d++) count[d + 1] += count[d];
+        for (uint32_t i = 0; i < n; i++) { /* in input order: stable */
+            const uint32_t pos = count[(ka[i] >> shift) & 255U]++;
+            kb[pos] = ka[i];
+            vb[pos] = va[i];
+        }
+        uint32_t* tk = ka; ka = kb; kb = tk;
+        int32_t* tv = va; va = vb; vb = tv;
+    }
+    memcpy(perm, va, sizeof(int32_t) * n);
+    if (sorted_keys) memcpy(sorted_keys, ka, sizeof(uint32_t) * n);
+    free(ka); free(kb); free(va); free(vb);
 }
 
 /* permute_train_data, nrc_helpers.cu:226-249. perm == NULL: the Feistel permutation of (seed, frame)

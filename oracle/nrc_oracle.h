@@ -102,6 +102,7 @@ void orc_propagate_factored(const void* end_vertices, const float* end_radiance,
                             int64_t num_records);
 void orc_feistel_keys(uint64_t seed, uint32_t frame, uint32_t keys[4]);
 void orc_permutation(uint64_t seed, uint32_t frame, int32_t* perm, uint32_t n);
+void orc_sort_pairs(const uint32_t* keys, uint32_t* sorted_keys, int32_t* perm, uint32_t n);
 void orc_permute(const float* q_src, const float* t_src, const int32_t* perm, uint64_t seed, uint32_t frame,
                  int32_t num_records, float* q_dst, float* t_dst, uint32_t n_out);
 

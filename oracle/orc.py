@@ -58,6 +58,7 @@ def lib() -> ctypes.CDLL:
         L.orc_propagate_factored.argtypes = [vp, vp, vp, i64, vp, vp, vp, i64]
         L.orc_feistel_keys.argtypes = [u64, u32, vp]
         L.orc_permutation.argtypes = [u64, u32, vp, u32]
+        L.orc_sort_pairs.argtypes = [vp, vp, vp, u32]
         L.orc_permute.argtypes = [vp, vp, vp, u64, u32, ctypes.c_int32, vp, vp, u32]
         L.orc_hash_encode.argtypes = [vp, vp, i64, ctypes.c_int, vp]
         L.orc_hash_forward.argtypes = [vp, vp, i64, ctypes.c_int, vp, ctypes.c_int]
@@ -255,6 +256,17 @@ def permutation(seed: int, frame: int, n: int) -> np.ndarray:
     if n:
         lib().orc_permutation(int(seed), int(frame), _v(out), int(n))
     return out
+
+
+def sort_pairs(keys: np.ndarray):
+    """The reference's shuffle (NRCUtil.cu:19-35): (permutation, sorted keys) of cub::DeviceRadixSort::SortPairs over the
+    u32 keys and the indices (stable LSD radix sort)."""
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    perm = np.empty(k.size, np.int32)
+    sk = np.empty(k.size, np.uint32)
+    if k.size:
+        lib().orc_sort_pairs(_v(k), _v(sk), _v(perm), int(k.size))
+    return perm, sk
 
 
 def permute(q_src: np.ndarray, t_src: np.ndarray, perm, seed: int, frame: int, num_records: int, n_out: int,

@@ -20,7 +20,7 @@ void frame(nrc::Network& net, hipStream_t stream, float* queries, float* results
 #include "nrc/frame.h"
 static_assert(sizeof(nrc_training_record) == 28, "TrainingRecord");
 static_assert(sizeof(nrc_train_suffix_end_vertex) == 16, "TrainingSuffixEndVertex");
-static_assert(sizeof(nrc_frame_buffers) == 13 * sizeof(void*), "nrc_frame_buffers");
+static_assert(sizeof(nrc_frame_buffers) == 14 * sizeof(void*), "nrc_frame_buffers");
 static_assert(sizeof(nrc_frame_params) == 48, "nrc_frame_params");
 
 // the one-call frame and the recorder at the reference's dump point, as a renderer writes them.

@@ -114,6 +114,6 @@ def test_layout_header_matches_python_constants(nrc):
 def test_frame_struct_layouts(nrc):
     """ctypes mirrors of include/nrc/frame.h structs have the C sizes (static_asserts in tests/cpp/shim_compile.cpp)."""
     F = nrc.frame
-    assert ctypes.sizeof(F.NrcFrameBuffers) == 13 * 8
+    assert ctypes.sizeof(F.NrcFrameBuffers) == 14 * 8
     assert ctypes.sizeof(F.NrcFrameParams) == 48
     assert F.TRAINING_RECORD_DTYPE.itemsize == 28 and F.END_VERTEX_DTYPE.itemsize == 16

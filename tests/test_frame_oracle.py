@@ -255,3 +255,17 @@ def test_propagate_factored_matches_python(nrc, orc):
     np.testing.assert_array_max_ulp(got, want, maxulp=2)
     plain = orc.propagate(f.end_vertices, end_rad, f.train_records, f.train_targets, nrec)
     assert not np.array_equal(got, plain)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 1000, 65536])
+def test_sort_pairs_is_the_stable_argsort(orc, n):
+    """orc_sort_pairs (NRCUtil.cu:19-35, cub SortPairs over the indices): numpy's stable argsort of the same keys, with
+    ties (a small key range) and all-equal keys (identity)."""
+    rng = np.random.default_rng(n)
+    for keys in (rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32),
+                 rng.integers(0, 5, n).astype(np.uint32) * np.uint32(0x10001),
+                 np.full(n, 7, np.uint32)):
+        perm, sk = orc.sort_pairs(keys)
+        np.testing.assert_array_equal(perm, np.argsort(keys, kind="stable"))
+        np.testing.assert_array_equal(sk, np.sort(keys))
+    assert orc.sort_pairs(np.full(n, 3, np.uint32))[0].tolist() == list(range(n))

@@ -94,6 +94,84 @@ def test_permutation_bitwise(nrc, orc, dev, n):
     assert np.array_equal(np.sort(got), np.arange(n))
 
 
+def _keys(kind: str, n: int) -> np.ndarray:
+    rng = np.random.default_rng(n * 7 + len(kind))
+    if kind == "random":      # curand's 32-bit keys: few ties
+        return rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    if kind == "ties":        # many ties in every digit
+        return rng.integers(0, 300, n).astype(np.uint32) * np.uint32(0x01010101)
+    if kind == "equal":       # all equal: the permutation must be the identity (stable)
+        return np.full(n, 0xDEADBEEF, np.uint32)
+    if kind == "sorted_desc":
+        return (np.uint32(0xFFFFFFFF) - np.arange(n, dtype=np.uint32)).astype(np.uint32)
+    return (rng.integers(0, 4, n).astype(np.uint32) << np.uint32(30))  # only the top digit differs
+
+
+@pytest.mark.parametrize("kind", ["random", "ties", "equal", "sorted_desc", "top_digit"])
+@pytest.mark.parametrize("n", [65536, 1, 17, 1000, 65537, (1 << 20) + 3])
+def test_sort_train_permutation_bitwise(nrc, orc, dev, kind, n):
+    """VERDICT r04 item 7: the reference's shuffle contract (NRCUtil.cu:19-35), cub::DeviceRadixSort::SortPairs of
+    caller-supplied u32 keys with the indices -- bit-exact against the oracle's stable LSD restatement and numpy's
+    stable argsort; ties keep index order (all-equal keys give the identity)."""
+    import torch
+    keys = _keys(kind, n)
+    kd = _t(keys.view(np.int32), dev)
+    perm = torch.full((n + 64,), -5, dtype=torch.int32, device=dev)
+    sk = torch.zeros(n, dtype=torch.int32, device=dev)
+    nrc.frame.sort_train_permutation(kd, perm, n, sorted_keys=sk)
+    torch.cuda.synchronize()
+    got = perm.cpu().numpy()
+    assert (got[n:] == -5).all(), "wrote past n"
+    want, want_keys = orc.sort_pairs(keys)
+    np.testing.assert_array_equal(got[:n], want)
+    np.testing.assert_array_equal(got[:n], np.argsort(keys, kind="stable"))
+    np.testing.assert_array_equal(sk.cpu().numpy().view(np.uint32), want_keys)
+    np.testing.assert_array_equal(kd.cpu().numpy().view(np.uint32), keys)  # input untouched
+    if kind == "equal":
+        np.testing.assert_array_equal(got[:n], np.arange(n))
+
+
+def test_sort_train_permutation_errors(nrc, dev):
+    import torch
+    keys = torch.zeros(100, dtype=torch.int32, device=dev)
+    perm = torch.zeros(100, dtype=torch.int32, device=dev)
+    small = torch.zeros(8, dtype=torch.uint8, device=dev)
+    with pytest.raises(nrc.NrcError):
+        nrc.frame.sort_train_permutation(keys, perm, 100, temp=small)
+    with pytest.raises(nrc.NrcError):
+        nrc.frame.sort_train_permutation(keys, perm, (1 << 24) + 1)
+    nrc.frame.sort_train_permutation(keys, perm, 0)  # no-op
+    assert nrc.frame.sort_train_permutation_temp_bytes(65536) >= 3 * 65536 * 4
+
+
+def test_process_frame_with_shuffle_keys(nrc, orc, dev):
+    """The frame driver with the renderer's keys (nrc_frame_buffers.shuffle_keys_d): the shuffled training buffers are
+    bitwise those made with the oracle's key-sort permutation passed explicitly, and the whole frame (losses, weights)
+    is bitwise the explicit-permutation frame."""
+    import torch
+    F = nrc.frame
+    f = nrc.synthetic.cornell_frame(128, 64, (4, 4), seed=8)
+    keys = _keys("random", 65536)
+    perm, _ = orc.sort_pairs(keys)
+    res = []
+    for use_keys in (True, False):
+        net = nrc.Network()
+        net.init(stream=torch.cuda.current_stream())
+        fb, tq0, tt0, rec = _device_frame(nrc, f, dev, with_perm=None if use_keys else perm)
+        if use_keys:
+            fb.shuffle_keys = _t(keys.view(np.int32), dev)
+        loss = F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records))
+        torch.cuda.synchronize()
+        res.append((loss, fb.train_queries[1].cpu().numpy(), fb.train_targets[1].cpu().numpy(),
+                    net.get_state(nrc.StateSlot.PARAMS)))
+        net.destroy()
+    nrec = min(f.num_training_records, 65536)
+    np.testing.assert_array_equal(res[0][1], tq0[perm % nrec])
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("num_records", [65536, 40000, 1, 70000, 0, -3])
 @pytest.mark.parametrize("explicit", [False, True])
 def test_permute_bitwise(nrc, orc, dev, num_records, explicit):
