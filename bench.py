@@ -187,10 +187,45 @@ def hash_bench(nrc, dev, iters: int) -> dict:
         net.train(tq[(f % 4) * B:], tt[(f % 4) * B:])
     infer_ms = timed(lambda i: net.infer(q, out, n), iters)
     train_ms = timed(lambda i: net.train(tq[(i % 4) * B:], tt[(i % 4) * B:]), 4 * iters)
+    # tiny-cuda-nn's f16-accumulate numerics for the same queries (NRC_PRECISION_F16_ACC16, round 5): its price per launch
+    out_t = torch.empty_like(out)
+    tcnn_ms = timed(lambda i: net.infer_precision(nrc.PRECISION_F16_ACC16, q, out_t, n), iters)
+    torch.cuda.synchronize()
+    d = float(torch.linalg.vector_norm(out_t - out) / torch.linalg.vector_norm(out))
     net.destroy()
     return {"workload": "SURVEY 8(f) row 3: InputEncoding::Hash, 2^21-query inference + 16384-sample train step",
             "M_queries_per_s": n / (infer_ms * 1e-3) / 1e6, "infer_kernel_ms": infer_ms, "train_step_ms": train_ms,
+            "infer_f16_acc16_ms": tcnn_ms, "f16_acc16_vs_default_rel_l2": d,
             "bound": "feature pass (one level table per CU in LDS: random LDS gathers + VALU) + MLP pass, DESIGN.md section 10"}
+
+
+def tcnn_numerics_bench(nrc, net, q, out, n: int, iters: int) -> dict:
+    """The price of north_star's 1e-3-vs-tiny-cuda-nn tolerance on random weights: the 2^21-query launch with tcnn's
+    f16-accumulate numerics (NRC_PRECISION_F16_ACC16: an f16 accumulator rounded after every 16-wide K chunk) next to the
+    default f32-accumulate kernel, same weights and queries, HIP events on the network's stream."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    out_t = torch.empty_like(out)
+
+    def timed(fn, k: int) -> float:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(k):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / k
+
+    default_ms = timed(lambda: net.infer(q, out, n), iters)
+    tcnn_ms = timed(lambda: net.infer_precision(nrc.PRECISION_F16_ACC16, q, out_t, n), iters)
+    d = float(torch.linalg.vector_norm(out_t - out) / torch.linalg.vector_norm(out))
+    return {"workload": "Frequency 64x5, 2^21 queries, bench weights", "default_ms": default_ms,
+            "f16_acc16_ms": tcnn_ms, "slowdown": tcnn_ms / default_ms, "f16_acc16_vs_default_rel_l2": d,
+            "iters": iters}
 
 
 def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
@@ -673,6 +708,7 @@ def main() -> None:
 
     wide = None if args.no_wide else wide_bench(nrc, dev, world, rank, max(10, args.steps // 4), barrier)
     hashgrid = hash_bench(nrc, dev, max(10, args.steps // 10)) if world == 1 and not args.no_hash else None
+    tcnn_numerics = tcnn_numerics_bench(nrc, net, q, out, nq, max(10, args.steps // 10)) if world == 1 else None
 
     achieved = FLOP_PER_QUERY * nq / (kernel_ms * 1e-3) / 1e12
     if c4:
@@ -711,6 +747,7 @@ def main() -> None:
         "frame": frame,
         "wide_c5": wide,
         "hash": hashgrid,
+        "tcnn_numerics": tcnn_numerics,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_F16_TFLOPS, "traffic": pmc_traffic(),
                      "frac_burst": achieved / PEAK_F16_TFLOPS,

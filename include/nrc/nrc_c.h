@@ -50,7 +50,7 @@ typedef struct nrc_config {
     /* Extensions (BASELINE.json configs[4]; not in the reference, whose FullyFusedMLP has 64 neurons): */
     uint32_t width;           /* MLP neurons: 64 (reference) or 128 (NRC_WIDE_*; Frequency / FrequencySH only) */
     uint32_t infer_precision; /* nrc_precision of infer(): F16 (default), F16_ACC16 (tcnn's f16 accumulation, width 64
-                               * Frequency only) or FP8 (width 128 only) */
+                               * Frequency or Hash) or FP8 (width 128 only) */
     /* RadianceQuery layout of every query buffer of the handle (the reference's compile-time
      * USE_COMPACT_RADIANCE_QUERY, config.h:113): NRC_QUERY_COMPACT (default, 15 f32) or NRC_QUERY_PADDED (16 f32 with
      * pad_ and its Identity(1) feature, layout.h). Padded: width 64, Frequency or Hash, infer_precision F16; the

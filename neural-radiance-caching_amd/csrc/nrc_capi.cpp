@@ -683,6 +683,14 @@ hipError_t infer_any(nrc_net* net, const float* in, float* out, uint32_t n) {
         uint32_t* const feat = net->hash_feat_arg();
         if (feat) net->hash_feat_acquire(net->stream);
         if (net->padq() && !feat) throw ApiError(NRC_ERR_UNSUPPORTED, "padded queries: the feature-pass Hash inference only");
+        if (net->cfg.infer_precision == NRC_PRECISION_F16_ACC16) {
+            if (!net->hash_feat) throw ApiError(NRC_ERR_INTERNAL, "Hash feature workspace missing");
+            net->hash_feat_acquire(net->stream);
+            const hipError_t e = launch_infer_hash_tcnn(in, out, n, net->wf_infer, net->infer, net->table_infer,
+                                                        net->hash_feat, net->stream);
+            if (e == hipSuccess) net->hash_feat_release(net->stream);
+            return e;
+        }
         const hipError_t e = launch_infer_hash(in, out, n, net->wf_infer, net->table_infer, nullptr, nullptr, 0, -1, 1.0f,
                                                net->stream, feat, net->padq());
         if (e == hipSuccess && feat) net->hash_feat_release(net->stream);
@@ -896,8 +904,10 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         if (c.infer_precision != NRC_PRECISION_F16 && c.infer_precision != NRC_PRECISION_FP8 &&
             c.infer_precision != NRC_PRECISION_F16_ACC16)
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown infer_precision");
-        if (c.infer_precision == NRC_PRECISION_F16_ACC16 && (c.width != NRC_WIDTH || encoding != NRC_ENCODING_FREQUENCY))
-            throw ApiError(NRC_ERR_UNSUPPORTED, "F16_ACC16 (tcnn numerics) is implemented for the width-64 Frequency network");
+        if (c.infer_precision == NRC_PRECISION_F16_ACC16 &&
+            (c.width != NRC_WIDTH || encoding == NRC_ENCODING_FREQUENCY_SH))
+            throw ApiError(NRC_ERR_UNSUPPORTED,
+                           "F16_ACC16 (tcnn numerics) is implemented for the width-64 Frequency and Hash networks");
         if (c.infer_precision == NRC_PRECISION_FP8 && c.width != NRC_WIDE_WIDTH)
             throw ApiError(NRC_ERR_UNSUPPORTED, "FP8 inference is implemented for the width-128 network only");
         if (c.width == NRC_WIDE_WIDTH && encoding == NRC_ENCODING_HASH)
@@ -1784,12 +1794,19 @@ nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* i
                                      hipStream_t stream) {
     return guarded([&] {
         check_live(net);
-        if (!net->wide() && precision == NRC_PRECISION_F16_ACC16) {  // tcnn numerics on a width-64 Frequency network
-            if (net->encoding != NRC_ENCODING_FREQUENCY)
-                throw ApiError(NRC_ERR_UNSUPPORTED, "F16_ACC16 is implemented for the Frequency encoding");
+        if (!net->wide() && precision == NRC_PRECISION_F16_ACC16) {  // tcnn numerics on a width-64 network
+            if (net->encoding == NRC_ENCODING_FREQUENCY_SH || net->padq())
+                throw ApiError(NRC_ERR_UNSUPPORTED, "F16_ACC16 is implemented for the compact Frequency / Hash encodings");
             if (n == 0) return;
             if (!in || !out) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "null input/output pointer");
-            HIP_CHECK(launch_infer_tcnn(in, out, n, net->wf_infer, net->infer, stream));
+            if (net->hash()) {
+                net->hash_feat_acquire(stream);
+                HIP_CHECK(launch_infer_hash_tcnn(in, out, n, net->wf_infer, net->infer, net->table_infer, net->hash_feat,
+                                                 stream));
+                net->hash_feat_release(stream);
+            } else {
+                HIP_CHECK(launch_infer_tcnn(in, out, n, net->wf_infer, net->infer, stream));
+            }
             return;
         }
         if (!net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "precision selection is for the width-128 network");

@@ -241,6 +241,10 @@ hipError_t launch_encode_sh(const float* queries, float* enc, int64_t n, hipStre
 // w0 = the f32 inference weights (canonical blob; layer 0 is rebuilt from it in canonical K order)
 hipError_t launch_infer_tcnn(const float* queries, float* out, int64_t n, const _Float16* wf, const float* w0,
                              hipStream_t s);
+// the same numerics for InputEncoding::Hash (round 5): feature pass into feat, then the f16-accumulate MLP pass;
+// w0 = the f32 inference MLP blob (Hash W0 [64][64] first)
+hipError_t launch_infer_hash_tcnn(const float* queries, float* out, int64_t n, const _Float16* wf, const float* w0,
+                                  const _Float16* grid, uint32_t* feat, hipStream_t s);
 hipError_t launch_encode(const float* queries, float* enc, int64_t n, hipStream_t s);
 hipError_t launch_encode_fast(const float* queries, float* enc, int64_t n, hipStream_t s, int variant = 0);
 // fwd+loss+bwd+per-block dW partials. n_total = 3 * global batch.

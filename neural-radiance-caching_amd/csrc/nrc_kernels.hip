@@ -3260,6 +3260,34 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, pools, parity);
 }
 
+// One feature pass of hash_feature_kernel over cnt <= kHashFeatStride queries (the launch shape of launch_infer_hash).
+static void launch_hash_feature_pass(const float* qc0, int64_t cnt, const uint32_t* g, uint32_t* feat, bool padq,
+                                     hipStream_t s) {
+    // query ranges per level (multiple of the 8 XCDs); knob hash_feat_p overrides (A/B). Round 4: 32 above 2^19
+    // queries (4 blocks per CU, two ranges' positions per XCD L2 at a time): 179.7 vs 185.3 us (P = 16) per 2^21
+    // queries in-process, 24 / 48 / 64 / 128 slower (profiles/r04_hash/ab_hash_feat_p*.json)
+    const int kp = knob(kKnobHashFeatP);
+    const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 32 : 8;
+#if NRC_DEBUG_KERNELS
+    const int fa = knob(kKnobHashFeatAbl);
+    if (fa > 0) {
+        auto k = fa == 1   ? hash_feature_kernel<1>
+                 : fa == 2 ? hash_feature_kernel<2>
+                 : fa == 4 ? hash_feature_kernel<4>
+                 : fa == 8 ? hash_feature_kernel<8>  // round-3 arithmetic (A/B of the packed form)
+                 : fa == 16 ? hash_feature_kernel<16>  // round-3 loop (A/B of the pipelined steps)
+                 : fa == 32 ? hash_feature_kernel<32>  // no position loads, scattered positions
+                 : fa == 33 ? hash_feature_kernel<33>  // 32 without the gathers
+                 : fa == 36 ? hash_feature_kernel<36>  // 32 without the stores
+                           : hash_feature_kernel<7>;
+        hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+        return;
+    }
+#endif
+    if (padq) hipLaunchKernelGGL(hash_feature_kernel<64>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+    else hipLaunchKernelGGL(hash_feature_kernel<0>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+}
+
 hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const _Float16* wf, const _Float16* grid,
                              const float* thr, float* rgba, int64_t n_acc, int mode, float w, hipStream_t s,
                              uint32_t* feat, bool padq) {
@@ -3273,29 +3301,7 @@ hipError_t launch_infer_hash(const float* queries, float* out, int64_t n, const 
         static int bpf[3] = {};
         for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
             const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
-            // query ranges per level (multiple of the 8 XCDs); knob hash_feat_p overrides (A/B). Round 4: 32 above 2^19
-            // queries (4 blocks per CU, two ranges' positions per XCD L2 at a time): 179.7 vs 185.3 us (P = 16) per 2^21
-            // queries in-process, 24 / 48 / 64 / 128 slower (profiles/r04_hash/ab_hash_feat_p*.json)
-            const int kp = knob(kKnobHashFeatP);
-            const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 32 : 8;
-            const float* qc0 = queries + c0 * qd;
-#if NRC_DEBUG_KERNELS
-            const int fa = knob(kKnobHashFeatAbl);
-            if (fa > 0) {
-                auto k = fa == 1   ? hash_feature_kernel<1>
-                         : fa == 2 ? hash_feature_kernel<2>
-                         : fa == 4 ? hash_feature_kernel<4>
-                         : fa == 8 ? hash_feature_kernel<8>  // round-3 arithmetic (A/B of the packed form)
-                         : fa == 16 ? hash_feature_kernel<16>  // round-3 loop (A/B of the pipelined steps)
-                         : fa == 32 ? hash_feature_kernel<32>  // no position loads, scattered positions
-                         : fa == 33 ? hash_feature_kernel<33>  // 32 without the gathers
-                         : fa == 36 ? hash_feature_kernel<36>  // 32 without the stores
-                                   : hash_feature_kernel<7>;
-                hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
-            } else
-#endif
-                if (padq) hipLaunchKernelGGL(hash_feature_kernel<64>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
-                else hipLaunchKernelGGL(hash_feature_kernel<0>, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
+            launch_hash_feature_pass(queries + c0 * qd, cnt, g, feat, padq, s);
             const int64_t acc = std::min<int64_t>(std::max<int64_t>(n_acc - c0, 0), cnt);
             const InferEpilogue e{thr ? thr + c0 * 3 : nullptr, rgba ? reinterpret_cast<float4*>(rgba) + c0 : nullptr, acc, w};
             const float* qc = queries + c0 * qd;
@@ -3367,18 +3373,26 @@ __device__ __forceinline__ void round_f16_inplace(f16v& c, int count) {
     }
 }
 
+// ENC 0: Frequency (K = 80, 5 chunks, pad features 66..79); ENC 3: Hash (round 5) from hash_feature_kernel's level features
+// (K = 64, 4 chunks: grid 0..31, OneBlob 32..55, Identity 56..61, pad 62, 63; feat = the pass's workspace), the same MLP
+// chunking -- tcnn runs the same FullyFusedMLP behind either encoding (NRCNetworkConfigs.h:84-128).
+template <int ENC>
 __global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restrict__ q, float* __restrict__ out,
                                                             int64_t n, const h8* __restrict__ wf,
-                                                            const float* __restrict__ w0) {
+                                                            const float* __restrict__ w0,
+                                                            const uint32_t* __restrict__ feat) {
+    static_assert(ENC == 0 || ENC == 3, "Frequency or Hash-from-features");
     constexpr int W = 8;  // waves per block
+    constexpr int KK0 = ENC == 3 ? 4 : 5, IN = ENC == 3 ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH;
+    constexpr int PAD0 = ENC == 3 ? 62 : 66;  // first constant-one feature
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
     __shared__ __attribute__((aligned(16))) _Float16 enc[W][32 * kTcnnRowHalves];
     copy_to_lds<512, kFwdFrags * 64>(lw, wf);
     __syncthreads();
     // layer-0 fragments in canonical K order: fragment (mb, kk), lane L, element j = W0[32 mb + L % 32][16 kk + 8 (L / 32) + j]
-    for (int i = threadIdx.x; i < 10 * 64; i += 512) {
-        const int frag = i >> 6, L = i & 63, mb = frag / 5, kk = frag % 5;
-        const float* src = w0 + (32 * mb + (L & 31)) * NRC_ENC_WIDTH + 16 * kk + 8 * (L >> 5);
+    for (int i = threadIdx.x; i < 2 * KK0 * 64; i += 512) {
+        const int frag = i >> 6, L = i & 63, mb = frag / KK0, kk = frag % KK0;
+        const float* src = w0 + (32 * mb + (L & 31)) * IN + 16 * kk + 8 * (L >> 5);
         h8 v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)src[j];
@@ -3386,55 +3400,79 @@ __global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restr
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
     _Float16* const row = &enc[wave][r * kTcnnRowHalves];
-    // pad features 66..79 = 1.0 (never rewritten)
+    // pad features (never rewritten)
     if (h == 0)
 #pragma unroll
-        for (int f = 66; f < 80; ++f) row[f] = (_Float16)1.0f;
+        for (int f = PAD0; f < IN; ++f) row[f] = (_Float16)1.0f;
     __syncthreads();
     char* const rowb = reinterpret_cast<char*>(row);
     const int64_t ntiles = (n + 31) / 32;
     for (int64_t g = (int64_t)blockIdx.x * W + wave; g < ntiles; g += (int64_t)gridDim.x * W) {
         const int64_t s = g * 32 + r;
-        const QLane Q = load_q(q, s < n ? s : n - 1, h);
-        h8 x[5];
-        encode_v3(Q, h, x);
-        // slots -> canonical features (slot_feature): TriangleWave slots 6d.. -> 12 d + 6 h.., OneBlob slots 18.. ->
-        // 36 + 12 h.., Identity slots 30..32 -> 60 + 3 h..
+        const int64_t sc = s < n ? s : n - 1;
+        const QLane Q = load_q(q, sc, h);
         uint32_t w[20];
+        if constexpr (ENC == 3) {
+            // encode_hashf's slots: levels 8h.. (features 16h.., one half2 per level), OneBlob dims 3h.. (features
+            // 32 + 12h..), Identity dims 3h.. (features 56 + 3h..)
 #pragma unroll
-        for (int kk = 0; kk < 5; ++kk) {
-            const u4 t = __builtin_bit_cast(u4, x[kk]);
-            w[4 * kk] = t.x;
-            w[4 * kk + 1] = t.y;
-            w[4 * kk + 2] = t.z;
-            w[4 * kk + 3] = t.w;
+            for (int i = 0; i < 8; ++i) w[i] = feat[(int64_t)(8 * h + i) * kHashFeatStride + sc];
+            blob_v3(Q.b0, w[8], w[9]);
+            blob_v3(Q.b1, w[10], w[11]);
+            blob_v3(Q.b2, w[12], w[13]);
+            w[14] = pk2(Q.i0, Q.i1);
+            w[15] = pk2(Q.i2, 1.0f);
+        } else {
+            h8 x[5];
+            encode_v3(Q, h, x);
+#pragma unroll
+            for (int kk = 0; kk < 5; ++kk) {
+                const u4 t = __builtin_bit_cast(u4, x[kk]);
+                w[4 * kk] = t.x;
+                w[4 * kk + 1] = t.y;
+                w[4 * kk + 2] = t.z;
+                w[4 * kk + 3] = t.w;
+            }
         }
         asm volatile("" ::: "memory");  // the previous tile's chunk reads of this row stay above these writes
+        if constexpr (ENC == 3) {
 #pragma unroll
-        for (int d = 0; d < 3; ++d)
+            for (int i = 0; i < 8; ++i) *(uint32_t*)(rowb + 2 * (16 * h) + 4 * i) = w[i];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) *(uint32_t*)(rowb + 2 * (12 * d + 6 * h) + 4 * i) = w[3 * d + i];
+            for (int i = 0; i < 6; ++i) *(uint32_t*)(rowb + 2 * (32 + 12 * h) + 4 * i) = w[8 + i];
+            const h2 id01 = __builtin_bit_cast(h2, w[14]), id2 = __builtin_bit_cast(h2, w[15]);
+            row[56 + 3 * h] = id01[0];
+            row[57 + 3 * h] = id01[1];
+            row[58 + 3 * h] = id2[0];
+        } else {
+            // slots -> canonical features (slot_feature): TriangleWave slots 6d.. -> 12 d + 6 h.., OneBlob slots 18.. ->
+            // 36 + 12 h.., Identity slots 30..32 -> 60 + 3 h..
 #pragma unroll
-        for (int i = 0; i < 6; ++i) *(uint32_t*)(rowb + 2 * (36 + 12 * h) + 4 * i) = w[9 + i];
-        const h2 id01 = __builtin_bit_cast(h2, w[15]), id2 = __builtin_bit_cast(h2, w[16]);
-        row[60 + 3 * h] = id01[0];
-        row[61 + 3 * h] = id01[1];
-        row[62 + 3 * h] = id2[0];
+            for (int d = 0; d < 3; ++d)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) *(uint32_t*)(rowb + 2 * (12 * d + 6 * h) + 4 * i) = w[3 * d + i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) *(uint32_t*)(rowb + 2 * (36 + 12 * h) + 4 * i) = w[9 + i];
+            const h2 id01 = __builtin_bit_cast(h2, w[15]), id2 = __builtin_bit_cast(h2, w[16]);
+            row[60 + 3 * h] = id01[0];
+            row[61 + 3 * h] = id01[1];
+            row[62 + 3 * h] = id2[0];
+        }
         // the wave's writes of every row land before its lanes read other lanes' rows (LDS is in order per wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        h8 in0[5];
+        h8 in0[KK0];
 #pragma unroll
-        for (int kk = 0; kk < 5; ++kk) in0[kk] = *(const h8*)(rowb + 32 * kk + 16 * h);
+        for (int kk = 0; kk < KK0; ++kk) in0[kk] = *(const h8*)(rowb + 32 * kk + 16 * h);
         asm volatile("" ::: "memory");
         lds_h8* const wl = (lds_h8*)(lw + lane);
-        // layer 0 (K = 80, 5 chunks) and the hidden layers (K = 64, 4 chunks)
+        // layer 0 (K = 80 / 64: 5 / 4 chunks) and the hidden layers (K = 64, 4 chunks)
         h8 y[4];
         {
             f16v c[2];
 #pragma unroll
-            for (int kk = 0; kk < 5; ++kk)
+            for (int kk = 0; kk < KK0; ++kk)
 #pragma unroll
                 for (int m = 0; m < 2; ++m) {
                     c[m] = mfma(wl[fwd_frag(0, m, kk) * 64], in0[kk], kk ? c[m] : zero16());
@@ -3485,7 +3523,26 @@ hipError_t launch_infer_tcnn(const float* queries, float* out, int64_t n, const 
     if (n <= 0) return hipSuccess;
     if (!wf || !w0) return hipErrorInvalidValue;
     static int bpc = 0;
-    return launch_persistent_infer(infer_tcnn_kernel, 512, bpc, (n + 31) / 32, queries, out, n, wf, s, w0);
+    return launch_persistent_infer(infer_tcnn_kernel<0>, 512, bpc, (n + 31) / 32, queries, out, n, wf, s, w0,
+                                   (const uint32_t*)nullptr);
+}
+
+// tcnn-numerics Hash inference (NRC_PRECISION_F16_ACC16, round 5): the feature pass, then infer_tcnn_kernel<3> per pass
+hipError_t launch_infer_hash_tcnn(const float* queries, float* out, int64_t n, const _Float16* wf, const float* w0,
+                                  const _Float16* grid, uint32_t* feat, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (!wf || !w0 || !grid || !feat) return hipErrorInvalidValue;
+    static int bpc = 0;
+    for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
+        const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
+        const float* qc = queries + c0 * NRC_INPUT_DIMS;
+        launch_hash_feature_pass(qc, cnt, reinterpret_cast<const uint32_t*>(grid), feat, false, s);
+        const hipError_t e = launch_persistent_infer(infer_tcnn_kernel<3>, 512, bpc, (cnt + 31) / 32, qc,
+                                                     out + c0 * NRC_OUTPUT_DIMS, cnt, wf, s, w0,
+                                                     (const uint32_t*)feat);
+        if (e != hipSuccess) return e;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_wide_pack(const float* w_infer, const float* w_train, const WideImages& im, hipStream_t s) {

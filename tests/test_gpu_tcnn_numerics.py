@@ -95,12 +95,17 @@ def test_debug_precision_entry_matches_config(nrc, torch, dev, tnet, golden):
 
 
 def test_unsupported_combinations(nrc, torch, dev, tnet):
-    for enc in (nrc.InputEncoding.Hash, nrc.InputEncoding.FrequencySH):
+    for enc in (nrc.InputEncoding.FrequencySH,):
         cfg = nrc.default_config(enc, infer_precision=nrc.PRECISION_F16_ACC16)
         n = nrc.Network()
         with pytest.raises(nrc.NrcError) as e:
             n.init(stream=torch.cuda.current_stream(), encoding=enc, config=cfg)
         assert e.value.status == 5
+    cfg = nrc.default_config(nrc.InputEncoding.Hash, infer_precision=nrc.PRECISION_F16_ACC16)
+    cfg.query_layout = nrc.QUERY_PADDED
+    with pytest.raises(nrc.NrcError) as e:
+        nrc.Network().init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash, config=cfg)
+    assert e.value.status == 5
     cfg = nrc.default_config(nrc.InputEncoding.Frequency, width=128, infer_precision=nrc.PRECISION_F16_ACC16)
     with pytest.raises(nrc.NrcError):
         nrc.Network().init(stream=torch.cuda.current_stream(), config=cfg)
@@ -157,3 +162,81 @@ def test_process_frame_on_a_tcnn_numerics_handle(nrc, torch, dev, tnet):
     torch.cuda.synchronize()
     assert torch.equal(fb.output_rgba, rgba)
     assert torch.equal(fb.results_inference[S:], rad[S:])
+
+
+# ---- InputEncoding::Hash (round 5): the same f16-accumulate MLP behind the HashGrid encoding ----
+@pytest.fixture()
+def hnet(nrc, torch, dev):
+    cfg = nrc.default_config(nrc.InputEncoding.Hash, infer_precision=nrc.PRECISION_F16_ACC16)
+    n = nrc.Network()
+    n.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash, config=cfg)
+    yield n
+    n.destroy()
+
+
+def _hash_params_random(nrc, orc):
+    """The Hash model's random init with the grid table drawn wide (tcnn initialises it to +-1e-4, which makes every grid
+    feature ~0 and the check blind to the grid): the MLP at init, the table uniform in [-1, 1]."""
+    p = orc.hash_init_params(7).copy()
+    rng = np.random.default_rng(5)
+    p[nrc.HASH_MLP_PARAMS:] = rng.uniform(-1.0, 1.0, p.size - nrc.HASH_MLP_PARAMS).astype(np.float32)
+    return p
+
+
+@pytest.mark.parametrize("n", [1, 33, 4096, 70001])
+def test_hash_random_weights_within_1e3_of_tcnn_emulation(nrc, orc, torch, dev, hnet, n):
+    """Hash F16_ACC16 against the Hash oracle's ORC_TCNN mode (the same feature pass, the MLP with f16 accumulation per
+    16-wide K chunk in canonical K order): north_star's 1e-3 relative L2 on random weights, and the per-query bound; the
+    default (f32-accumulate) Hash kernel's distance to ORC_TCNN is printed beside it."""
+    params = _hash_params_random(nrc, orc)
+    hnet.set_state(nrc.StateSlot.INFER, params)
+    q_np = nrc.synthetic.cornell_queries(n, seed=1200 + n)
+    y = infer(torch, dev, hnet, q_np)
+    y_tcnn = orc.hash_forward(params, q_np, orc.TCNN)
+    r = rel(y, y_tcnn)
+    d = nrc.Network()
+    d.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+    d.set_state(nrc.StateSlot.INFER, params)
+    y_def = infer(torch, dev, d, q_np)
+    d.destroy()
+    print(f"Hash n={n}: F16_ACC16 rel-L2 vs ORC_TCNN {r:.2e}; default kernel vs ORC_TCNN {rel(y_def, y_tcnn):.2e}")
+    assert r <= 1e-3
+    assert per_query_ok(y, y_tcnn) <= 0.001 * n + 1
+
+
+def test_hash_trained_weights_two_passes(nrc, orc, torch, dev, hnet):
+    """Self-trained Hash weights (8 steps of 16,384 samples), then 2^21 + 77 queries -- two feature passes -- through the
+    F16_ACC16 kernel; a sample of rows across both passes within 1e-3 of ORC_TCNN."""
+    for f in range(2):
+        q, t = nrc.synthetic.cornell_batch(nrc.BATCH_SIZE * 4, seed=4200 + f)
+        q, t = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
+        for b in range(4):
+            hnet.train(q[b * nrc.BATCH_SIZE:], t[b * nrc.BATCH_SIZE:])
+    params = hnet.get_state(nrc.StateSlot.INFER)
+    N = (1 << 21) + 77
+    q_np = nrc.synthetic.cornell_queries(N, seed=4300)
+    y = infer(torch, dev, hnet, q_np)
+    idx = np.concatenate([np.arange(0, N, 1021), np.arange(N - 77, N)])
+    y_ref = orc.hash_forward(params, q_np[idx], orc.TCNN)
+    r = rel(y[idx], y_ref)
+    print(f"Hash trained weights, {N} queries, {idx.size} rows: rel-L2 vs ORC_TCNN {r:.2e}")
+    assert r <= 1e-3
+    assert np.isfinite(y).all()
+
+
+def test_hash_debug_precision_entry_matches_config(nrc, orc, torch, dev, hnet):
+    d = nrc.Network()
+    d.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+    try:
+        params = _hash_params_random(nrc, orc)
+        for net in (hnet, d):
+            net.set_state(nrc.StateSlot.INFER, params)
+        q = torch.from_numpy(nrc.synthetic.cornell_queries(3000, seed=6)).to(dev)
+        a, b, c = (torch.zeros((3000, 3), device=dev) for _ in range(3))
+        hnet.infer(q, a, 3000)
+        d.infer_precision(nrc.PRECISION_F16_ACC16, q, b, 3000)
+        d.infer(q, c, 3000)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b) and not torch.equal(a, c)
+    finally:
+        d.destroy()
