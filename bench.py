@@ -190,6 +190,7 @@ def hash_bench(nrc, dev, iters: int) -> dict:
     # tiny-cuda-nn's f16-accumulate numerics for the same queries (NRC_PRECISION_F16_ACC16, round 5): its price per launch
     out_t = torch.empty_like(out)
     tcnn_ms = timed(lambda i: net.infer_precision(nrc.PRECISION_F16_ACC16, q, out_t, n), iters)
+    net.infer(q, out, n)  # the default kernel's output with the same (trained-since) weights
     torch.cuda.synchronize()
     d = float(torch.linalg.vector_norm(out_t - out) / torch.linalg.vector_norm(out))
     net.destroy()
