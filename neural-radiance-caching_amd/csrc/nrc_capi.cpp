@@ -175,9 +175,23 @@ void build_scatter_maps(std::vector<int>& fwd, std::vector<int>& bwd, int encodi
 
 // The same two maps for the t16 training layout (Frequency, nrc_train16.hip): position in the 16x16x32 forward
 // training image (fwdt) and in its backward image (bwd). The inference image keeps build_scatter_maps' fwd.
-void build_t16_maps(std::vector<int>& fwdt, std::vector<int>& bwd) {
-    fwdt.assign(NRC_NUM_PARAMS, -1);
-    bwd.assign(NRC_NUM_PARAMS, -1);
+// Hash (round 5): its layer offsets and slot map (t16_hash_slot_feature), and W0^T of the 32 grid features in the
+// backward image's fragments 36..39 (kT16BwdFragsHash).
+int t16_layer_off(int encoding, int l) {
+    if (encoding != NRC_ENCODING_HASH) return kLayerOff[l];
+    return l == 0 ? NRC_HASH_W0_OFFSET : l <= 4 ? NRC_HASH_W1_OFFSET + (l - 1) * 4096 : NRC_HASH_W5_OFFSET;
+}
+int t16_feature(int encoding, int K) {
+    return encoding == NRC_ENCODING_HASH ? t16_hash_slot_feature(K) : t16_slot_feature(K);
+}
+
+void build_t16_maps(std::vector<int>& fwdt, std::vector<int>& bwd, int encoding) {
+    const bool hash = encoding == NRC_ENCODING_HASH;
+    const int n = hash ? NRC_HASH_MLP_PARAMS : NRC_NUM_PARAMS, in0 = hash ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH;
+    int off[NRC_NUM_LAYERS];
+    for (int l = 0; l < NRC_NUM_LAYERS; ++l) off[l] = t16_layer_off(encoding, l);
+    fwdt.assign(n, -1);
+    bwd.assign(n, -1);
     auto pos = [](int frag, int lane, int j) { return frag * kFragHalves + lane * 8 + j; };
     // row o of a 64-row operand <-> (k-step s, lane group g, element j) of t16_row
     auto sgj = [](int o, int& s, int& g, int& j) {
@@ -186,15 +200,22 @@ void build_t16_maps(std::vector<int>& fwdt, std::vector<int>& bwd) {
         j = 4 * ((o >> 4) & 1) + (o & 3);
     };
     for (int K = 0; K < 96; ++K) {
-        const int f = t16_slot_feature(K);
+        const int f = t16_feature(encoding, K);
         if (f < 0) continue;
-        for (int o = 0; o < 64; ++o)
-            fwdt[kLayerOff[0] + o * NRC_ENC_WIDTH + f] = pos(t16_fwd_frag(0, o >> 4, K >> 5), 16 * ((K >> 3) & 3) + (o & 15), K & 7);
+        for (int o = 0; o < 64; ++o) {
+            fwdt[off[0] + o * in0 + f] = pos(t16_fwd_frag(0, o >> 4, K >> 5), 16 * ((K >> 3) & 3) + (o & 15), K & 7);
+            if (hash && f < 2 * NRC_HASH_LEVELS) {
+                // W0^T: A[grid slot f (M-block f >> 4, row f & 15)][k = row o of delta_0 (k-step s, group g, element j)]
+                int s, g, j;
+                sgj(o, s, g, j);
+                bwd[off[0] + o * in0 + f] = pos(kT16BwdFrags + 2 * (f >> 4) + s, 16 * g + (f & 15), j);
+            }
+        }
     }
     for (int l = 1; l <= 4; ++l)
         for (int o = 0; o < 64; ++o)
             for (int i = 0; i < 64; ++i) {
-                const int p = kLayerOff[l] + o * 64 + i;
+                const int p = off[l] + o * 64 + i;
                 int s, g, j;
                 sgj(i, s, g, j);
                 fwdt[p] = pos(t16_fwd_frag(l, o >> 4, s), 16 * g + (o & 15), j);
@@ -203,7 +224,7 @@ void build_t16_maps(std::vector<int>& fwdt, std::vector<int>& bwd) {
             }
     for (int o = 0; o < NRC_OUT_PADDED; ++o)
         for (int i = 0; i < 64; ++i) {
-            const int p = kLayerOff[5] + o * 64 + i;
+            const int p = off[5] + o * 64 + i;
             int s, g, j;
             sgj(i, s, g, j);
             fwdt[p] = pos(t16_fwd_frag(5, 0, s), 16 * g + o, j);
@@ -214,18 +235,19 @@ void build_t16_maps(std::vector<int>& fwdt, std::vector<int>& bwd) {
 
 // Slab map of the t16 layout (t16_slab_pos): register i of lane l of tile (tm, tn) holds dW[16 tm + 4 (l >> 4) + i]
 // [16 tn + (l & 15)] (layer 0: column = K slot -> feature, -1 for the dummy slots).
-std::vector<int> build_t16_slab_map() {
+std::vector<int> build_t16_slab_map(int encoding) {
+    const bool hash = encoding == NRC_ENCODING_HASH;
     std::vector<int> m(slab_floats(0), -1);
     for (int L = 0; L < NRC_NUM_LAYERS; ++L) {
-        const int ntm = L == 5 ? 1 : 4, in_dim = L == 0 ? NRC_ENC_WIDTH : 64;
+        const int ntm = L == 5 ? 1 : 4, in_dim = L == 0 ? (hash ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH) : 64;
         for (int tm = 0; tm < ntm; ++tm)
             for (int tn = 0; tn < t16_ntn(L); ++tn)
                 for (int lane = 0; lane < 64; ++lane)
                     for (int i = 0; i < 4; ++i) {
                         const int row = 16 * tm + 4 * (lane >> 4) + i, col = 16 * tn + (lane & 15);
-                        const int f = L == 0 ? t16_slot_feature(col) : col;
+                        const int f = L == 0 ? t16_feature(encoding, col) : col;
                         if (f < 0) continue;
-                        m[t16_slab_pos(L, tm, tn, lane, i)] = kLayerOff[L] + row * in_dim + f;
+                        m[t16_slab_pos(L, tm, tn, lane, i)] = t16_layer_off(encoding, L) + row * in_dim + f;
                     }
     }
     return m;
@@ -233,7 +255,13 @@ std::vector<int> build_t16_slab_map() {
 
 // Training kernel of a 64-wide Frequency network: the t16-layout kernels (f16 slabs) unless the train_kernel knob
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
-bool want_t16(int encoding) { return encoding == NRC_ENCODING_FREQUENCY && knob(kKnobTrainKernel) != 32; }
+// Round 5: InputEncoding::Hash too (compact records; padded Hash handles keep the 32x32 kernel).
+// backward image allocation: the largest layout (32x32 Hash 38 fragments, t16 Frequency 36, t16 Hash 40)
+constexpr int kWbHalves = (kBwdFragsHash > kT16BwdFragsHash ? kBwdFragsHash : kT16BwdFragsHash) * kFragHalves;
+bool want_t16(int encoding, bool padq) {
+    if (knob(kKnobTrainKernel) == 32) return false;
+    return encoding == NRC_ENCODING_FREQUENCY || (encoding == NRC_ENCODING_HASH && !padq);
+}
 
 std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
@@ -495,6 +523,7 @@ struct nrc_net {
         b.n_total = (int)n_total();
         b.slab_param = slab_param;
         b.n_slab = n_slab;
+        b.slab_closed = t16 && !hash();
         return b;
     }
     GridBuffers grid_buffers() const {
@@ -602,6 +631,7 @@ int dc_shape(uint32_t b) {
 
 // training blocks = weight-gradient slabs of a b-sample step of this handle's training kernel
 int train_block_count(const nrc_net* net, uint32_t b) {
+    if (net->t16 && net->hash()) return (int)((b + 127u) / 128u);  // the role-split kernel, 128 samples per block
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0) {
         const int S = dc_samples_per_block(dc_shape(b));
         if (S <= 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "train_shape knob names no decoupled-chain shape");
@@ -656,7 +686,7 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     if (net->hash())
         HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                     net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                    net->step_scatter(blocks), net->padq()));
+                                    net->step_scatter(blocks), net->padq(), net->t16));
     else
         train_partials(net, in, tgt, b, 3.0f * (float)b);
     net->step += 1;
@@ -966,7 +996,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMalloc(&net->ema, pb));
         HIP_CHECK(hipMalloc(&net->infer, pb));
         HIP_CHECK(hipMalloc(&net->wf_train, sizeof(_Float16) * kFwdHalves));
-        HIP_CHECK(hipMalloc(&net->wb_train, sizeof(_Float16) * kBwdHalvesHash));
+        HIP_CHECK(hipMalloc(&net->wb_train, sizeof(_Float16) * kWbHalves));
         HIP_CHECK(hipMalloc(&net->wf_infer, sizeof(_Float16) * kFwdHalves));
         HIP_CHECK(hipMalloc(&net->fwd_pos, sizeof(int) * net->n_mlp));
         HIP_CHECK(hipMalloc(&net->bwd_pos, sizeof(int) * net->n_mlp));
@@ -994,11 +1024,11 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemset(net->v, 0, pb));
         HIP_CHECK(hipMemset(net->ema, 0, pb));
         HIP_CHECK(hipMemset(net->wf_train, 0, sizeof(_Float16) * kFwdHalves));
-        HIP_CHECK(hipMemset(net->wb_train, 0, sizeof(_Float16) * kBwdHalvesHash));
+        HIP_CHECK(hipMemset(net->wb_train, 0, sizeof(_Float16) * kWbHalves));
         HIP_CHECK(hipMemset(net->wf_infer, 0, sizeof(_Float16) * kFwdHalves));
         std::vector<int> fwd, bwd;
         build_scatter_maps(fwd, bwd, net->encoding);
-        net->t16 = want_t16(net->encoding);
+        net->t16 = want_t16(net->encoding, net->padq());
         {
             // the decoupled-chain kernel is the default; knob train_kernel = 1 / 2 selects round 2's role-split /
             // 4-wave t16 kernels (in-process A/B)
@@ -1007,7 +1037,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         }
         if (net->t16) {
             std::vector<int> fwdt;
-            build_t16_maps(fwdt, bwd);
+            build_t16_maps(fwdt, bwd, net->encoding);
             HIP_CHECK(hipMalloc(&net->fwdt_pos, sizeof(int) * net->n_mlp));
             HIP_CHECK(hipMemcpy(net->fwdt_pos, fwdt.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
 #if NRC_DEBUG_KERNELS
@@ -1021,8 +1051,8 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemcpy(net->fwd_pos, fwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         {
-            const std::vector<int> sm = net->t16 ? build_t16_slab_map() : build_slab_map(net->encoding);
-            if (net->t16)  // the reduction maps t16 slab positions in closed form (t16_slab_param): same map
+            const std::vector<int> sm = net->t16 ? build_t16_slab_map(net->encoding) : build_slab_map(net->encoding);
+            if (net->t16 && !net->hash())  // the reduction maps Frequency t16 slab positions in closed form (t16_slab_param)
                 for (size_t i = 0; i < sm.size(); ++i)
                     if (sm[i] != t16_slab_param((int)i))
                         throw ApiError(NRC_ERR_INTERNAL, "t16_slab_param disagrees with the slab map at " + std::to_string(i));
@@ -1392,7 +1422,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
             // (unless grid_fixed is the buffer itself)
             HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
                                         net->wb_train, net->table_train, net->grid_grad, net->slabs, net->loss_partials,
-                                        net->stream, net->step_scatter(blocks), net->padq()));
+                                        net->stream, net->step_scatter(blocks), net->padq(), net->t16));
             if (grid_fixed)
                 HIP_CHECK(launch_grid_grad_export_fixed(net->grid_grad, grid_fixed, net->n_grid, net->nonfinite(),
                                                         net->stream));

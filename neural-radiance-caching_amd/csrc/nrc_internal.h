@@ -55,6 +55,24 @@ __host__ __device__ constexpr int t16_slot_feature(int K) {
         return pid < 14 ? 66 + pid : -1;
     }((K % 32) / 8, 8 * (K / 32) + K % 8);
 }
+// InputEncoding::Hash in the t16 layout (round 5): the same 96 K slots with lane group g's 9 TriangleWave slots replaced
+// by its 4 grid levels 4g .. 4g + 3 (n 0..7: canonical feature 8g + n, so K = canonical feature for the 32 grid
+// features) and a pad slot (n 8); OneBlob / Identity slots as for Frequency (canonical 32.. / 56..); the two
+// constant-one features 62, 63 in group 0's slots n 8 and 11; every other slot a dummy with zero weights.
+__host__ __device__ constexpr int t16_hash_slot_feature(int K) {
+    return [](int g, int n) {
+        if (n <= 7) return 8 * g + n;
+        if (n == 8 || n == 11) return g == 0 ? (n == 8 ? 62 : 63) : -1;
+        if (n == 9 || n == 10) return g < 3 ? 56 + 2 * g + (n - 9) : -1;
+        if (n >= 12 && n <= 19) return g < 3 ? 32 + 4 * (2 * g + (n >= 16)) + (n & 3) : -1;
+        return -1;
+    }((K % 32) / 8, 8 * (K / 32) + K % 8);
+}
+static_assert(t16_hash_slot_feature(13) == 13 && t16_hash_slot_feature(32 + 1) == 56 && t16_hash_slot_feature(32 + 4) == 32,
+              "t16 Hash slot map");
+// Hash backward image in the t16 layout: the 36 fragments of W_l^T, then W0^T restricted to the 32 grid features as
+// 16x16x32 A operands: fragment 36 + 2 mb + s holds rows (grid slots) 16 mb .. 16 mb + 15, k-step s of delta_0's rows
+constexpr int kT16BwdFragsHash = kT16BwdFrags + 4;
 // Weight-gradient slab of one block in the t16 layout (f16 elements): per layer, 16x16 dW tiles (tm, tn) row-major
 // (L0 4 x 6 tiles, L1..L4 4 x 4, L5 1 x 4: 23,552 elements, as the 32x32 slab), stored as column pairs: tiles
 // (tm, 2p) and (tm, 2p + 1) are one 1-KiB record [lane 0..63][8], elements 0..3 = accumulator registers 0..3 of the
@@ -298,12 +316,26 @@ struct ModelBuffers {
     int n_total;  // all parameters (MLP + grid): index of the loss in a data-parallel gradient buffer
     const int* slab_param;  // [n_slab] parameter of each slab position, -1 = padding
     int n_slab;             // slab stride (floats per training block)
+    bool slab_closed;       // f16 slabs of the Frequency t16 layout: the reduction maps positions in closed form
+                            // (t16_slab_param) instead of loading slab_param
 };
 
 // slabs: f16 (nrc_train16.hip slab_pair), reduced by launch_reduce_adam (ModelBuffers::slab_f16)
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
                           hipStream_t s, bool split = false, int groups = 2, bool padq = false);
+// InputEncoding::Hash on the t16 role-split kernel (round 5): the encoder gathers levels 4g .. 4g + 3 from the f16
+// training table; the chain waves also write each sample's position and its 16 levels' (dy0, dy1) = W0^T delta_0 of the
+// grid features (f16 pairs, [level][sample], zeros past b) for grid_scatter_kernel. wb: kT16BwdFragsHash fragments.
+struct HashTrainOut {
+    const uint32_t* table;  // f16 training table as half2 entries
+    float4* pos;            // [bcap]
+    uint32_t* dy;           // [NRC_HASH_LEVELS][bcap]
+    int64_t bcap;
+};
+hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                               const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
+                               const HashTrainOut& ho, hipStream_t s);
 // samples per block of the role-split t16 kernel: 64 x groups (knob "t16_groups"; 128 by default)
 int t16_groups();  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16
@@ -392,7 +424,8 @@ hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, con
                                 int64_t* waves, hipStream_t s);
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
-                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false);
+                             float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false,
+                             bool t16 = false);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "nrc_device.h"
+#include "nrc_hash.h"
 
 namespace nrc_amd {
 namespace t16 {
@@ -59,6 +60,27 @@ __device__ __forceinline__ void encode16(float p0, float p1, float p2, float bA,
     w[3] = pk2_abs_v(t[6], t[7]);
     w[4] = pk2(__builtin_fabsf(t[8]), iA);
     w[5] = pk2(iB, g == 0 ? pad : 1.0f);
+    blob_v3(bA, w[6], w[7]);
+    blob_v3(bB, w[8], w[9]);
+    w[10] = w[11] = 0x3C003C00u;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) x[s] = __builtin_bit_cast(h8, u4{w[4 * s], w[4 * s + 1], w[4 * s + 2], w[4 * s + 3]});
+}
+
+// InputEncoding::Hash in the same 24 slots per lane group (t16_hash_slot_feature): the 4 grid levels 4g .. 4g + 3 of the
+// sample (hash_level_feature: tcnn's corners and f16 interpolation, gathers from the f16 training table), pad 1.0,
+// Identity, pad, OneBlob as encode16, pads. Levels 0 and 1 (group 0) are dense: the first two levels of every group
+// take the dense/hashed select.
+__device__ __forceinline__ void encode16_hash(float p0, float p1, float p2, float bA, float bB, float iA, float iB, int g,
+                                              const uint32_t* __restrict__ table, h8 (&x)[3]) {
+    uint32_t w[12];
+    const int l0 = 4 * g;
+    w[0] = hash_level_feature<true>(p0, p1, p2, l0, table);
+    w[1] = hash_level_feature<true>(p0, p1, p2, l0 + 1, table);
+    w[2] = hash_level_feature<false>(p0, p1, p2, l0 + 2, table);
+    w[3] = hash_level_feature<false>(p0, p1, p2, l0 + 3, table);
+    w[4] = pk2(1.0f, iA);
+    w[5] = pk2(iB, 1.0f);
     blob_v3(bA, w[6], w[7]);
     blob_v3(bB, w[8], w[9]);
     w[10] = w[11] = 0x3C003C00u;

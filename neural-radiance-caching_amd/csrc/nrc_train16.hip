@@ -16,6 +16,7 @@
 //   [sample][feature] images) and delta_{L-1} = (W_L^T delta_L) * [a_{L-1} > 0] (register chain, backward image in
 //   LDS), the next layer's images written to the other buffer, the dW tiles streamed to the block's slab.
 #include "nrc_t16.h"
+#include "nrc_hash.h"
 
 #include <type_traits>
 
@@ -490,12 +491,17 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // dependency latency; the step's critical path is the chain alone instead of chain + dW.
 // G: 16-sample groups per chain wave (64 G samples per block); PADQ: padded RadianceQuery records (16 floats: the
 // position load takes pad_ along, 16 bytes instead of 12, the other loads one float further)
-template <int AUX, int G = 2, bool PADQ = false>
+// ENC 1 (round 5): InputEncoding::Hash -- the encoder gathers each lane group's 4 grid levels (t16_hash_slot_feature),
+// and after the last chain step the chain waves form dL/d(grid features) = W0^T delta_0 (4 MFMAs per group from the
+// backward image's fragments 36..39, read from global memory) and write it with the sample positions for
+// grid_scatter_kernel (ho). Everything else -- forward, loss, delta chain, dW waves, slab layout -- is the Frequency
+// kernel's.
+template <int AUX, int G = 2, bool PADQ = false, int ENC = 0>
 __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                                int64_t b, float n_total, float loss_scale,
                                                                const h8* __restrict__ wf, const h8* __restrict__ wb,
                                                                _Float16* __restrict__ slabs,
-                                                               float* __restrict__ loss_partials) {
+                                                               float* __restrict__ loss_partials, HashTrainOut ho) {
     const int lane = threadIdx.x & 63;
     __shared__ __attribute__((aligned(16))) char smem[kLds];
     h8* lwb = (h8*)(smem + kOffWb);
@@ -623,9 +629,13 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         tg[u][0] = tq[u].x; tg[u][1] = tq[u].y; tg[u][2] = tq[u].z;
-        float pad = 1.0f;
-        if constexpr (PADQ) pad = pq[u].w;
-        encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
+        if constexpr (ENC == 1) {
+            encode16_hash(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, ho.table, x[u]);
+        } else {
+            float pad = 1.0f;
+            if constexpr (PADQ) pad = pq[u].w;
+            encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
+        }
         const u4 w = __builtin_bit_cast(u4, x[u][2]);
         *(u2*)(img_x2 + off32(r[u], 2 * g)) = u2{w.x, w.y};
         *(u2*)(img_x2 + off32(r[u], 2 * g + 1)) = u2{w.z, w.w};
@@ -789,11 +799,37 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         }                                                                                                          \
     }                                                                                                              \
     lds_barrier();
+    // Hash: W0^T of the grid features (16x16x32 A operands, fragments 36 + 2 mb + s), loaded from global memory during
+    // the chain (they are read once, after the last step)
+    [[maybe_unused]] h8 W0g[2][2];
+    if constexpr (ENC == 1) {
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) W0g[mb][s] = wb[(kT16BwdFrags + 2 * mb + s) * 64 + lane];
+    }
     NRC_T16S_STEP(4, img_d1, img_a1)
     NRC_T16S_STEP(3, img_d0, img_a0)
     NRC_T16S_STEP(2, img_d1, img_a1)
     NRC_T16S_STEP(1, img_d0, img_a0)
 #undef NRC_T16S_STEP
+    if constexpr (ENC == 1) {
+        // dL/d(grid slot 16 mb + 4 g + i) of sample c = (W0^T delta_0): registers (0, 1) / (2, 3) of M-block mb are the
+        // two features of levels 8 mb + 2 g and 8 mb + 2 g + 1; f16 pairs [level][sample], zeros for padding samples
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int64_t sg = (int64_t)blockIdx.x * (64 * G) + r[u];
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+                f4 c = mfma16(W0g[mb][0], d[u][0], f4{0.f, 0.f, 0.f, 0.f});
+                c = mfma16(W0g[mb][1], d[u][1], c);
+                const int lv = 8 * mb + 2 * g;
+                ho.dy[(int64_t)lv * ho.bcap + sg] = valid[u] ? pk2(c[0], c[1]) : 0u;
+                ho.dy[(int64_t)(lv + 1) * ho.bcap + sg] = valid[u] ? pk2(c[2], c[3]) : 0u;
+            }
+            if (g == 0) ho.pos[sg] = float4{pq[u].x, pq[u].y, pq[u].z, 0.0f};
+        }
+    }
 }
 
 int t16_blocks(int64_t b, int groups = 2) { return (int)((b + 64 * groups - 1) / (64 * groups)); }
@@ -809,7 +845,7 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
     if (padq) {  // padded RadianceQuery records: the production shape only
         if (!split || stamps || groups != 2) return hipErrorNotSupported;
         hipLaunchKernelGGL((train16_split_kernel<16, 2, true>), grid, dim3(128 * kWaves), 0, s, queries, targets, b,
-                           n_total, loss_scale, f, bw, slabs, loss_partials);
+                           n_total, loss_scale, f, bw, slabs, loss_partials, HashTrainOut{});
         return hipGetLastError();
     }
     if (split && !stamps) {
@@ -821,14 +857,14 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
             // each; bitwise the decoupled-chain shape 4, but 14.5-14.7 vs 12.9-13.7 us per step
 #if NRC_DEBUG_KERNELS
             hipLaunchKernelGGL((train16_split_kernel<16, 1>), dim3(t16_blocks(b, 1)), dim3(128 * kWaves), 0, s, queries,
-                               targets, b, n_total, loss_scale, f, bw, slabs, loss_partials);
+                               targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, HashTrainOut{});
             return hipGetLastError();
 #else
             return hipErrorNotSupported;
 #endif
         }
         hipLaunchKernelGGL((train16_split_kernel<16, 2>), grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
-                           loss_scale, f, bw, slabs, loss_partials);
+                           loss_scale, f, bw, slabs, loss_partials, HashTrainOut{});
         return hipGetLastError();
     }
 #if NRC_DEBUG_KERNELS
@@ -843,6 +879,16 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
 #else
     return hipErrorNotSupported;  // the 4-wave kernel and the stamped builds live in libnrc_amd_debug.so
 #endif
+}
+
+hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                               const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
+                               const HashTrainOut& ho, hipStream_t s) {
+    if (b <= 0) return hipSuccess;
+    if (!ho.table || !ho.pos || !ho.dy || ho.bcap < (int64_t)t16_blocks(b) * 128) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 1>), dim3(t16_blocks(b)), dim3(128 * kWaves), 0, s, queries,
+                       targets, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, ho);
+    return hipGetLastError();
 }
 
 }  // namespace nrc_amd
