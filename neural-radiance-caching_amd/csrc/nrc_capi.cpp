@@ -323,6 +323,16 @@ std::string config_json(int encoding, const nrc_config& c) {
 
 struct nrc_net {
     hipStream_t stream = nullptr;
+    // Hash training (round 5): a second stream on which the MLP reduce + Adam runs beside the grid scatter (they touch
+    // disjoint state); fork after the training kernel, join before the step ends (side_ready)
+    hipStream_t side = nullptr;
+    hipEvent_t side_fork = nullptr, side_join = nullptr;
+    void side_ready() {
+        if (side) return;
+        HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&side_fork, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&side_join, hipEventDisableTiming));
+    }
     int encoding = NRC_ENCODING_FREQUENCY;
     int config_encoding = NRC_ENCODING_FREQUENCY;  // what nrc_set_config last asked for (JSON only, see there)
     nrc_config cfg{};
@@ -480,6 +490,12 @@ struct nrc_net {
         frame_scratch_bytes = 0;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer); f(hash_feat);
         hash_feat = nullptr;
+        if (side) (void)hipStreamSynchronize(side);
+        if (side_fork) (void)hipEventDestroy(side_fork);
+        if (side_join) (void)hipEventDestroy(side_join);
+        if (side) (void)hipStreamDestroy(side);
+        side = nullptr;
+        side_fork = side_join = nullptr;
         if (feat_done) (void)hipEventDestroy(feat_done);
         feat_done = nullptr;
         feat_stream = nullptr;
@@ -683,16 +699,26 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     }
     const int blocks = train_block_count(net, b);
     net->ensure_slabs(blocks);
-    if (net->hash())
+    if (net->hash()) {
+        // training kernel -> fork: [main] grid scatter -> grid Adam, [side] MLP slab reduce + Adam -> join
+        net->side_ready();
         HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
                                     net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                    net->step_scatter(blocks), net->padq(), net->t16));
-    else
-        train_partials(net, in, tgt, b, 3.0f * (float)b);
+                                    net->step_scatter(blocks), net->padq(), net->t16, net->side_fork));
+        net->step += 1;
+        HIP_CHECK(hipStreamWaitEvent(net->side, net->side_fork, 0));
+        HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
+                                     loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->side));
+        HIP_CHECK(hipEventRecord(net->side_join, net->side));
+        HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
+        HIP_CHECK(hipStreamWaitEvent(net->stream, net->side_join, 0));
+        if (loss_h) *loss_h = net->read_loss();
+        return;
+    }
+    train_partials(net, in, tgt, b, 3.0f * (float)b);
     net->step += 1;
     HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
                                  loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
-    if (net->hash()) HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
     if (loss_h) {
         *loss_h = net->read_loss();
     }

@@ -425,7 +425,7 @@ hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, con
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false,
-                             bool t16 = false);
+                             bool t16 = false, hipEvent_t after_train = nullptr);  // recorded between training kernel and scatter
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);

@@ -3884,7 +3884,7 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc, bool padq,
-                             bool t16) {
+                             bool t16, hipEvent_t after_train) {
     if (b <= 0) return hipSuccess;
     const int blocks = train_blocks(b);
     const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
@@ -3906,6 +3906,10 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
                            loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
                            reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
                            bcap);
+    if (after_train) {
+        const hipError_t e = hipEventRecord(after_train, s);
+        if (e != hipSuccess) return e;
+    }
     // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep of the exact 64-bit scatter,
     // profiles/r03_hash/scatter_plan_sweep.txt (round 1's f16 scatter: profiles/r01_hash/README.md)
     const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);
