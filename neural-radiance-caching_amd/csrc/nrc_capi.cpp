@@ -255,12 +255,12 @@ std::vector<int> build_t16_slab_map(int encoding) {
 
 // Training kernel of a 64-wide Frequency network: the t16-layout kernels (f16 slabs) unless the train_kernel knob
 // selects the round-1 32x32x16 train_kernel (in-process A/B; read once per nrc_init).
-// Round 5: InputEncoding::Hash too (compact records; padded Hash handles keep the 32x32 kernel).
+// Round 5: InputEncoding::Hash too (compact and padded records).
 // backward image allocation: the largest layout (32x32 Hash 38 fragments, t16 Frequency 36, t16 Hash 40)
 constexpr int kWbHalves = (kBwdFragsHash > kT16BwdFragsHash ? kBwdFragsHash : kT16BwdFragsHash) * kFragHalves;
-bool want_t16(int encoding, bool padq) {
+bool want_t16(int encoding) {
     if (knob(kKnobTrainKernel) == 32) return false;
-    return encoding == NRC_ENCODING_FREQUENCY || (encoding == NRC_ENCODING_HASH && !padq);
+    return encoding == NRC_ENCODING_FREQUENCY || encoding == NRC_ENCODING_HASH;
 }
 
 std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
@@ -1054,7 +1054,7 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemset(net->wf_infer, 0, sizeof(_Float16) * kFwdHalves));
         std::vector<int> fwd, bwd;
         build_scatter_maps(fwd, bwd, net->encoding);
-        net->t16 = want_t16(net->encoding, net->padq());
+        net->t16 = want_t16(net->encoding);
         {
             // the decoupled-chain kernel is the default; knob train_kernel = 1 / 2 selects round 2's role-split /
             // 4-wave t16 kernels (in-process A/B)

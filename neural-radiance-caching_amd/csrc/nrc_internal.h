@@ -335,7 +335,7 @@ struct HashTrainOut {
 };
 hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                                const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
-                               const HashTrainOut& ho, hipStream_t s);
+                               const HashTrainOut& ho, hipStream_t s, bool padq = false);
 // samples per block of the role-split t16 kernel: 64 x groups (knob "t16_groups"; 128 by default)
 int t16_groups();  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16

@@ -3891,11 +3891,10 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
     if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap || !sc->nf.codes || !sc->nf.tag_dev || !sc->nf.tag)
         return hipErrorInvalidValue;
     if (t16) {  // round 5: the t16 role-split kernel (nrc_train16.hip), f16 slabs in the t16 layout
-        if (padq) return hipErrorNotSupported;
         const hipError_t e = launch_train16_hash(queries, targets, b, n_total, loss_scale, wf, wb,
                                                  reinterpret_cast<_Float16*>(slabs), loss_partials,
                                                  HashTrainOut{reinterpret_cast<const uint32_t*>(grid), sc->pos, sc->dy, bcap},
-                                                 s);
+                                                 s, padq);
         if (e != hipSuccess) return e;
     } else if (padq)
         hipLaunchKernelGGL((train_kernel<false, 1, true>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,

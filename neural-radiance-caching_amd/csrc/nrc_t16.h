@@ -71,15 +71,17 @@ __device__ __forceinline__ void encode16(float p0, float p1, float p2, float bA,
 // sample (hash_level_feature: tcnn's corners and f16 interpolation, gathers from the f16 training table), pad 1.0,
 // Identity, pad, OneBlob as encode16, pads. Levels 0 and 1 (group 0) are dense: the first two levels of every group
 // take the dense/hashed select.
+// pad: the value of slot 8 of lane group 0 -- canonical feature 62, the first constant-one column -- 1.0 for compact
+// queries and the query's pad_ for padded ones
 __device__ __forceinline__ void encode16_hash(float p0, float p1, float p2, float bA, float bB, float iA, float iB, int g,
-                                              const uint32_t* __restrict__ table, h8 (&x)[3]) {
+                                              const uint32_t* __restrict__ table, h8 (&x)[3], float pad = 1.0f) {
     uint32_t w[12];
     const int l0 = 4 * g;
     w[0] = hash_level_feature<true>(p0, p1, p2, l0, table);
     w[1] = hash_level_feature<true>(p0, p1, p2, l0 + 1, table);
     w[2] = hash_level_feature<false>(p0, p1, p2, l0 + 2, table);
     w[3] = hash_level_feature<false>(p0, p1, p2, l0 + 3, table);
-    w[4] = pk2(1.0f, iA);
+    w[4] = pk2(g == 0 ? pad : 1.0f, iA);
     w[5] = pk2(iB, 1.0f);
     blob_v3(bA, w[6], w[7]);
     blob_v3(bB, w[8], w[9]);

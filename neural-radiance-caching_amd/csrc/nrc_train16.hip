@@ -629,13 +629,10 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         tg[u][0] = tq[u].x; tg[u][1] = tq[u].y; tg[u][2] = tq[u].z;
-        if constexpr (ENC == 1) {
-            encode16_hash(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, ho.table, x[u]);
-        } else {
-            float pad = 1.0f;
-            if constexpr (PADQ) pad = pq[u].w;
-            encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
-        }
+        float pad = 1.0f;
+        if constexpr (PADQ) pad = pq[u].w;
+        if constexpr (ENC == 1) encode16_hash(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, ho.table, x[u], pad);
+        else encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
         const u4 w = __builtin_bit_cast(u4, x[u][2]);
         *(u2*)(img_x2 + off32(r[u], 2 * g)) = u2{w.x, w.y};
         *(u2*)(img_x2 + off32(r[u], 2 * g + 1)) = u2{w.z, w.w};
@@ -883,11 +880,15 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
 
 hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                                const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
-                               const HashTrainOut& ho, hipStream_t s) {
+                               const HashTrainOut& ho, hipStream_t s, bool padq) {
     if (b <= 0) return hipSuccess;
     if (!ho.table || !ho.pos || !ho.dy || ho.bcap < (int64_t)t16_blocks(b) * 128) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 1>), dim3(t16_blocks(b)), dim3(128 * kWaves), 0, s, queries,
-                       targets, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, ho);
+    if (padq)
+        hipLaunchKernelGGL((train16_split_kernel<16, 2, true, 1>), dim3(t16_blocks(b)), dim3(128 * kWaves), 0, s, queries,
+                           targets, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, ho);
+    else
+        hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 1>), dim3(t16_blocks(b)), dim3(128 * kWaves), 0, s, queries,
+                           targets, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, ho);
     return hipGetLastError();
 }
 
