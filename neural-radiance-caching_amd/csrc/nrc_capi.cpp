@@ -323,16 +323,6 @@ std::string config_json(int encoding, const nrc_config& c) {
 
 struct nrc_net {
     hipStream_t stream = nullptr;
-    // Hash training (round 5): a second stream on which the MLP reduce + Adam runs beside the grid scatter (they touch
-    // disjoint state); fork after the training kernel, join before the step ends (side_ready)
-    hipStream_t side = nullptr;
-    hipEvent_t side_fork = nullptr, side_join = nullptr;
-    void side_ready() {
-        if (side) return;
-        HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-        HIP_CHECK(hipEventCreateWithFlags(&side_fork, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&side_join, hipEventDisableTiming));
-    }
     int encoding = NRC_ENCODING_FREQUENCY;
     int config_encoding = NRC_ENCODING_FREQUENCY;  // what nrc_set_config last asked for (JSON only, see there)
     nrc_config cfg{};
@@ -490,12 +480,6 @@ struct nrc_net {
         frame_scratch_bytes = 0;
         f(grid_grad); f(grid_steps); f(grid_bias); f(table_train); f(table_infer); f(hash_feat);
         hash_feat = nullptr;
-        if (side) (void)hipStreamSynchronize(side);
-        if (side_fork) (void)hipEventDestroy(side_fork);
-        if (side_join) (void)hipEventDestroy(side_join);
-        if (side) (void)hipStreamDestroy(side);
-        side = nullptr;
-        side_fork = side_join = nullptr;
         if (feat_done) (void)hipEventDestroy(feat_done);
         feat_done = nullptr;
         feat_stream = nullptr;
@@ -682,6 +666,18 @@ void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b,
                                        net->slabs, net->loss_partials, net->stream, net->encoding));
 }
 
+// Hash fwd + loss + bwd + dW slabs + grid scatter of b samples (n_total = 3 x global batch). The t16 kernel reads the
+// batch's level features from the handle's feature workspace (shared with inference: the event protocol of
+// hash_feat_acquire / _release orders them across streams); knob hash_infer = 1 keeps the gathering encoder (A/B).
+void train_hash(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total, int blocks) {
+    uint32_t* const feat = net->t16 && knob(kKnobHashInfer) != 1 ? net->hash_feat : nullptr;
+    if (feat) net->hash_feat_acquire(net->stream);
+    HIP_CHECK(launch_train_hash(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train, net->table_train,
+                                net->grid_grad, net->slabs, net->loss_partials, net->stream, net->step_scatter(blocks),
+                                net->padq(), net->t16, feat));
+    if (feat) net->hash_feat_release(net->stream);
+}
+
 void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float* loss_h, float* loss_d = nullptr) {
     check_live(net);
     if (b == 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "batch size must be >= 1");
@@ -700,18 +696,19 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     const int blocks = train_block_count(net, b);
     net->ensure_slabs(blocks);
     if (net->hash()) {
-        // training kernel -> fork: [main] grid scatter -> grid Adam, [side] MLP slab reduce + Adam -> join
-        net->side_ready();
-        HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train, net->wb_train,
-                                    net->table_train, net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                    net->step_scatter(blocks), net->padq(), net->t16, net->side_fork));
+        // training kernel + grid scatter, then both optimizer updates: one launch for the t16 slabs (launch_hash_adam;
+        // a second stream for the MLP update measured slower: each cross-stream event added ~6 us of idle GPU)
+        train_hash(net, in, tgt, b, 3.0f * (float)b, blocks);
         net->step += 1;
-        HIP_CHECK(hipStreamWaitEvent(net->side, net->side_fork, 0));
-        HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
-                                     loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->side));
-        HIP_CHECK(hipEventRecord(net->side_join, net->side));
-        HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
-        HIP_CHECK(hipStreamWaitEvent(net->stream, net->side_join, 0));
+        float* const ld = loss_d ? loss_d : net->loss_dev;
+        if (net->t16) {
+            HIP_CHECK(launch_hash_adam(net->slabs, blocks, net->loss_partials, ld, net->buffers(), net->grid_buffers(),
+                                       net->optim(net->step), net->stream));
+        } else {
+            HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr, ld, net->buffers(),
+                                         net->optim(net->step), net->stream));
+            HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
+        }
         if (loss_h) *loss_h = net->read_loss();
         return;
     }
@@ -1446,9 +1443,7 @@ void do_train_grad(nrc_net* net, const float* in, const float* tgt, uint32_t b, 
             // exported after the MLP part: rounded to f16, as f32, into the caller's gradient (nrc_train_grad), or
             // exchange-encoded into grid_fixed (nrc_train_grad_fixed, nrc_train_dp); the export zeroes the buffer
             // (unless grid_fixed is the buffer itself)
-            HIP_CHECK(launch_train_hash(in, tgt, b, 3.0f * (float)global_b, net->cfg.loss_scale, net->wf_train,
-                                        net->wb_train, net->table_train, net->grid_grad, net->slabs, net->loss_partials,
-                                        net->stream, net->step_scatter(blocks), net->padq(), net->t16));
+            train_hash(net, in, tgt, b, 3.0f * (float)global_b, blocks);
             if (grid_fixed)
                 HIP_CHECK(launch_grid_grad_export_fixed(net->grid_grad, grid_fixed, net->n_grid, net->nonfinite(),
                                                         net->stream));

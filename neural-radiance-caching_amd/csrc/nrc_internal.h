@@ -324,11 +324,13 @@ struct ModelBuffers {
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
                           hipStream_t s, bool split = false, int groups = 2, bool padq = false);
-// InputEncoding::Hash on the t16 role-split kernel (round 5): the encoder gathers levels 4g .. 4g + 3 from the f16
-// training table; the chain waves also write each sample's position and its 16 levels' (dy0, dy1) = W0^T delta_0 of the
+// InputEncoding::Hash on the t16 role-split kernel (round 5): the encoder reads levels 4g .. 4g + 3 from the feature
+// pass's workspace (or gathers them from the f16 training table); the chain waves also write each sample's position and its 16 levels' (dy0, dy1) = W0^T delta_0 of the
 // grid features (f16 pairs, [level][sample], zeros past b) for grid_scatter_kernel. wb: kT16BwdFragsHash fragments.
 struct HashTrainOut {
     const uint32_t* table;  // f16 training table as half2 entries
+    const uint32_t* feat;   // the samples' level features ([level][kHashFeatStride], hash_feature_kernel over the batch
+                            // with the training table), or null: the kernel gathers from the table itself
     float4* pos;            // [bcap]
     uint32_t* dy;           // [NRC_HASH_LEVELS][bcap]
     int64_t bcap;
@@ -402,6 +404,9 @@ struct GridBuffers {
 // corrections are exactly 1.0f there)
 constexpr uint32_t kGridBiasLen = 1u << 16;
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
+// Hash training (round 5): the MLP's fused slab reduce + Adam/EMA (f16 t16 slabs) and the grid's Adam in one launch
+hipError_t launch_hash_adam(const float* slabs, int nslabs, const float* loss_partials, float* loss_out,
+                            const ModelBuffers& mb, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
 // Hash training workspace: per sample its position and the 16 levels' (dy0, dy1) f16 pairs ([level][sample]),
 // written by the training kernel and consumed by grid_scatter_kernel.
 struct HashScatter {
@@ -422,10 +427,11 @@ hipError_t launch_grid_grad_export_fixed(int64_t* g64, int64_t* out, int n, cons
 constexpr int kFixedMaxRanks = 63;
 hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, const _Float16* wf, uint64_t* stamps,
                                 int64_t* waves, hipStream_t s);
+// feat (t16 only, may be null): the handle's level-feature workspace; the batch's features are computed into it first
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false,
-                             bool t16 = false, hipEvent_t after_train = nullptr);  // recorded between training kernel and scatter
+                             bool t16 = false, uint32_t* feat = nullptr);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);

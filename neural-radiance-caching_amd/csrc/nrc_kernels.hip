@@ -2461,31 +2461,31 @@ __device__ __forceinline__ float lane_partial_sum(const float* __restrict__ p, i
 // butterfly (one load latency instead of a serial chain of nslabs loads).
 // H: f16 slabs (the t16 training kernel's), converted to f32 before the same fixed-order f32 sums
 template <bool H>
-__global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
-                                                          const float* __restrict__ loss_partials,
-                                                          float* __restrict__ grad_io, float* __restrict__ loss_out,
-                                                          ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+__device__ __forceinline__ void reduce_adam_body(const int blk, int mode, const float* __restrict__ slabs, int nslabs,
+                                                 const float* __restrict__ loss_partials, float* __restrict__ grad_io,
+                                                 float* __restrict__ loss_out, const ModelBuffers& mb,
+                                                 const OptimArgs& oa, float lr_t, float ema_debias) {
 #pragma clang fp contract(off)
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ f4 part[kRedGroups][kRedParams];
     const int pl = threadIdx.x & (kRedParams - 1), grp = threadIdx.x / kRedParams;
-    const int p0 = (blockIdx.x * kRedParams + pl) * kRedVec;  // slab position (reduce modes) / parameter (apply, pack)
+    const int p0 = (blk * kRedParams + pl) * kRedVec;  // slab position (reduce modes) / parameter (apply, pack)
     // diagnostic build: per-block s_memrealtime stamps of thread 0 (entry, slab sums done, after the combine barrier,
     // Adam issued) in g_infer_clock, read back by nrc_debug_read_infer_clock (tools/reduce_stamps.py)
     auto stamp = [&](int k) {
 #if NRC_DEBUG_KERNELS
-        if (threadIdx.x == 0 && mode == kReduceFused && blockIdx.x < kInferClockWavesMax)
-            g_infer_clock[6 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
-        if (k == 0 && threadIdx.x == 0 && mode == kReduceFused && blockIdx.x < kInferClockWavesMax) {
-            g_infer_clock[6 * blockIdx.x + 4] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-            g_infer_clock[6 * blockIdx.x + 5] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
+        if (threadIdx.x == 0 && mode == kReduceFused && blk < kInferClockWavesMax)
+            g_infer_clock[6 * blk + k] = __builtin_amdgcn_s_memrealtime();
+        if (k == 0 && threadIdx.x == 0 && mode == kReduceFused && blk < kInferClockWavesMax) {
+            g_infer_clock[6 * blk + 4] = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+            g_infer_clock[6 * blk + 5] = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);
         }
 #else
         (void)k;
 #endif
     };
     stamp(0);
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
+    if (blk == 0 && threadIdx.x < 64) {
         if (mode == kReduceFused || mode == kReduceOnly) {
             float L = 0.0f;
             L = lane_partial_sum(loss_partials, nslabs, threadIdx.x);
@@ -2506,7 +2506,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         // in one go (the remainder used to be a serial loop: 4 round trips for the 64 slabs of a 2,048-sample step).
         // the slab position this thread combines (threads < 64): t16 slabs map it in closed form, the 32x32 slabs
         // through the map (one branch-free load, every thread)
-        const int mypos = blockIdx.x * kRedParams * kRedVec + (threadIdx.x & (kRedParams * kRedVec - 1));
+        const int mypos = blk * kRedParams * kRedVec + (threadIdx.x & (kRedParams * kRedVec - 1));
         int pp_raw;
         if constexpr (H) pp_raw = mb.slab_closed ? t16_slab_param(mypos) : mb.slab_param[mypos];
         else pp_raw = mb.slab_param[mypos];
@@ -2570,8 +2570,16 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, cons
         return;
     }
     if (threadIdx.x >= kRedParams * kRedVec) return;
-    const int p = blockIdx.x * kRedParams * kRedVec + threadIdx.x;
+    const int p = blk * kRedParams * kRedVec + threadIdx.x;
     adam_pack_one(mode, p, mode == kApplyOnly ? grad_io[p] : 0.0f, mb, oa, lr_t, ema_debias);
+}
+
+template <bool H>
+__global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(int mode, const float* __restrict__ slabs, int nslabs,
+                                                          const float* __restrict__ loss_partials,
+                                                          float* __restrict__ grad_io, float* __restrict__ loss_out,
+                                                          ModelBuffers mb, OptimArgs oa, float lr_t, float ema_debias) {
+    reduce_adam_body<H>(blockIdx.x, mode, slabs, nslabs, loss_partials, grad_io, loss_out, mb, oa, lr_t, ema_debias);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3175,13 +3183,14 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
 }
 
 // One feature pass of hash_feature_kernel over cnt <= kHashFeatStride queries (the launch shape of launch_infer_hash).
+// p_default: query ranges per level when the knob is unset (0: the inference choice below)
 static void launch_hash_feature_pass(const float* qc0, int64_t cnt, const uint32_t* g, uint32_t* feat, bool padq,
-                                     hipStream_t s) {
+                                     hipStream_t s, int p_default = 0) {
     // query ranges per level (multiple of the 8 XCDs); knob hash_feat_p overrides (A/B). Round 4: 32 above 2^19
     // queries (4 blocks per CU, two ranges' positions per XCD L2 at a time): 179.7 vs 185.3 us (P = 16) per 2^21
     // queries in-process, 24 / 48 / 64 / 128 slower (profiles/r04_hash/ab_hash_feat_p*.json)
     const int kp = knob(kKnobHashFeatP);
-    const int P = kp > 0 ? kp : cnt > ((int64_t)1 << 19) ? 32 : 8;
+    const int P = kp > 0 ? kp : p_default > 0 ? p_default : cnt > ((int64_t)1 << 19) ? 32 : 8;
 #if NRC_DEBUG_KERNELS
     const int fa = knob(kKnobHashFeatAbl);
     if (fa > 0) {
@@ -3688,9 +3697,10 @@ __device__ __forceinline__ float fixed_decode_gradient(int64_t e) {
     return fixed_gradient((int64_t)(u & ((1ull << 48) - 1)) - kFixedOff, code);
 }
 
-__global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
+__device__ __forceinline__ void grid_adam_body(const int blk, int mode, const GridBuffers& gb, const OptimArgs& oa,
+                                               float ema_debias) {
 #pragma clang fp contract(off)
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blk * 256 + threadIdx.x;
     if (i >= gb.n) return;
     float w = gb.params[i], inf;
     if (mode == kPackOnly) {
@@ -3736,6 +3746,45 @@ __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb
     }
     gb.table_train[i] = (_Float16)w;
     gb.table_infer[i] = (_Float16)inf;
+}
+
+__global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
+    grid_adam_body(blockIdx.x, mode, gb, oa, ema_debias);
+}
+
+// The Hash training step's two optimizer updates in one launch (round 5): blocks [0, nred) reduce the MLP's f16 slabs and
+// apply its Adam/EMA (reduce_adam_kernel<true>, kReduceFused), the rest step the grid (grid_adam_kernel, kReduceFused).
+// They touch disjoint state; the latency-bound slab reduction runs beside the grid's HBM streaming instead of behind
+// it, and the step has one kernel boundary fewer.
+// (the two halves as separate functions: inlined into one body the compiler wraps both in one loop region, which the
+// scalar-branch-load + masked-store rule of tools/asm_hazard_check.py rejects)
+__device__ __attribute__((noinline)) void hash_adam_mlp(int blk, const float* slabs, int nslabs, const float* loss_partials,
+                                                        float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
+                                                        float lr_t, float ema_debias) {
+    reduce_adam_body<true>(blk, kReduceFused, slabs, nslabs, loss_partials, nullptr, loss_out, mb, oa, lr_t, ema_debias);
+}
+__device__ __attribute__((noinline)) void hash_adam_grid(int blk, const GridBuffers& gb, const OptimArgs& oa,
+                                                         float ema_debias) {
+    grid_adam_body(blk, kReduceFused, gb, oa, ema_debias);
+}
+__global__ __launch_bounds__(256) void hash_adam_kernel(int nred, const float* __restrict__ slabs, int nslabs,
+                                                        const float* __restrict__ loss_partials, float* __restrict__ loss_out,
+                                                        ModelBuffers mb, GridBuffers gb, OptimArgs oa, float lr_t,
+                                                        float ema_debias) {
+    if ((int)blockIdx.x < nred) hash_adam_mlp(blockIdx.x, slabs, nslabs, loss_partials, loss_out, mb, oa, lr_t, ema_debias);
+    else hash_adam_grid((int)blockIdx.x - nred, gb, oa, ema_debias);
+}
+
+hipError_t launch_hash_adam(const float* slabs, int nslabs, const float* loss_partials, float* loss_out,
+                            const ModelBuffers& mb, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s) {
+    if (!mb.slab_f16 || nslabs < 1) return hipErrorInvalidValue;
+    static_assert(kRedThreads == 256, "one block shape for both halves");
+    float lr_t, ema_debias;
+    adam_host_factors(oa, lr_t, ema_debias);
+    const int nred = mb.n_slab / (kRedParams * kRedVec);
+    hipLaunchKernelGGL(hash_adam_kernel, dim3((unsigned)(nred + (gb.n + 255) / 256)), dim3(256), 0, s, nred, slabs, nslabs,
+                       loss_partials, loss_out, mb, gb, oa, lr_t, ema_debias);
+    return hipGetLastError();
 }
 
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s) {
@@ -3884,17 +3933,21 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc, bool padq,
-                             bool t16, hipEvent_t after_train) {
+                             bool t16, uint32_t* feat) {
     if (b <= 0) return hipSuccess;
     const int blocks = train_blocks(b);
     const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
     if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap || !sc->nf.codes || !sc->nf.tag_dev || !sc->nf.tag)
         return hipErrorInvalidValue;
     if (t16) {  // round 5: the t16 role-split kernel (nrc_train16.hip), f16 slabs in the t16 layout
+        const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
+        // the batch's level features first, one level table per block in LDS (hash_feature_kernel, as for inference):
+        // the training kernel's 128 blocks would otherwise gather 2 M table entries at their CUs' L1 line rate
+        const bool fp = feat && b <= kHashFeatStride;
+        if (fp) launch_hash_feature_pass(queries, b, g, feat, padq, s, b >= 8192 ? 16 : 8);
         const hipError_t e = launch_train16_hash(queries, targets, b, n_total, loss_scale, wf, wb,
                                                  reinterpret_cast<_Float16*>(slabs), loss_partials,
-                                                 HashTrainOut{reinterpret_cast<const uint32_t*>(grid), sc->pos, sc->dy, bcap},
-                                                 s, padq);
+                                                 HashTrainOut{g, fp ? feat : nullptr, sc->pos, sc->dy, bcap}, s, padq);
         if (e != hipSuccess) return e;
     } else if (padq)
         hipLaunchKernelGGL((train_kernel<false, 1, true>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
@@ -3905,10 +3958,6 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
                            loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
                            reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
                            bcap);
-    if (after_train) {
-        const hipError_t e = hipEventRecord(after_train, s);
-        if (e != hipSuccess) return e;
-    }
     // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep of the exact 64-bit scatter,
     // profiles/r03_hash/scatter_plan_sweep.txt (round 1's f16 scatter: profiles/r01_hash/README.md)
     const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);

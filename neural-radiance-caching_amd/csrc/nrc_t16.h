@@ -90,6 +90,21 @@ __device__ __forceinline__ void encode16_hash(float p0, float p1, float p2, floa
     for (int s = 0; s < 3; ++s) x[s] = __builtin_bit_cast(h8, u4{w[4 * s], w[4 * s + 1], w[4 * s + 2], w[4 * s + 3]});
 }
 
+// The same slots with the 4 level features already computed (hash_feature_kernel's workspace): F[i] = level 4g + i.
+__device__ __forceinline__ void encode16_hashf(const uint32_t (&F)[4], float bA, float bB, float iA, float iB, int g,
+                                               h8 (&x)[3], float pad = 1.0f) {
+    uint32_t w[12];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = F[i];
+    w[4] = pk2(g == 0 ? pad : 1.0f, iA);
+    w[5] = pk2(iB, 1.0f);
+    blob_v3(bA, w[6], w[7]);
+    blob_v3(bB, w[8], w[9]);
+    w[10] = w[11] = 0x3C003C00u;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) x[s] = __builtin_bit_cast(h8, u4{w[4 * s], w[4 * s + 1], w[4 * s + 2], w[4 * s + 3]});
+}
+
 // ---- training-side pieces shared by nrc_train16.hip and nrc_train_dc.hip ----
 typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 

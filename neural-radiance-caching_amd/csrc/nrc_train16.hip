@@ -491,7 +491,8 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // dependency latency; the step's critical path is the chain alone instead of chain + dW.
 // G: 16-sample groups per chain wave (64 G samples per block); PADQ: padded RadianceQuery records (16 floats: the
 // position load takes pad_ along, 16 bytes instead of 12, the other loads one float further)
-// ENC 1 (round 5): InputEncoding::Hash -- the encoder gathers each lane group's 4 grid levels (t16_hash_slot_feature),
+// ENC 3 / 1 (round 5): InputEncoding::Hash -- the encoder reads each lane group's 4 grid levels (t16_hash_slot_feature)
+// from the batch's feature pass (3) or gathers them from the table (1, A/B),
 // and after the last chain step the chain waves form dL/d(grid features) = W0^T delta_0 (4 MFMAs per group from the
 // backward image's fragments 36..39, read from global memory) and write it with the sample positions for
 // grid_scatter_kernel (ho). Everything else -- forward, loss, delta chain, dW waves, slab layout -- is the Frequency
@@ -597,6 +598,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     PQ pq[G];
     f3 tq[G];
     f2 bl[G], id[G];
+    [[maybe_unused]] uint32_t F[G][4];  // ENC 3: the sample's level features 4g .. 4g + 3 (hash_feature_kernel)
     const int gg = g < 3 ? g : 0;
 #pragma unroll
     for (int u = 0; u < G; ++u) {
@@ -610,6 +612,13 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(bl[u]) : "v"(qr + 3 + X + 2 * gg) : "memory");
         asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(id[u]) : "v"(qr + 9 + X + 2 * gg) : "memory");
         asm volatile("global_load_dwordx3 %0, %1, off" : "=v"(tq[u]) : "v"(t + sc * 3) : "memory");
+        if constexpr (ENC == 3) {
+            // padding samples read the last sample's features (finite), as they read its query
+            const uint32_t* fr = ho.feat + (int64_t)(4 * g) * kHashFeatStride + sc;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                asm volatile("global_load_dword %0, %1, off" : "=v"(F[u][i]) : "v"(fr + i * kHashFeatStride) : "memory");
+        }
     }
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
@@ -617,7 +626,14 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         __builtin_amdgcn_global_load_lds((const void*)(wf + (f < kT16FwdFrags ? f : kT16FwdFrags - 1) * 64 + lane),
                                          (__attribute__((address_space(3))) void*)(lwf + f * 64), 16, 0, 0);
     }
-    if constexpr (G == 2)
+    if constexpr (G == 2 && ENC == 3)
+        asm volatile("s_waitcnt vmcnt(12)"
+                     : "+v"(pq[0]), "+v"(pq[1]), "+v"(bl[0]), "+v"(bl[1]), "+v"(id[0]), "+v"(id[1]), "+v"(tq[0]), "+v"(tq[1]),
+                       "+v"(F[0][0]), "+v"(F[0][1]), "+v"(F[0][2]), "+v"(F[0][3]), "+v"(F[1][0]), "+v"(F[1][1]),
+                       "+v"(F[1][2]), "+v"(F[1][3])
+                     :
+                     : "memory");
+    else if constexpr (G == 2)
         asm volatile("s_waitcnt vmcnt(12)"
                      : "+v"(pq[0]), "+v"(pq[1]), "+v"(bl[0]), "+v"(bl[1]), "+v"(id[0]), "+v"(id[1]), "+v"(tq[0]), "+v"(tq[1])
                      :
@@ -631,7 +647,8 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         tg[u][0] = tq[u].x; tg[u][1] = tq[u].y; tg[u][2] = tq[u].z;
         float pad = 1.0f;
         if constexpr (PADQ) pad = pq[u].w;
-        if constexpr (ENC == 1) encode16_hash(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, ho.table, x[u], pad);
+        if constexpr (ENC == 3) encode16_hashf(F[u], bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
+        else if constexpr (ENC == 1) encode16_hash(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, ho.table, x[u], pad);
         else encode16(pq[u].x, pq[u].y, pq[u].z, bl[u].x, bl[u].y, id[u].x, id[u].y, g, x[u], pad);
         const u4 w = __builtin_bit_cast(u4, x[u][2]);
         *(u2*)(img_x2 + off32(r[u], 2 * g)) = u2{w.x, w.y};
@@ -799,7 +816,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     // Hash: W0^T of the grid features (16x16x32 A operands, fragments 36 + 2 mb + s), loaded from global memory during
     // the chain (they are read once, after the last step)
     [[maybe_unused]] h8 W0g[2][2];
-    if constexpr (ENC == 1) {
+    if constexpr (ENC == 1 || ENC == 3) {
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -810,7 +827,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     NRC_T16S_STEP(2, img_d1, img_a1)
     NRC_T16S_STEP(1, img_d0, img_a0)
 #undef NRC_T16S_STEP
-    if constexpr (ENC == 1) {
+    if constexpr (ENC == 1 || ENC == 3) {
         // dL/d(grid slot 16 mb + 4 g + i) of sample c = (W0^T delta_0): registers (0, 1) / (2, 3) of M-block mb are the
         // two features of levels 8 mb + 2 g and 8 mb + 2 g + 1; f16 pairs [level][sample], zeros for padding samples
 #pragma unroll
@@ -883,12 +900,19 @@ hipError_t launch_train16_hash(const float* queries, const float* targets, int64
                                const HashTrainOut& ho, hipStream_t s, bool padq) {
     if (b <= 0) return hipSuccess;
     if (!ho.table || !ho.pos || !ho.dy || ho.bcap < (int64_t)t16_blocks(b) * 128) return hipErrorInvalidValue;
-    if (padq)
-        hipLaunchKernelGGL((train16_split_kernel<16, 2, true, 1>), dim3(t16_blocks(b)), dim3(128 * kWaves), 0, s, queries,
-                           targets, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, ho);
+    const dim3 grid(t16_blocks(b)), block(128 * kWaves);
+    const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
+    if (ho.feat && padq)
+        hipLaunchKernelGGL((train16_split_kernel<16, 2, true, 3>), grid, block, 0, s, queries, targets, b, n_total,
+                           loss_scale, f, bw, slabs, loss_partials, ho);
+    else if (ho.feat)
+        hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 3>), grid, block, 0, s, queries, targets, b, n_total,
+                           loss_scale, f, bw, slabs, loss_partials, ho);
+    else if (!padq)  // the gathering encoder (A/B: knob hash_infer = 1)
+        hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 1>), grid, block, 0, s, queries, targets, b, n_total,
+                           loss_scale, f, bw, slabs, loss_partials, ho);
     else
-        hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 1>), dim3(t16_blocks(b)), dim3(128 * kWaves), 0, s, queries,
-                           targets, b, n_total, loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, ho);
+        return hipErrorNotSupported;
     return hipGetLastError();
 }
 
