@@ -523,7 +523,7 @@ struct nrc_net {
         b.n_total = (int)n_total();
         b.slab_param = slab_param;
         b.n_slab = n_slab;
-        b.slab_closed = t16 && !hash();
+        b.slab_closed = t16 ? (hash() ? 2 : 1) : 0;
         return b;
     }
     GridBuffers grid_buffers() const {
@@ -696,19 +696,14 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
     const int blocks = train_block_count(net, b);
     net->ensure_slabs(blocks);
     if (net->hash()) {
-        // training kernel + grid scatter, then both optimizer updates: one launch for the t16 slabs (launch_hash_adam;
-        // a second stream for the MLP update measured slower: each cross-stream event added ~6 us of idle GPU)
+        // training kernel + grid scatter, then the MLP and grid optimizer updates (a second stream for the MLP update, beside
+        // the scatter, measured slower: each cross-stream event added ~6 us of idle GPU; one launch holding both updates
+        // as noinline halves ran 75 us)
         train_hash(net, in, tgt, b, 3.0f * (float)b, blocks);
         net->step += 1;
-        float* const ld = loss_d ? loss_d : net->loss_dev;
-        if (net->t16) {
-            HIP_CHECK(launch_hash_adam(net->slabs, blocks, net->loss_partials, ld, net->buffers(), net->grid_buffers(),
-                                       net->optim(net->step), net->stream));
-        } else {
-            HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr, ld, net->buffers(),
-                                         net->optim(net->step), net->stream));
-            HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
-        }
+        HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
+                                     loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
+        HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
         if (loss_h) *loss_h = net->read_loss();
         return;
     }
@@ -1075,9 +1070,9 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
         HIP_CHECK(hipMemcpy(net->bwd_pos, bwd.data(), sizeof(int) * net->n_mlp, hipMemcpyHostToDevice));
         {
             const std::vector<int> sm = net->t16 ? build_t16_slab_map(net->encoding) : build_slab_map(net->encoding);
-            if (net->t16 && !net->hash())  // the reduction maps Frequency t16 slab positions in closed form (t16_slab_param)
+            if (net->t16)  // the reduction maps t16 slab positions in closed form (t16_slab_param, t16_hash_slab_param)
                 for (size_t i = 0; i < sm.size(); ++i)
-                    if (sm[i] != t16_slab_param((int)i))
+                    if (sm[i] != (net->hash() ? t16_hash_slab_param((int)i) : t16_slab_param((int)i)))
                         throw ApiError(NRC_ERR_INTERNAL, "t16_slab_param disagrees with the slab map at " + std::to_string(i));
             net->n_slab = (int)sm.size();
             HIP_CHECK(hipMalloc(&net->slab_param, sizeof(int) * sm.size()));

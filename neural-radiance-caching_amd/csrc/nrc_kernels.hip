@@ -2508,7 +2508,7 @@ __device__ __forceinline__ void reduce_adam_body(const int blk, int mode, const 
         // through the map (one branch-free load, every thread)
         const int mypos = blk * kRedParams * kRedVec + (threadIdx.x & (kRedParams * kRedVec - 1));
         int pp_raw;
-        if constexpr (H) pp_raw = mb.slab_closed ? t16_slab_param(mypos) : mb.slab_param[mypos];
+        if constexpr (H) pp_raw = mb.slab_closed == 2 ? t16_hash_slab_param(mypos) : t16_slab_param(mypos);
         else pp_raw = mb.slab_param[mypos];
         f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         auto ld = [&](int slab) -> f4 {
@@ -3750,41 +3750,6 @@ __device__ __forceinline__ void grid_adam_body(const int blk, int mode, const Gr
 
 __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
     grid_adam_body(blockIdx.x, mode, gb, oa, ema_debias);
-}
-
-// The Hash training step's two optimizer updates in one launch (round 5): blocks [0, nred) reduce the MLP's f16 slabs and
-// apply its Adam/EMA (reduce_adam_kernel<true>, kReduceFused), the rest step the grid (grid_adam_kernel, kReduceFused).
-// They touch disjoint state; the latency-bound slab reduction runs beside the grid's HBM streaming instead of behind
-// it, and the step has one kernel boundary fewer.
-// (the two halves as separate functions: inlined into one body the compiler wraps both in one loop region, which the
-// scalar-branch-load + masked-store rule of tools/asm_hazard_check.py rejects)
-__device__ __attribute__((noinline)) void hash_adam_mlp(int blk, const float* slabs, int nslabs, const float* loss_partials,
-                                                        float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
-                                                        float lr_t, float ema_debias) {
-    reduce_adam_body<true>(blk, kReduceFused, slabs, nslabs, loss_partials, nullptr, loss_out, mb, oa, lr_t, ema_debias);
-}
-__device__ __attribute__((noinline)) void hash_adam_grid(int blk, const GridBuffers& gb, const OptimArgs& oa,
-                                                         float ema_debias) {
-    grid_adam_body(blk, kReduceFused, gb, oa, ema_debias);
-}
-__global__ __launch_bounds__(256) void hash_adam_kernel(int nred, const float* __restrict__ slabs, int nslabs,
-                                                        const float* __restrict__ loss_partials, float* __restrict__ loss_out,
-                                                        ModelBuffers mb, GridBuffers gb, OptimArgs oa, float lr_t,
-                                                        float ema_debias) {
-    if ((int)blockIdx.x < nred) hash_adam_mlp(blockIdx.x, slabs, nslabs, loss_partials, loss_out, mb, oa, lr_t, ema_debias);
-    else hash_adam_grid((int)blockIdx.x - nred, gb, oa, ema_debias);
-}
-
-hipError_t launch_hash_adam(const float* slabs, int nslabs, const float* loss_partials, float* loss_out,
-                            const ModelBuffers& mb, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s) {
-    if (!mb.slab_f16 || nslabs < 1) return hipErrorInvalidValue;
-    static_assert(kRedThreads == 256, "one block shape for both halves");
-    float lr_t, ema_debias;
-    adam_host_factors(oa, lr_t, ema_debias);
-    const int nred = mb.n_slab / (kRedParams * kRedVec);
-    hipLaunchKernelGGL(hash_adam_kernel, dim3((unsigned)(nred + (gb.n + 255) / 256)), dim3(256), 0, s, nred, slabs, nslabs,
-                       loss_partials, loss_out, mb, gb, oa, lr_t, ema_debias);
-    return hipGetLastError();
 }
 
 hipError_t launch_grid_adam(int mode, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s) {
