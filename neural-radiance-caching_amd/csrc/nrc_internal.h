@@ -70,17 +70,6 @@ __host__ __device__ constexpr int t16_hash_slot_feature(int K) {
 }
 static_assert(t16_hash_slot_feature(13) == 13 && t16_hash_slot_feature(32 + 1) == 56 && t16_hash_slot_feature(32 + 4) == 32,
               "t16 Hash slot map");
-__host__ __device__ constexpr int t16_hash_slab_param(int pos) {
-    const int L = pos < 6144 ? 0 : pos < 22528 ? 1 + (pos - 6144) / 4096 : 5;
-    const int off = pos - (L == 0 ? 0 : L <= 4 ? 6144 + (L - 1) * 4096 : 22528);
-    const int ntn = t16_ntn(L), rec = off >> 9, q = off & 511, lane = q >> 3, e = q & 7;
-    const int tm = rec / (ntn >> 1), tn = 2 * (rec % (ntn >> 1)) + (e >> 2);
-    const int row = 16 * tm + 4 * (lane >> 4) + (e & 3), col = 16 * tn + (lane & 15);
-    const int f = L == 0 ? t16_hash_slot_feature(col) : col;
-    const int in_dim = L == 0 ? NRC_HASH_ENC_WIDTH : 64;
-    const int loff = L == 0 ? NRC_HASH_W0_OFFSET : L <= 4 ? NRC_HASH_W1_OFFSET + (L - 1) * 4096 : NRC_HASH_W5_OFFSET;
-    return f < 0 ? -1 : loff + row * in_dim + f;
-}
 // Hash backward image in the t16 layout: the 36 fragments of W_l^T, then W0^T restricted to the 32 grid features as
 // 16x16x32 A operands: fragment 36 + 2 mb + s holds rows (grid slots) 16 mb .. 16 mb + 15, k-step s of delta_0's rows
 constexpr int kT16BwdFragsHash = kT16BwdFrags + 4;
@@ -114,8 +103,18 @@ __host__ __device__ constexpr int t16_slab_param(int pos) {
 static_assert(t16_slab_param(t16_slab_pos(3, 2, 1, 37, 2)) == NRC_W1_OFFSET + 2 * 4096 + (32 + 4 * 2 + 2) * 64 + 16 + 5,
               "t16 slab inverse");
 // The same inverse for InputEncoding::Hash's t16 slabs (round 5): t16_hash_slot_feature, in_dim 64, the Hash layer
-// offsets (checked against build_t16_slab_map at nrc_init). Defined after t16_hash_slot_feature below.
-__host__ __device__ constexpr int t16_hash_slab_param(int pos);
+// offsets (checked against build_t16_slab_map at nrc_init).
+__host__ __device__ constexpr int t16_hash_slab_param(int pos) {
+    const int L = pos < 6144 ? 0 : pos < 22528 ? 1 + (pos - 6144) / 4096 : 5;
+    const int off = pos - (L == 0 ? 0 : L <= 4 ? 6144 + (L - 1) * 4096 : 22528);
+    const int ntn = t16_ntn(L), rec = off >> 9, q = off & 511, lane = q >> 3, e = q & 7;
+    const int tm = rec / (ntn >> 1), tn = 2 * (rec % (ntn >> 1)) + (e >> 2);
+    const int row = 16 * tm + 4 * (lane >> 4) + (e & 3), col = 16 * tn + (lane & 15);
+    const int f = L == 0 ? t16_hash_slot_feature(col) : col;
+    const int in_dim = L == 0 ? NRC_HASH_ENC_WIDTH : 64;
+    const int loff = L == 0 ? NRC_HASH_W0_OFFSET : L <= 4 ? NRC_HASH_W1_OFFSET + (L - 1) * 4096 : NRC_HASH_W5_OFFSET;
+    return f < 0 ? -1 : loff + row * in_dim + f;
+}
 
 // Gradient exchange buffer: loss-scaled dL/dW (NRC_NUM_PARAMS f32) followed by the minibatch loss.
 
