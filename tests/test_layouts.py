@@ -129,3 +129,20 @@ def test_t16_transposed_reads_are_conflict_free():
                             a = off(32 * kk + 8 * G + 4 * second + q, 4 * t + p)
                             banks += [(a // 4) % 64, (a // 4 + 1) % 64]
                         assert len(set(banks)) == 64, (off.__name__, t, kk, second, half)
+
+
+def test_t16_slot_and_slab_maps_host_check(tmp_path):
+    """tests/cpp/t16_maps_check.cpp compiled for the host against csrc/nrc_internal.h: the t16 layer-0 slot maps
+    (Frequency, Hash) put every canonical feature in exactly one K slot, the closed-form slab inverses reach every MLP
+    parameter exactly once, and the Hash W0^T fragments do not collide (no GPU needed)."""
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "t16_maps_check"
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O1", f"-I{root / 'include'}",
+                        f"-I{root / 'neural-radiance-caching_amd' / 'csrc'}", str(root / "tests" / "cpp" / "t16_maps_check.cpp"),
+                        "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and "t16 maps OK" in out.stdout, out.stdout + out.stderr
