@@ -223,10 +223,11 @@ nrc_status nrc_get_step(const nrc_net* net, uint32_t* step);
 nrc_status nrc_set_step(nrc_net* net, uint32_t step);
 
 /* ---- test / tuning entries ---- */
-/* Process-wide A/B knobs (the library reads no environment variables): "train_kernel" (Frequency training kernel at
- * nrc_init: -1/0 decoupled chain, 1 / 2 round-2 t16 role-split / 4-wave, 32 round-1 32x32x16), "train_shape" (decoupled
- * chain block shape 0..7, -1 = by batch size), "scatter_min" / "scatter_max" (Hash grid-scatter slice plan), "hash_infer"
- * (Hash inference: 1 = the round-2 gather kernel instead of the LDS-table feature pass), "t16_groups" (1 = 64-sample blocks
+/* Process-wide A/B knobs (the library reads no environment variables): "train_kernel" (training kernel at nrc_init:
+ * Frequency -1/0 decoupled chain, 1 / 2 round-2 t16 role-split / 4-wave; 32 the round-1 32x32x16 kernel, for Frequency
+ * and Hash), "train_shape" (decoupled chain block shape 0..7, -1 = by batch size), "scatter_min" / "scatter_max" (Hash
+ * grid-scatter slice plan), "hash_infer" (Hash: 1 = gather the table entries per query -- the round-2 inference kernel
+ * and, in training, the t16 kernel's gathering encoder -- instead of the LDS-table feature pass), "t16_groups" (1 = 64-sample blocks
  * of the role-split kernel, debug library), "peer_path" (nrc_train_dp over a peer exchange: 0 reduce / push / apply
  * launches, 1 fused, 2 split; tests: 3 the split form's gradient pass + push alone, 4 its wait + sum + Adam alone),
  * "px_polls" (bound of the exchange's wait loops, -1 = 2^21 polls, about 10 s); debug library only: "dc_dw0_delay",
