@@ -620,23 +620,6 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
         else hash_corners_lds<kDense>(p.x, p.y, p.z, level, C);
     };
     auto gather = [&](const LdsCorners& C, uint32_t (&v)[8]) {
-        if constexpr ((ABL & 128) != 0) {
-            // round-5 A/B: corners 2p, 2p + 1 differ only in x; for an even cell x their entries share an aligned 8-byte
-            // slot (offsets differ in bit 2 only, hashed and dense alike), so one ds_read_b64 serves both, and the
-            // partner's own 4-byte read goes to entry 0 (a broadcast) unless it lies elsewhere
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const uint32_t o0 = C.off[2 * p], o1 = C.off[2 * p + 1];
-                const bool same = (o0 ^ o1) == 4u;
-                typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-                const u2v pr = *reinterpret_cast<const u2v*>(ltb + (o0 & ~7u));
-                const uint32_t far = *reinterpret_cast<const uint32_t*>(ltb + (same ? 0u : o1));
-                const bool odd = (o0 & 4u) != 0u;
-                v[2 * p] = odd ? pr.y : pr.x;
-                v[2 * p + 1] = same ? (odd ? pr.x : pr.y) : far;
-            }
-            return;
-        }
 #pragma unroll
         for (int c = 0; c < 8; ++c) v[c] = (ABL & 1) ? C.off[c] : *reinterpret_cast<const uint32_t*>(ltb + C.off[c]);
     };
@@ -3219,7 +3202,6 @@ static void launch_hash_feature_pass(const float* qc0, int64_t cnt, const uint32
                  : fa == 32 ? hash_feature_kernel<32>  // no position loads, scattered positions
                  : fa == 33 ? hash_feature_kernel<33>  // 32 without the gathers
                  : fa == 36 ? hash_feature_kernel<36>  // 32 without the stores
-                 : fa == 128 ? hash_feature_kernel<128>  // round 5: paired 8-byte corner reads (A/B)
                            : hash_feature_kernel<7>;
         hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
         return;
@@ -3927,7 +3909,9 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
         // the batch's level features first, one level table per block in LDS (hash_feature_kernel, as for inference):
         // the training kernel's 128 blocks would otherwise gather 2 M table entries at their CUs' L1 line rate
         const bool fp = feat && b <= kHashFeatStride;
-        if (fp) launch_hash_feature_pass(queries, b, g, feat, padq, s, b >= 8192 ? 16 : 8);
+        // P = 8 query ranges per level (the minimum of the kernel's block map): 16,384-sample step 63.7 us vs 63.9 (16)
+        // and 67.8 (32), profiles/r05_hash/
+        if (fp) launch_hash_feature_pass(queries, b, g, feat, padq, s, 8);
         const hipError_t e = launch_train16_hash(queries, targets, b, n_total, loss_scale, wf, wb,
                                                  reinterpret_cast<_Float16*>(slabs), loss_partials,
                                                  HashTrainOut{g, fp ? feat : nullptr, sc->pos, sc->dy, bcap}, s, padq);

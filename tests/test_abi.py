@@ -74,7 +74,7 @@ def test_knob_values_are_range_checked(nrc):
     zero (SIGFPE). Out-of-range values are NRC_ERR_INVALID_ARGUMENT now and leave the knob unchanged (no GPU needed)."""
     L = nrc._lib
     bad = {"train_shape": [8, 100, -2], "train_kernel": [3, 31, 33, -5], "t16_groups": [0, 3], "hash_infer": [2, -2],
-           "scatter_min": [0, 15, 1 << 21], "scatter_max": [7], "hash_feat_abl": [37, 127, 129], "dc_dw0_delay": [-2, 1 << 21],
+           "scatter_min": [0, 15, 1 << 21], "scatter_max": [7], "hash_feat_abl": [37, 128], "dc_dw0_delay": [-2, 1 << 21],
            "hash_feat_p": [0, 12, 264], "peer_path": [5, -2], "px_polls": [0, -2, (1 << 21) + 1]}
     for name, values in bad.items():
         before = L.get_knob(name)
