@@ -263,11 +263,11 @@ bool want_t16(int encoding) {
     return encoding == NRC_ENCODING_FREQUENCY || encoding == NRC_ENCODING_HASH;
 }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
                                             "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path",
-                                            "px_polls"};
-static_assert(kKnobCount == 11, "one initial value and one name per knob");
+                                            "px_polls", "scatter_part"};
+static_assert(kKnobCount == 12, "one initial value and one name per knob");
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -435,15 +435,32 @@ struct nrc_net {
     }
     HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
     int scatter_blocks = 0;
+    int64_t* scatter_part = nullptr;  // per-slice partial sums of the fused step's fine levels (ScatterPartials)
+    int64_t scatter_part_words = 0;
+    // the partial layout of a fused b-sample step (knob scatter_part: first level with partials), buffer grown to fit
+    ScatterPartials step_partials(uint32_t b) {
+        const int k = knob(kKnobScatterPart);
+        ScatterPartials p = scatter_partials_layout(b, k >= 0 ? k : kScatterPartFirst);
+        if (p.total > scatter_part_words) {
+            if (scatter_part) HIP_CHECK(hipFree(scatter_part));
+            scatter_part = nullptr;
+            scatter_part_words = 0;
+            HIP_CHECK(hipMalloc(&scatter_part, sizeof(int64_t) * (size_t)p.total));
+            scatter_part_words = p.total;
+        }
+        if (p.total) p.base = scatter_part;
+        return p;
+    }
     uint8_t* grid_nf = nullptr;       // [n_grid] non-finite contribution codes (GridNonFinite)
     uint32_t* grid_nf_tag = nullptr;  // tag of the last scatter that recorded one
     uint32_t nf_seq = 0;              // tag of the current step's scatter
     GridNonFinite nonfinite() const { return GridNonFinite{grid_nf, grid_nf_tag, nf_seq}; }
     // the scatter workspace for a new training step (a fresh non-finite tag)
-    const HashScatter* step_scatter(int blocks) {
+    const HashScatter* step_scatter(int blocks, const ScatterPartials& part) {
         ensure_scatter(blocks);
         nf_seq = nf_seq + 1u ? nf_seq + 1u : 1u;
         scatter.nf = nonfinite();
+        scatter.part = part;
         return &scatter;
     }
 
@@ -487,8 +504,10 @@ struct nrc_net {
         f(grid_nf); f(grid_nf_tag);
         grid_nf = nullptr;
         grid_nf_tag = nullptr;
-        f(scatter.pos); f(scatter.dy);
+        f(scatter.pos); f(scatter.dy); f(scatter_part);
         scatter = HashScatter{};
+        scatter_part = nullptr;
+        scatter_part_words = 0;
         scatter_blocks = 0;
         f(wide_img16); f(wide_img8); f(wide_scales);
         f(wide_fwd_train); f(wide_bwd_train); f(wide_ws_in); f(wide_ws_d); f(wide_slabs); f(wide_loss_partials);
@@ -526,8 +545,9 @@ struct nrc_net {
         b.slab_closed = t16 ? (hash() ? 2 : 1) : 0;
         return b;
     }
-    GridBuffers grid_buffers() const {
+    GridBuffers grid_buffers(const ScatterPartials& part = ScatterPartials{}) const {
         GridBuffers g;
+        g.part = part;
         g.params = params + n_mlp; g.m = m + n_mlp; g.v = v + n_mlp; g.ema = ema + n_mlp; g.infer = infer + n_mlp;
         g.grad64 = grid_grad; g.grad32 = nullptr; g.fixed = nullptr; g.steps = grid_steps;
         g.nf = nonfinite();
@@ -669,12 +689,14 @@ void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b,
 // Hash fwd + loss + bwd + dW slabs + grid scatter of b samples (n_total = 3 x global batch). The t16 kernel reads the
 // batch's level features from the handle's feature workspace (shared with inference: the event protocol of
 // hash_feat_acquire / _release orders them across streams); knob hash_infer = 1 keeps the gathering encoder (A/B).
-void train_hash(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total, int blocks) {
+// part: the fused step's partial sums (do_train; the next grid_adam_kernel consumes them), else none (grad64 only).
+void train_hash(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total, int blocks,
+                const ScatterPartials& part = ScatterPartials{}) {
     uint32_t* const feat = net->t16 && knob(kKnobHashInfer) != 1 ? net->hash_feat : nullptr;
     if (feat) net->hash_feat_acquire(net->stream);
     HIP_CHECK(launch_train_hash(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train, net->table_train,
-                                net->grid_grad, net->slabs, net->loss_partials, net->stream, net->step_scatter(blocks),
-                                net->padq(), net->t16, feat));
+                                net->grid_grad, net->slabs, net->loss_partials, net->stream,
+                                net->step_scatter(blocks, part), net->padq(), net->t16, feat));
     if (feat) net->hash_feat_release(net->stream);
 }
 
@@ -699,11 +721,13 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
         // training kernel + grid scatter, then the MLP and grid optimizer updates (a second stream for the MLP update, beside
         // the scatter, measured slower: each cross-stream event added ~6 us of idle GPU; one launch holding both updates
         // as noinline halves ran 75 us)
-        train_hash(net, in, tgt, b, 3.0f * (float)b, blocks);
+        // the fine levels' scatter stores per-slice partials that the grid update sums (no memory-side atomics)
+        const ScatterPartials part = net->step_partials(b);
+        train_hash(net, in, tgt, b, 3.0f * (float)b, blocks, part);
         net->step += 1;
         HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
                                      loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
-        HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(), net->optim(net->step), net->stream));
+        HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(part), net->optim(net->step), net->stream));
         if (loss_h) *loss_h = net->read_loss();
         return;
     }
@@ -867,6 +891,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobHashFeatP: return v == -1 || (v >= 8 && v <= 256 && v % 8 == 0);
         case kKnobPeerPath: return v >= -1 && v <= 4;
         case kKnobPxPolls: return v == -1 || (v >= 1 && v <= kPeerPolls);
+        case kKnobScatterPart: return v >= -1 && v <= NRC_HASH_LEVELS;
         default: return false;
     }
 }

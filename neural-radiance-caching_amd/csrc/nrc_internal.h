@@ -382,7 +382,8 @@ enum Knob : int {
                            // 2 split (reduce + push, then wait + sum + Adam); tests: 3 the split form's gradient pass +
                            // push alone (no optimizer step), 4 its wait + sum + Adam alone (the step the last 3 pushed)
     kKnobPxPolls = 10,     // bound of the peer exchange's wait loops (-1 = kPeerPolls, about 10 s; 1..2^21)
-    kKnobCount = 11
+    kKnobScatterPart = 11, // Hash training: first grid level whose scatter stores per-slice partials (-1 default, 0..16)
+    kKnobCount = 12
 };
 int knob(Knob k);
 
@@ -398,8 +399,24 @@ struct GridNonFinite {
     uint32_t tag = 0;
 };
 // HashGrid parameters (the grid part of the model arrays) and their optimizer state
+// Per-slice partial sums of the grid scatter (round 5): level l's nslice[l] sample slices x its entries x 2 features,
+// int64 fixed point, at base + off[l]; every scatter block of such a level stores its part of one slice densely (plain
+// stores, no global atomics), and grid_adam_kernel sums the slices in slice order. Levels with nslice 0 (the coarse
+// ones: few entries touched, so dense stores would be mostly zeros) and every level when base is null add into grad64
+// with global atomics instead (the data-parallel exports read grad64).
+struct ScatterPartials {
+    int64_t* base = nullptr;
+    int64_t off[NRC_HASH_LEVELS] = {};
+    int nslice[NRC_HASH_LEVELS] = {};
+    int64_t total = 0;  // int64 words of the layout
+};
+// the layout of a b-sample step under the current scatter plan (knobs scatter_min / scatter_max), partial sums for
+// levels first_level.. (nslice 0 below: those levels flush into grad64 with atomics; total 0 when first_level = 16)
+ScatterPartials scatter_partials_layout(int64_t b, int first_level);
+constexpr int kScatterPartFirst = 4;  // default first level (knob scatter_part)
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
+    ScatterPartials part;  // kReduceFused: the step's partial sums when part.base is set (else grad64)
     int64_t* grad64;      // [n] exact fixed-point sums (value x 2^24) of the f16 contributions, accumulated by
                           // grid_scatter_kernel, rounded to f16 and zeroed by grid_adam_kernel
     const float* grad32;  // kApplyOnly: the all-reduced data-parallel gradient (f32 [n], read-only)
@@ -424,6 +441,7 @@ struct HashScatter {
     uint32_t* dy;  // [NRC_HASH_LEVELS][bcap]
     int64_t bcap;
     GridNonFinite nf;
+    ScatterPartials part;  // base set: flush into per-slice partials (plain stores) instead of grad64 (atomics)
 };
 // Data-parallel exports of the grid accumulator (both zero it for the next step and consume the non-finite codes):
 // f32 -- each sum rounded to f16 (nrc_train_grad); fixed -- the exact sum in the exchange encoding below, for an int64

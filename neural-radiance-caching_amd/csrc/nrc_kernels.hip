@@ -3713,8 +3713,19 @@ __device__ __forceinline__ void grid_adam_body(const int blk, int mode, const Gr
             gradient = fixed_decode_gradient(gb.fixed[i]) / oa.loss_scale;
             if (gb.fixed == gb.grad64) gb.grad64[i] = 0;
         } else {
-            gradient = fixed_gradient(gb.grad64[i], take_nonfinite(gb.nf, i)) / oa.loss_scale;
-            gb.grad64[i] = 0;
+            // the step's exact sum: the level's per-slice partials (grid_scatter_kernel's plain-store levels, round 5)
+            // added in slice order, else the atomic accumulator (zeroed for the next step); exact int64 either way
+            const int l = i < 8192 ? 0 : 1 + ((i - 8192) >> 16);
+            int64_t sum = 0;
+            if (gb.part.base && gb.part.nslice[l]) {
+                const int j = i - (l == 0 ? 0 : 8192 + ((l - 1) << 16)), stride = l == 0 ? 8192 : 65536;
+                const int64_t* src = gb.part.base + gb.part.off[l] + j;
+                for (int sl = 0; sl < gb.part.nslice[l]; ++sl) sum += src[(int64_t)sl * stride];
+            } else {
+                sum = gb.grad64[i];
+                gb.grad64[i] = 0;
+            }
+            gradient = fixed_gradient(sum, take_nonfinite(gb.nf, i)) / oa.loss_scale;
         }
         if (gradient != 0.0f) {
             const uint32_t st = gb.steps[i] + 1u;
@@ -3824,7 +3835,7 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
                                                                        const uint32_t* __restrict__ dy, int64_t bcap,
                                                                        ScatterPlan plan,
                                                                        unsigned long long* __restrict__ grad,
-                                                                       GridNonFinite nf) {
+                                                                       GridNonFinite nf, ScatterPartials pt) {
     __shared__ unsigned long long acc[kScatterPart][2];  // 128 KiB: one block per CU
     int level = 0;
 #pragma unroll
@@ -3889,10 +3900,48 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
         load();
     }
     __syncthreads();
+    if (pt.base && pt.nslice[level]) {
+        // round 5, the fine levels (most entries touched): this block's part of its slice stored densely, zeros
+        // included, with plain 16-byte stores instead of memory-side atomics; grid_adam_kernel sums the slices
+        typedef long long i2v __attribute__((ext_vector_type(2)));
+        i2v* const dst = reinterpret_cast<i2v*>(pt.base + pt.off[level] + (int64_t)(local / nparts) * 2 * lsize) + e0;
+        for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads)
+            dst[i] = i2v{(long long)acc[i][0], (long long)acc[i][1]};
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < 2 * ne; i += kScatterThreads) {
         const unsigned long long v = acc[i >> 1][i & 1];
         if (v) __hip_atomic_fetch_add(grad + 2 * (uint64_t)(lbase + e0) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// the plan of launch_train_hash (slice per level: min(smax, smin << l)) and the partial-sum layout it implies
+static ScatterPlan scatter_plan(int64_t bcap, int& nb) {
+    const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);
+    const int smin = kmin > 0 ? kmin : 2048, smax = kmax > 0 ? kmax : 4096;
+    ScatterPlan plan;
+    nb = 0;
+    for (int l = 0; l < NRC_HASH_LEVELS; ++l) {
+        const int sl = (int)std::min<int64_t>((int64_t)smax, (int64_t)smin << l);
+        plan.first_block[l] = nb;
+        plan.slice[l] = sl;
+        nb += scatter_parts(l) * (int)((bcap + sl - 1) / sl);
+    }
+    plan.first_block[NRC_HASH_LEVELS] = nb;
+    return plan;
+}
+
+ScatterPartials scatter_partials_layout(int64_t b, int first_level) {
+    const int64_t bcap = (int64_t)train_blocks(b) * kTrainSamplesPerBlock;
+    int nb = 0;
+    const ScatterPlan plan = scatter_plan(bcap, nb);
+    ScatterPartials p;
+    for (int l = first_level; l < NRC_HASH_LEVELS; ++l) {
+        p.off[l] = p.total;
+        p.nslice[l] = (int)((bcap + plan.slice[l] - 1) / plan.slice[l]);
+        p.total += (int64_t)p.nslice[l] * 2 * (l == 0 ? 4096 : NRC_HASH_T);
+    }
+    return p;
 }
 
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
@@ -3927,19 +3976,17 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
                            bcap);
     // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep of the exact 64-bit scatter,
     // profiles/r03_hash/scatter_plan_sweep.txt (round 1's f16 scatter: profiles/r01_hash/README.md)
-    const int kmin = knob(kKnobScatterMin), kmax = knob(kKnobScatterMax);
-    const int smin = kmin > 0 ? kmin : 2048, smax = kmax > 0 ? kmax : 4096;
-    ScatterPlan plan;
     int nb = 0;
-    for (int l = 0; l < NRC_HASH_LEVELS; ++l) {
-        const int sl = (int)std::min<int64_t>((int64_t)smax, (int64_t)smin << l);
-        plan.first_block[l] = nb;
-        plan.slice[l] = sl;
-        nb += scatter_parts(l) * (int)((bcap + sl - 1) / sl);
+    const ScatterPlan plan = scatter_plan(bcap, nb);
+    if (sc->part.base) {  // the partial layout must be this plan's (levels without slices flush with atomics)
+        int first = 0;
+        while (first < NRC_HASH_LEVELS && !sc->part.nslice[first]) ++first;
+        const ScatterPartials want = scatter_partials_layout(b, first);
+        for (int l = 0; l < NRC_HASH_LEVELS; ++l)
+            if (want.off[l] != sc->part.off[l] || want.nslice[l] != sc->part.nslice[l]) return hipErrorInvalidValue;
     }
-    plan.first_block[NRC_HASH_LEVELS] = nb;
     hipLaunchKernelGGL(grid_scatter_kernel, dim3(nb), dim3(kScatterThreads), 0, s, sc->pos, sc->dy, bcap, plan,
-                       reinterpret_cast<unsigned long long*>(grid_grad), sc->nf);
+                       reinterpret_cast<unsigned long long*>(grid_grad), sc->nf, sc->part);
     return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #   tools/gpu_round.sh energy <variants> [rounds]                 J/query A/B of inference variants (debug library)
 #   tools/gpu_round.sh power [power_paths.py args...]             power / clock / nJ per query of the product paths
 #   tools/gpu_round.sh hash-abl <knob values> [knob]              Hash feature-pass A/B over a knob (tools/ab_hash_p.py)
+#   tools/gpu_round.sh hash-train-ab [values] [knob]              fused Hash training step A/B (tools/ab_hash_train.py)
 #   tools/gpu_round.sh pmc-hash                                   PMC + kernel trace of tools/bench_hash.py
 #   tools/gpu_round.sh dp-timing                                  2-rank DP timing (tools/gpu_dp_timing.sh)
 #   tools/gpu_round.sh rehearse-dp2                               2 ranks on one GPU through bench.py (tools/rehearse_dp2.sh)
@@ -84,6 +85,11 @@ hash-abl)
   values=$1 knob=${2:-hash_feat_abl}
   NRC_LIB_PATH="$DEBUG_LIB" timeout -k 10 300 python tools/ab_hash_p.py --knob "$knob" --ps="$values" --rounds 5 > gpurun_out/ab_hash.json 2> gpurun_out/ab_hash.err || { echo "hash A/B failed"; tail -20 gpurun_out/ab_hash.err; exit 4; }
   cat gpurun_out/ab_hash.json
+  ;;
+hash-train-ab)
+  values=${1:-16,0,2,4,6,8} knob=${2:-scatter_part}
+  timeout -k 10 300 python tools/ab_hash_train.py --knob "$knob" --values "$values" > gpurun_out/ab_hash_train.json 2> gpurun_out/ab_hash_train.err || { echo "hash train A/B failed"; tail -20 gpurun_out/ab_hash_train.err; exit 4; }
+  cat gpurun_out/ab_hash_train.json
   ;;
 pmc-hash)
   bash tools/gpu_pmc.sh pmc_hash python3 "$ROOT/tools/bench_hash.py" --iters 5 || exit 6
