@@ -413,7 +413,9 @@ struct ScatterPartials {
 // the layout of a b-sample step under the current scatter plan (knobs scatter_min / scatter_max), partial sums for
 // levels first_level.. (nslice 0 below: those levels flush into grad64 with atomics; total 0 when first_level = 16)
 ScatterPartials scatter_partials_layout(int64_t b, int first_level);
-constexpr int kScatterPartFirst = 4;  // default first level (knob scatter_part)
+// default first level (knob scatter_part): fused step 63.0 us all-atomic, 58.3 / 57.6 / 57.4 / 56.5 / 57.2 from level
+// 0 / 2 / 4 / 6 / 8 (profiles/r05_hash/ab_scatter_part.json, parameters bitwise equal)
+constexpr int kScatterPartFirst = 6;
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
     ScatterPartials part;  // kReduceFused: the step's partial sums when part.base is set (else grad64)

@@ -25,10 +25,14 @@ def main() -> None:
     ap.add_argument("--values", default="16,0,2,4,6,8")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--set", action="append", default=[], help="name=value knob held for the whole run")
     args = ap.parse_args()
     import torch
 
     nrc = nrc_loader.load()
+    for kv in args.set:
+        k, v = kv.split("=")
+        nrc._lib.set_knob(k, int(v))
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     vals = [int(v) for v in args.values.split(",")]
@@ -68,7 +72,7 @@ def main() -> None:
         equal[v] = equal[v] and bool(np.array_equal(nets[v].get_state(nrc.StateSlot.PARAMS), p1))
     res = {v: {"median_us": float(np.median(times[v])), "min_us": float(np.min(times[v])),
                "params_bitwise_equal_to_first": equal[v]} for v in vals}
-    print(json.dumps({"knob": args.knob, "batch": B, "by_value": res}))
+    print(json.dumps({"knob": args.knob, "held": args.set, "batch": B, "by_value": res}))
     for n in nets.values():
         n.destroy()
 

@@ -12,7 +12,7 @@
 #   tools/gpu_round.sh energy <variants> [rounds]                 J/query A/B of inference variants (debug library)
 #   tools/gpu_round.sh power [power_paths.py args...]             power / clock / nJ per query of the product paths
 #   tools/gpu_round.sh hash-abl <knob values> [knob]              Hash feature-pass A/B over a knob (tools/ab_hash_p.py)
-#   tools/gpu_round.sh hash-train-ab [values] [knob]              fused Hash training step A/B (tools/ab_hash_train.py)
+#   tools/gpu_round.sh hash-train-ab [values] [knob] [tag] [k=v...] fused Hash training step A/B (tools/ab_hash_train.py)
 #   tools/gpu_round.sh pmc-hash                                   PMC + kernel trace of tools/bench_hash.py
 #   tools/gpu_round.sh dp-timing                                  2-rank DP timing (tools/gpu_dp_timing.sh)
 #   tools/gpu_round.sh rehearse-dp2                               2 ranks on one GPU through bench.py (tools/rehearse_dp2.sh)
@@ -87,9 +87,10 @@ hash-abl)
   cat gpurun_out/ab_hash.json
   ;;
 hash-train-ab)
-  values=${1:-16,0,2,4,6,8} knob=${2:-scatter_part}
-  timeout -k 10 300 python tools/ab_hash_train.py --knob "$knob" --values "$values" > gpurun_out/ab_hash_train.json 2> gpurun_out/ab_hash_train.err || { echo "hash train A/B failed"; tail -20 gpurun_out/ab_hash_train.err; exit 4; }
-  cat gpurun_out/ab_hash_train.json
+  values=${1:-16,0,2,4,6,8} knob=${2:-scatter_part} tag=${3:-0}; shift $(( $# < 3 ? $# : 3 ))
+  held=(); for kv in "$@"; do held+=(--set "$kv"); done
+  timeout -k 10 300 python tools/ab_hash_train.py --knob "$knob" --values "$values" "${held[@]}" > "gpurun_out/ab_hash_train_$tag.json" 2> "gpurun_out/ab_hash_train_$tag.err" || { echo "hash train A/B failed"; tail -20 "gpurun_out/ab_hash_train_$tag.err"; exit 4; }
+  cat "gpurun_out/ab_hash_train_$tag.json"
   ;;
 pmc-hash)
   bash tools/gpu_pmc.sh pmc_hash python3 "$ROOT/tools/bench_hash.py" --iters 5 || exit 6
