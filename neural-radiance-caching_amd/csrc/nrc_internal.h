@@ -383,7 +383,8 @@ enum Knob : int {
                            // push alone (no optimizer step), 4 its wait + sum + Adam alone (the step the last 3 pushed)
     kKnobPxPolls = 10,     // bound of the peer exchange's wait loops (-1 = kPeerPolls, about 10 s; 1..2^21)
     kKnobScatterPart = 11, // Hash training: first grid level whose scatter stores per-slice partials (-1 default, 0..16)
-    kKnobCount = 12
+    kKnobScatterCompact = 12, // Hash training: first grid level whose scatter queues its in-part corners (-1 default, 0..16)
+    kKnobCount = 13
 };
 int knob(Knob k);
 
@@ -416,6 +417,9 @@ ScatterPartials scatter_partials_layout(int64_t b, int first_level);
 // default first level (knob scatter_part): fused step 63.0 us all-atomic, 58.3 / 57.6 / 57.4 / 56.5 / 57.2 from level
 // 0 / 2 / 4 / 6 / 8 (profiles/r05_hash/ab_scatter_part.json, parameters bitwise equal)
 constexpr int kScatterPartFirst = 6;
+// default first level of the corner queue (knob scatter_compact): step 57.3 us without, 56.0 from level 4, 55.8 from
+// level 10 (profiles/r05_hash/ab_scatter_compact_repeat.json, 12 interleaved rounds x 2)
+constexpr int kScatterCompactFirst = 10;
 struct GridBuffers {
     float *params, *m, *v, *ema, *infer;
     ScatterPartials part;  // kReduceFused: the step's partial sums when part.base is set (else grad64)

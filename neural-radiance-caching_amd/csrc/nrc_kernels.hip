@@ -3697,15 +3697,64 @@ __device__ __forceinline__ float fixed_decode_gradient(int64_t e) {
     return fixed_gradient((int64_t)(u & ((1ull << 48) - 1)) - kFixedOff, code);
 }
 
+// tcnn's grid Adam for parameter i with this step's gradient (already divided by the loss scale): an exactly-zero
+// gradient keeps moments, weight and the entry's own step counter (no l2); the EMA over every entry, and the two f16
+// tables repacked. The state is loaded first and unconditionally (grid_adam_load: the moments of an untouched entry too),
+// so that every load of a parameter is in flight before its gradient is known and before any store (the conditional
+// loads after the gradient made grid_adam_kernel a chain of memory round trips per parameter; measured neutral, 56.2 vs
+// 56.5 us per Hash step).
+struct GridAdamIn {
+    float w, m, v, e;
+    uint32_t st;
+};
+__device__ __forceinline__ GridAdamIn grid_adam_load(int i, const GridBuffers& gb) {
+    return GridAdamIn{gb.params[i], gb.m[i], gb.v[i], gb.ema[i], gb.steps[i]};
+}
+__device__ __forceinline__ void grid_adam_step(int i, float gradient, const GridAdamIn& a, const GridBuffers& gb,
+                                               const OptimArgs& oa, float ema_debias) {
+#pragma clang fp contract(off)
+    float w = a.w;
+    if (gradient != 0.0f) {
+        const uint32_t st = a.st + 1u;
+        gb.steps[i] = st;
+        // two powf per parameter made this kernel VALU-bound (~12 us per step): table lookup instead
+        float s2, d1;
+        if (st <= gb.bias_len) {
+            const float2 bc = gb.bias[st];
+            s2 = bc.x;
+            d1 = bc.y;
+        } else {
+            s2 = sqrtf(1.0f - powf(oa.beta2, (float)st));
+            d1 = 1.0f - powf(oa.beta1, (float)st);
+        }
+        const float lr_i = oa.lr * s2 / d1;
+        const float gsq = gradient * gradient;
+        const float m1 = oa.beta1 * a.m + (1.0f - oa.beta1) * gradient;
+        const float v1 = oa.beta2 * a.v + (1.0f - oa.beta2) * gsq;
+        gb.m[i] = m1;
+        gb.v[i] = v1;
+        const float eff = lr_i / (sqrtf(v1) + oa.eps);
+        w = w - eff * m1;
+        gb.params[i] = w;
+    }
+    const float e = a.e * oa.ema_decay + w * (1.0f - oa.ema_decay);
+    gb.ema[i] = e;
+    const float inf = e / ema_debias;
+    gb.infer[i] = inf;
+    gb.table_train[i] = (_Float16)w;
+    gb.table_infer[i] = (_Float16)inf;
+}
+
 __device__ __forceinline__ void grid_adam_body(const int blk, int mode, const GridBuffers& gb, const OptimArgs& oa,
                                                float ema_debias) {
 #pragma clang fp contract(off)
     const int i = blk * 256 + threadIdx.x;
     if (i >= gb.n) return;
-    float w = gb.params[i], inf;
     if (mode == kPackOnly) {
-        inf = gb.infer[i];
+        gb.table_train[i] = (_Float16)gb.params[i];
+        gb.table_infer[i] = (_Float16)gb.infer[i];
     } else {
+        const GridAdamIn a = grid_adam_load(i, gb);
         float gradient;
         if (mode == kApplyOnly) {
             gradient = gb.grad32[i] / oa.loss_scale;
@@ -3727,36 +3776,8 @@ __device__ __forceinline__ void grid_adam_body(const int blk, int mode, const Gr
             }
             gradient = fixed_gradient(sum, take_nonfinite(gb.nf, i)) / oa.loss_scale;
         }
-        if (gradient != 0.0f) {
-            const uint32_t st = gb.steps[i] + 1u;
-            gb.steps[i] = st;
-            // two powf per parameter made this kernel VALU-bound (~12 us per step): table lookup instead
-            float s2, d1;
-            if (st <= gb.bias_len) {
-                const float2 bc = gb.bias[st];
-                s2 = bc.x;
-                d1 = bc.y;
-            } else {
-                s2 = sqrtf(1.0f - powf(oa.beta2, (float)st));
-                d1 = 1.0f - powf(oa.beta1, (float)st);
-            }
-            const float lr_i = oa.lr * s2 / d1;
-            const float gsq = gradient * gradient;
-            const float m1 = oa.beta1 * gb.m[i] + (1.0f - oa.beta1) * gradient;
-            const float v1 = oa.beta2 * gb.v[i] + (1.0f - oa.beta2) * gsq;
-            gb.m[i] = m1;
-            gb.v[i] = v1;
-            const float eff = lr_i / (sqrtf(v1) + oa.eps);
-            w = w - eff * m1;
-            gb.params[i] = w;
-        }
-        const float e = gb.ema[i] * oa.ema_decay + w * (1.0f - oa.ema_decay);
-        gb.ema[i] = e;
-        inf = e / ema_debias;
-        gb.infer[i] = inf;
+        grid_adam_step(i, gradient, a, gb, oa, ema_debias);
     }
-    gb.table_train[i] = (_Float16)w;
-    gb.table_infer[i] = (_Float16)inf;
 }
 
 __global__ __launch_bounds__(256) void grid_adam_kernel(int mode, GridBuffers gb, OptimArgs oa, float ema_debias) {
@@ -3821,6 +3842,7 @@ constexpr int kScatterThreads = 1024, kScatterPart = 8192, kScatterPer = 2;
 struct ScatterPlan {
     int first_block[NRC_HASH_LEVELS + 1];  // level l owns blocks [first_block[l], first_block[l + 1])
     int slice[NRC_HASH_LEVELS];            // samples per block at level l
+    int compact_first;                     // levels from here queue their in-part corners (below: direct adds)
 };
 constexpr int scatter_parts(int level) { return level == 0 ? 1 : NRC_HASH_T / kScatterPart; }
 
@@ -3831,12 +3853,24 @@ __device__ __forceinline__ int64_t f16_to_fixed(uint32_t h) {
     return (h & 0x8000u) ? -mag : mag;
 }
 
+// Round 5: the corners are compacted before their fixed-point adds. A block owns one table part (a quarter of a fine
+// level), so each lane's 8 corners land in it with probability 1/4 at the fine levels -- but the f16 -> fixed-point
+// conversion and the 64-bit LDS add of a corner ran for the whole wave whenever one lane needed them (exec-masked
+// branches), and the kernel was VALU-bound (PMC: VALU busy ~70 % of its 19.6 us). Now each wave appends the in-part
+// corners' (entry, contribution pair) words to its own LDS queue (ballot + mbcnt offsets) and drains the queue with
+// all 64 lanes busy when it holds more than kScatterQueue - 64 words, and at the end. The sums are the same exact
+// integers (integer adds in any order). Only the fine levels (knob scatter_compact, default kScatterCompactFirst):
+// at the coarse ones a block's part holds all 8 corners of most samples, on a few entries, and the queued adds of a
+// drain then collide on them at once.
+constexpr int kScatterQueue = 192;  // words per wave: 16 waves x 192 x 8 B = 24 KiB beside the 128-KiB table
+
 __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const float4* __restrict__ pos,
                                                                        const uint32_t* __restrict__ dy, int64_t bcap,
                                                                        ScatterPlan plan,
                                                                        unsigned long long* __restrict__ grad,
                                                                        GridNonFinite nf, ScatterPartials pt) {
     __shared__ unsigned long long acc[kScatterPart][2];  // 128 KiB: one block per CU
+    __shared__ uint64_t queue[kScatterThreads / 64][kScatterQueue];
     int level = 0;
 #pragma unroll
     for (int l = 1; l < NRC_HASH_LEVELS; ++l) level += (int)blockIdx.x >= plan.first_block[l];
@@ -3849,6 +3883,9 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
     const uint32_t ne = min((uint32_t)kScatterPart, lsize - e0);
     const uint32_t* dyl = dy + (int64_t)level * bcap;
     const int64_t s1 = min(bcap, s0 + slice);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t* const q = queue[threadIdx.x >> 6];
+    uint32_t qn = 0;  // words in this wave's queue (wave-uniform)
     // the first batch's loads are issued before the table is zeroed (their latency hides behind it)
     uint32_t dv[kScatterPer];
     float4 p[kScatterPer];
@@ -3861,6 +3898,38 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
             p[j] = sj < s1 ? pos[sj] : float4{0.0f, 0.0f, 0.0f, 0.0f};
         }
     };
+    // every queued word: (entry - e0) << 32 | the f16 contribution pair; the wave's own LDS writes are read back by
+    // other lanes of the same wave (LDS executes a wave's instructions in order; the fence keeps the compiler's order)
+    // the fixed-point adds of one corner's contribution pair cb at table entry e0 + e
+    auto add = [&](const uint32_t e, const uint32_t cb) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            const uint32_t hb = (cb >> (16 * f)) & 0xFFFFu;
+            if ((hb & 0x7C00u) == 0x7C00u) {
+                // inf / NaN: no fixed-point value; recorded for the kernels that round the sums
+                const uint32_t gi = 2u * (lbase + e0 + e) + (uint32_t)f;
+                const uint32_t code = (hb & 0x3FFu) ? 3u : ((hb & 0x8000u) ? 2u : 1u);
+                atomicOr(reinterpret_cast<uint32_t*>(nf.codes) + (gi >> 2), code << (8u * (gi & 3u)));
+                __hip_atomic_store(nf.tag_dev, nf.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (hb & 0x7FFFu) {
+                atomicAdd(&acc[e][f], (unsigned long long)f16_to_fixed(hb));
+            }
+        }
+    };
+    const bool compact = level >= plan.compact_first;
+    auto drain = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t t = lane; t < qn; t += 64) {
+            const uint64_t w = q[t];
+            add((uint32_t)(w >> 32), (uint32_t)w);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        qn = 0;
+    };
     load();
     for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads) acc[i][0] = acc[i][1] = 0ull;
     __syncthreads();
@@ -3869,29 +3938,31 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
         for (int j = 0; j < kScatterPer; ++j) {
             const h2v d = __builtin_bit_cast(h2v, dv[j]);
             const float dy0 = (float)d[0], dy1 = (float)d[1];
-            if (dy0 == 0.0f && dy1 == 0.0f) continue;  // also the samples past the slice
+            const bool active = (dv[j] & 0x7FFF7FFFu) != 0u;  // not both dy zero (also the samples past the slice)
             HashCorners C;
             if (level <= 1) hash_corners<true>(p[j].x, p[j].y, p[j].z, level, C);
             else hash_corners<false>(p[j].x, p[j].y, p[j].z, level, C);
 #pragma unroll
             for (int cc = 0; cc < 8; ++cc) {
                 const uint32_t e = C.entry[cc] - lbase - e0;
-                if (e < ne) {
-                    const h2v c = {(_Float16)(C.w[cc] * dy0), (_Float16)(C.w[cc] * dy1)};
-                    const uint32_t cb = __builtin_bit_cast(uint32_t, c);
-#pragma unroll
-                    for (int f = 0; f < 2; ++f) {
-                        const uint32_t hb = (cb >> (16 * f)) & 0xFFFFu;
-                        if ((hb & 0x7C00u) == 0x7C00u) {
-                            // inf / NaN: no fixed-point value; recorded for the kernels that round the sums
-                            const uint32_t gi = 2u * (lbase + e0 + e) + (uint32_t)f;
-                            const uint32_t code = (hb & 0x3FFu) ? 3u : ((hb & 0x8000u) ? 2u : 1u);
-                            atomicOr(reinterpret_cast<uint32_t*>(nf.codes) + (gi >> 2), code << (8u * (gi & 3u)));
-                            __hip_atomic_store(nf.tag_dev, nf.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        } else if (hb & 0x7FFFu) {
-                            atomicAdd(&acc[e][f], (unsigned long long)f16_to_fixed(hb));
-                        }
+                // w * dy rounded to f32, then to f16 (tcnn's half2 product): the empty asm keeps the compiler from
+                // fusing the two roundings into one v_fma_mixlo_f16 (another number in double-rounding cases)
+                float w0 = C.w[cc] * dy0, w1 = C.w[cc] * dy1;
+                asm volatile("" : "+v"(w0), "+v"(w1));
+                const h2v c = {(_Float16)w0, (_Float16)w1};
+                const uint32_t cb = __builtin_bit_cast(uint32_t, c);
+                const bool in = active && e < ne && (cb & 0x7FFF7FFFu) != 0u;  // zero contributions add nothing
+                if (compact) {  // block-uniform
+                    const uint64_t m = __ballot(in);
+                    if (m) {  // wave-uniform
+                        const uint32_t off =
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        if (in) q[qn + off] = ((uint64_t)e << 32) | cb;
+                        qn += (uint32_t)__popcll(m);
+                        if (qn > (uint32_t)(kScatterQueue - 64)) drain();
                     }
+                } else if (in) {
+                    add(e, cb);
                 }
             }
         }
@@ -3899,6 +3970,7 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
         if (s0 + (s - s0 - threadIdx.x) >= s1) break;  // block-uniform
         load();
     }
+    if (qn) drain();
     __syncthreads();
     if (pt.base && pt.nslice[level]) {
         // round 5, the fine levels (most entries touched): this block's part of its slice stored densely, zeros
@@ -3928,6 +4000,8 @@ static ScatterPlan scatter_plan(int64_t bcap, int& nb) {
         nb += scatter_parts(l) * (int)((bcap + sl - 1) / sl);
     }
     plan.first_block[NRC_HASH_LEVELS] = nb;
+    const int kc = knob(kKnobScatterCompact);
+    plan.compact_first = kc >= 0 ? kc : kScatterCompactFirst;
     return plan;
 }
 

@@ -135,3 +135,32 @@ def test_loop_rule_catches_the_round1_shape(tmp_path):
     assert not asm_hazard_check.scan_branch_store_loops(_write(tmp_path, no_branch_load))
     no_masked_store = ROUND1.replace("\ts_cbranch_execz .LBB0_10\n", "")
     assert not asm_hazard_check.scan_branch_store_loops(_write(tmp_path, no_masked_store))
+
+
+# a self-loop of loads only (the grid Adam's slice sum) placed after an exec-masked store region and a scalar-branch
+# load: the self-loop is one block, not everything before it (round 5: the checker had walked the self-loop's
+# predecessors into the kernel entry and reported a 272-block "loop")
+SELF_LOOP = """_Z6kernelv:
+\ts_and_b64 vcc, exec, s[2:3]
+\ts_cbranch_vccnz .LBB0_2
+.LBB0_1:
+\tglobal_load_dwordx2 v[6:7], v[4:5], off
+.LBB0_2:
+\ts_and_saveexec_b64 s[4:5], s[0:1]
+\ts_cbranch_execz .LBB0_3
+\tglobal_store_dword v1, v1, s[2:3]
+.LBB0_3:
+\tglobal_load_dwordx2 v[6:7], v[4:5], off sc1
+\ts_add_u32 s6, s6, -1
+\ts_cmp_lg_u32 s6, 0
+\ts_cbranch_scc1 .LBB0_3
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_loop_rule_self_loop_is_one_block(tmp_path):
+    path = _write(tmp_path, SELF_LOOP)
+    blocks = asm_hazard_check._blocks(next(iter(asm_hazard_check.kernels(path).values())))
+    assert [len(l) for l in asm_hazard_check._natural_loops(blocks)] == [1]
+    assert not asm_hazard_check.scan_branch_store_loops(path)

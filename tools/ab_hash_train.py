@@ -23,7 +23,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--knob", default="scatter_part")
     ap.add_argument("--values", default="16,0,2,4,6,8")
-    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--rounds", type=int, default=7)  # interleaved rounds per value
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--set", action="append", default=[], help="name=value knob held for the whole run")
     args = ap.parse_args()

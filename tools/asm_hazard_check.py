@@ -225,8 +225,10 @@ def _natural_loops(blocks) -> list[set[int]]:
     for u in range(n):
         for h in blocks[u][1]:
             if h in dom[u]:  # back edge u -> h
+                # the blocks that reach u without passing h; a self-loop (u == h) is that block alone (walking its
+                # predecessors would take in the loop's entry path and everything before it)
                 body = {h, u}
-                stack = [u]
+                stack = [u] if u != h else []
                 while stack:
                     x = stack.pop()
                     for p in preds[x]:

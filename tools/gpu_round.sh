@@ -89,7 +89,7 @@ hash-abl)
 hash-train-ab)
   values=${1:-16,0,2,4,6,8} knob=${2:-scatter_part} tag=${3:-0}; shift $(( $# < 3 ? $# : 3 ))
   held=(); for kv in "$@"; do held+=(--set "$kv"); done
-  timeout -k 10 300 python tools/ab_hash_train.py --knob "$knob" --values "$values" "${held[@]}" > "gpurun_out/ab_hash_train_$tag.json" 2> "gpurun_out/ab_hash_train_$tag.err" || { echo "hash train A/B failed"; tail -20 "gpurun_out/ab_hash_train_$tag.err"; exit 4; }
+  timeout -k 10 300 python tools/ab_hash_train.py --knob "$knob" --values="$values" "${held[@]}" > "gpurun_out/ab_hash_train_$tag.json" 2> "gpurun_out/ab_hash_train_$tag.err" || { echo "hash train A/B failed"; tail -20 "gpurun_out/ab_hash_train_$tag.err"; exit 4; }
   cat "gpurun_out/ab_hash_train_$tag.json"
   ;;
 pmc-hash)
