@@ -35,7 +35,7 @@ FLOP_PER_QUERY_WIDE = 2 * (66 * 128 + 4 * 128 * 128 + 128 * 3)  # 148,736 (SURVE
 PEAK_HBM_GBS = 8000.0
 QUERIES_PER_GPU = 1 << 21
 QUERIES_C4 = 1 << 22  # configs[3]: the 2K frame, sharded over the ranks
-ROUND = "r04"
+ROUND = "r05"
 
 
 def parse():
