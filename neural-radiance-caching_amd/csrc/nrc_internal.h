@@ -417,6 +417,9 @@ ScatterPartials scatter_partials_layout(int64_t b, int first_level);
 // default first level (knob scatter_part): fused step 63.0 us all-atomic, 58.3 / 57.6 / 57.4 / 56.5 / 57.2 from level
 // 0 / 2 / 4 / 6 / 8 (profiles/r05_hash/ab_scatter_part.json, parameters bitwise equal)
 constexpr int kScatterPartFirst = 6;
+// at most this many slices per level use partials (bigger batches flush with atomics: the partial bytes, and the grid
+// Adam's reads of them, grow with the batch; 8 slices = 32,768 samples at the default plan, 40 MiB)
+constexpr int kMaxPartialSlices = 8;
 // default first level of the corner queue (knob scatter_compact): step 57.3 us without, 56.0 from level 4, 55.8 from
 // level 10 (profiles/r05_hash/ab_scatter_compact_repeat.json, 12 interleaved rounds x 2)
 constexpr int kScatterCompactFirst = 10;

@@ -4011,9 +4011,11 @@ ScatterPartials scatter_partials_layout(int64_t b, int first_level) {
     const ScatterPlan plan = scatter_plan(bcap, nb);
     ScatterPartials p;
     for (int l = first_level; l < NRC_HASH_LEVELS; ++l) {
+        const int ns = (int)((bcap + plan.slice[l] - 1) / plan.slice[l]);
+        if (ns > kMaxPartialSlices) continue;  // a large batch: the atomic flush (partials would grow with the batch)
         p.off[l] = p.total;
-        p.nslice[l] = (int)((bcap + plan.slice[l] - 1) / plan.slice[l]);
-        p.total += (int64_t)p.nslice[l] * 2 * (l == 0 ? 4096 : NRC_HASH_T);
+        p.nslice[l] = ns;
+        p.total += (int64_t)ns * 2 * (l == 0 ? 4096 : NRC_HASH_T);
     }
     return p;
 }

@@ -375,3 +375,41 @@ def test_hash_training_is_deterministic(nrc, orc, dev):
     finally:
         for n in nets:
             n.destroy()
+
+
+@pytest.mark.parametrize("b", [16384, 20000, 40000])
+def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b):
+    """Round 5: the grid scatter's fine levels store per-slice partial sums that grid_adam_kernel adds (knob
+    scatter_part, default from level 6), levels 10-15 queue their in-part corners before the adds (scatter_compact), and
+    past 8 slices per level (b > 32,768) the partials give way to the atomic flush. The sums are exact integers, so
+    every form must leave the same state, bit for bit, as the all-atomic, uncompacted scatter (both knobs 16) --
+    including the 20,000-sample batch whose last slice is ragged."""
+    import torch
+    L = nrc._lib
+    forms = [{}, {"scatter_part": 16, "scatter_compact": 16}, {"scatter_part": 0, "scatter_compact": 0}]
+    nets = []
+    for _ in forms:
+        n = nrc.Network()
+        n.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+        nets.append(n)
+    try:
+        losses = [[] for _ in forms]
+        for it in range(3):
+            q, t = nrc.synthetic.cornell_batch(b, seed=700 + it)
+            qd, td = _t(q, dev), _t(t, dev)
+            for k, (n, f) in enumerate(zip(nets, forms)):
+                for name, v in f.items():
+                    L.set_knob(name, v)
+                try:
+                    losses[k].append(n.train_batch(qd, td, b, loss=True))
+                finally:
+                    for name in f:
+                        L.set_knob(name, -1)
+        assert losses[0] == losses[1] == losses[2]
+        for slot in nrc.StateSlot:
+            ref = nets[1].get_state(slot)
+            for n in (nets[0], nets[2]):
+                np.testing.assert_array_equal(n.get_state(slot), ref)
+    finally:
+        for n in nets:
+            n.destroy()
