@@ -436,19 +436,25 @@ struct nrc_net {
     HashScatter scatter{};  // Hash training: per-sample positions and grid-feature gradients (grid_scatter_kernel)
     int scatter_blocks = 0;
     int64_t* scatter_part = nullptr;  // per-slice partial sums of the fused step's fine levels (ScatterPartials)
-    int64_t scatter_part_words = 0;
-    // the partial layout of a fused b-sample step (knob scatter_part: first level with partials), buffer grown to fit
+    size_t scatter_part_bytes = 0;
+    // the partial layout of a fused b-sample step (knob scatter_part: first level with partials), buffer grown to fit:
+    // the int64 form, the int32 form (same element count) and the per-block form flags, in one allocation
     ScatterPartials step_partials(uint32_t b) {
         const int k = knob(kKnobScatterPart);
         ScatterPartials p = scatter_partials_layout(b, k >= 0 ? k : kScatterPartFirst);
-        if (p.total > scatter_part_words) {
+        const size_t bytes = (size_t)p.total * (sizeof(int64_t) + sizeof(int32_t)) + sizeof(uint32_t) * (size_t)p.nflags;
+        if (bytes > scatter_part_bytes) {
             if (scatter_part) HIP_CHECK(hipFree(scatter_part));
             scatter_part = nullptr;
-            scatter_part_words = 0;
-            HIP_CHECK(hipMalloc(&scatter_part, sizeof(int64_t) * (size_t)p.total));
-            scatter_part_words = p.total;
+            scatter_part_bytes = 0;
+            HIP_CHECK(hipMalloc(&scatter_part, bytes));
+            scatter_part_bytes = bytes;
         }
-        if (p.total) p.base = scatter_part;
+        if (p.total) {
+            p.base = scatter_part;
+            p.base32 = reinterpret_cast<int32_t*>(scatter_part + p.total);
+            p.flags = reinterpret_cast<uint32_t*>(p.base32 + p.total);
+        }
         return p;
     }
     uint8_t* grid_nf = nullptr;       // [n_grid] non-finite contribution codes (GridNonFinite)
@@ -507,7 +513,7 @@ struct nrc_net {
         f(scatter.pos); f(scatter.dy); f(scatter_part);
         scatter = HashScatter{};
         scatter_part = nullptr;
-        scatter_part_words = 0;
+        scatter_part_bytes = 0;
         scatter_blocks = 0;
         f(wide_img16); f(wide_img8); f(wide_scales);
         f(wide_fwd_train); f(wide_bwd_train); f(wide_ws_in); f(wide_ws_d); f(wide_slabs); f(wide_loss_partials);

@@ -405,11 +405,18 @@ struct GridNonFinite {
 // stores, no global atomics), and grid_adam_kernel sums the slices in slice order. Levels with nslice 0 (the coarse
 // ones: few entries touched, so dense stores would be mostly zeros) and every level when base is null add into grad64
 // with global atomics instead (the data-parallel exports read grad64).
+// A block's part of a slice is stored as int32 when every one of its sums fits (the usual case: |sum| < 128 in f16
+// units), else as int64; flags[foff[l] + slice * parts(l) + part] says which (1 = int64), so the partial bytes the
+// grid Adam reads are halved without giving up exactness.
 struct ScatterPartials {
-    int64_t* base = nullptr;
+    int64_t* base = nullptr;   // int64 form, element e of (level l, slice s) at base + off[l] + s * 2 * entries(l) + e
+    int32_t* base32 = nullptr; // int32 form, the same element indexing
+    uint32_t* flags = nullptr; // per (level, slice, part): 1 = that block stored the int64 form
     int64_t off[NRC_HASH_LEVELS] = {};
+    int foff[NRC_HASH_LEVELS] = {};
     int nslice[NRC_HASH_LEVELS] = {};
-    int64_t total = 0;  // int64 words of the layout
+    int64_t total = 0;  // elements of the layout (each form)
+    int nflags = 0;
 };
 // the layout of a b-sample step under the current scatter plan (knobs scatter_min / scatter_max), partial sums for
 // levels first_level.. (nslice 0 below: those levels flush into grad64 with atomics; total 0 when first_level = 16)

@@ -3764,12 +3764,32 @@ __device__ __forceinline__ void grid_adam_body(const int blk, int mode, const Gr
         } else {
             // the step's exact sum: the level's per-slice partials (grid_scatter_kernel's plain-store levels, round 5)
             // added in slice order, else the atomic accumulator (zeroed for the next step); exact int64 either way
-            const int l = i < 8192 ? 0 : 1 + ((i - 8192) >> 16);
+            // level and table part are block-uniform (256 parameters per block, 8,192 / 16,384 per part)
+            const int l = __builtin_amdgcn_readfirstlane(i < 8192 ? 0 : 1 + ((i - 8192) >> 16));
             int64_t sum = 0;
             if (gb.part.base && gb.part.nslice[l]) {
                 const int j = i - (l == 0 ? 0 : 8192 + ((l - 1) << 16)), stride = l == 0 ? 8192 : 65536;
+                const int nparts = l == 0 ? 1 : NRC_HASH_T / 8192;
+                const int part = __builtin_amdgcn_readfirstlane(j / (2 * 8192));
+                const int ns = gb.part.nslice[l];
+                // every slice's form flag (scalar loads), then every slice's partial, branch-free: an int32 element is
+                // read as the aligned 8-byte pair holding it (the lanes of a wave still read each line once)
+                uint32_t wide = 0;
+#pragma unroll
+                for (int sl = 0; sl < kMaxPartialSlices; ++sl)
+                    wide |= (sl < ns ? gb.part.flags[gb.part.foff[l] + min(sl, ns - 1) * nparts + part] : 0u) << sl;
                 const int64_t* src = gb.part.base + gb.part.off[l] + j;
-                for (int sl = 0; sl < gb.part.nslice[l]; ++sl) sum += src[(int64_t)sl * stride];
+                const int64_t* src32 = reinterpret_cast<const int64_t*>(gb.part.base32 + gb.part.off[l] + (j & ~1));
+                int64_t v[kMaxPartialSlices];
+#pragma unroll
+                for (int sl = 0; sl < kMaxPartialSlices; ++sl) {
+                    const int sc = min(sl, ns - 1);
+                    const bool w = (wide >> sc) & 1u;
+                    const int64_t raw = *(w ? src + (int64_t)sc * stride : src32 + (int64_t)sc * (stride / 2));
+                    v[sl] = w ? raw : (int64_t)(int32_t)(uint32_t)(raw >> (32 * (j & 1)));
+                }
+#pragma unroll
+                for (int sl = 0; sl < kMaxPartialSlices; ++sl) sum += sl < ns ? v[sl] : 0;
             } else {
                 sum = gb.grad64[i];
                 gb.grad64[i] = 0;
@@ -3974,11 +3994,28 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
     __syncthreads();
     if (pt.base && pt.nslice[level]) {
         // round 5, the fine levels (most entries touched): this block's part of its slice stored densely, zeros
-        // included, with plain 16-byte stores instead of memory-side atomics; grid_adam_kernel sums the slices
-        typedef long long i2v __attribute__((ext_vector_type(2)));
-        i2v* const dst = reinterpret_cast<i2v*>(pt.base + pt.off[level] + (int64_t)(local / nparts) * 2 * lsize) + e0;
-        for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads)
-            dst[i] = i2v{(long long)acc[i][0], (long long)acc[i][1]};
+        // included, with plain 16-byte stores instead of memory-side atomics; grid_adam_kernel sums the slices. As
+        // int32 when every sum of the part fits (half the bytes), else as int64 (flagged)
+        const int sl = local / nparts;
+        bool wide = false;
+        for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads) {
+            const int64_t v0 = (int64_t)acc[i][0], v1 = (int64_t)acc[i][1];
+            wide = wide || v0 != (int64_t)(int32_t)v0 || v1 != (int64_t)(int32_t)v1;
+        }
+        const bool any_wide = __syncthreads_or(wide) != 0;
+        const int64_t el = pt.off[level] + (int64_t)sl * 2 * lsize + 2 * e0;
+        if (any_wide) {
+            typedef long long i2v __attribute__((ext_vector_type(2)));
+            i2v* const dst = reinterpret_cast<i2v*>(pt.base + el);
+            for (uint32_t i = threadIdx.x; i < ne; i += kScatterThreads)
+                dst[i] = i2v{(long long)acc[i][0], (long long)acc[i][1]};
+        } else {
+            typedef int i4v __attribute__((ext_vector_type(4)));
+            i4v* const dst = reinterpret_cast<i4v*>(pt.base32 + el);  // two entries per 16-byte store
+            for (uint32_t i = threadIdx.x; 2 * i < ne; i += kScatterThreads)
+                dst[i] = i4v{(int)acc[2 * i][0], (int)acc[2 * i][1], (int)acc[2 * i + 1][0], (int)acc[2 * i + 1][1]};
+        }
+        if (threadIdx.x == 0) pt.flags[pt.foff[level] + sl * nparts + part] = any_wide ? 1u : 0u;
         return;
     }
     for (uint32_t i = threadIdx.x; i < 2 * ne; i += kScatterThreads) {
@@ -4014,8 +4051,10 @@ ScatterPartials scatter_partials_layout(int64_t b, int first_level) {
         const int ns = (int)((bcap + plan.slice[l] - 1) / plan.slice[l]);
         if (ns > kMaxPartialSlices) continue;  // a large batch: the atomic flush (partials would grow with the batch)
         p.off[l] = p.total;
+        p.foff[l] = p.nflags;
         p.nslice[l] = ns;
         p.total += (int64_t)ns * 2 * (l == 0 ? 4096 : NRC_HASH_T);
+        p.nflags += ns * scatter_parts(l);
     }
     return p;
 }
