@@ -3858,6 +3858,8 @@ hipError_t launch_grid_grad_export_fixed(int64_t* g64, int64_t* out, int n, cons
 // (position * 0.005 spans ~1.6 * 2^l cells per axis), so their LDS adds collide on a few addresses and serialise --
 // a block's time grows with (slice samples / touched entries) -- while a fine level's block costs mostly its
 // table flush. So the slice doubles per level from `min` to `max`.
+// Round 5: from level kScatterPartFirst (knob scatter_part) a block stores its part of its slice densely as per-slice
+// partial sums instead of the atomic flush (ScatterPartials, int32 where every sum fits), summed by grid_adam_kernel.
 constexpr int kScatterThreads = 1024, kScatterPart = 8192, kScatterPer = 2;
 struct ScatterPlan {
     int first_block[NRC_HASH_LEVELS + 1];  // level l owns blocks [first_block[l], first_block[l + 1])

@@ -377,13 +377,14 @@ def test_hash_training_is_deterministic(nrc, orc, dev):
             n.destroy()
 
 
-@pytest.mark.parametrize("b", [16384, 20000, 40000])
-def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b):
+@pytest.mark.parametrize("b,tscale", [(16384, 1.0), (20000, 1.0), (40000, 1.0), (16384, 3000.0)])
+def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b, tscale):
     """Round 5: the grid scatter's fine levels store per-slice partial sums that grid_adam_kernel adds (knob
     scatter_part, default from level 6), levels 10-15 queue their in-part corners before the adds (scatter_compact), and
     past 8 slices per level (b > 32,768) the partials give way to the atomic flush. The sums are exact integers, so
     every form must leave the same state, bit for bit, as the all-atomic, uncompacted scatter (both knobs 16) --
-    including the 20,000-sample batch whose last slice is ragged."""
+    including the 20,000-sample batch whose last slice is ragged, and targets x 3000, whose large gradients make some
+    blocks' partial sums overflow int32 (those blocks store the int64 form)."""
     import torch
     L = nrc._lib
     forms = [{}, {"scatter_part": 16, "scatter_compact": 16}, {"scatter_part": 0, "scatter_compact": 0}]
@@ -396,7 +397,7 @@ def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b):
         losses = [[] for _ in forms]
         for it in range(3):
             q, t = nrc.synthetic.cornell_batch(b, seed=700 + it)
-            qd, td = _t(q, dev), _t(t, dev)
+            qd, td = _t(q, dev), _t(t * np.float32(tscale), dev)
             for k, (n, f) in enumerate(zip(nets, forms)):
                 for name, v in f.items():
                     L.set_knob(name, v)
@@ -406,6 +407,19 @@ def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b):
                     for name in f:
                         L.set_knob(name, -1)
         assert losses[0] == losses[1] == losses[2]
+        if tscale > 1.0:
+            # the int64 form was taken: some fine-level entry's gradient over the 16,384 samples (4 slices) exceeds
+            # 4 x 128 in f16 units, so one of its slice sums reached 2^31 in fixed point
+            g = torch.zeros(nets[0].grad_floats, device=dev)
+            q, t = nrc.synthetic.cornell_batch(b, seed=700)
+            probe = nrc.Network()
+            probe.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Hash)
+            try:
+                probe.train_grad(_t(q, dev), _t(t * np.float32(tscale), dev), b, b, g)
+                fine = g[21504 + 2 * (4096 + 5 * 32768):21504 + 991232].abs()
+                assert float(fine[torch.isfinite(fine)].max()) > 512.0
+            finally:
+                probe.destroy()
         for slot in nrc.StateSlot:
             ref = nets[1].get_state(slot)
             for n in (nets[0], nets[2]):
