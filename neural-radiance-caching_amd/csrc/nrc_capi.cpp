@@ -263,11 +263,11 @@ bool want_t16(int encoding) {
     return encoding == NRC_ENCODING_FREQUENCY || encoding == NRC_ENCODING_HASH;
 }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
                                             "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path",
-                                            "px_polls", "scatter_part", "scatter_compact"};
-static_assert(kKnobCount == 13, "one initial value and one name per knob");
+                                            "px_polls", "scatter_part", "scatter_compact", "hash_train_feat"};
+static_assert(kKnobCount == 14, "one initial value and one name per knob");
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -900,6 +900,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobPxPolls: return v == -1 || (v >= 1 && v <= kPeerPolls);
         case kKnobScatterPart:
         case kKnobScatterCompact: return v >= -1 && v <= NRC_HASH_LEVELS;
+        case kKnobHashTrainFeat: return v >= -1 && v <= 1;
         default: return false;
     }
 }

@@ -384,7 +384,8 @@ enum Knob : int {
     kKnobPxPolls = 10,     // bound of the peer exchange's wait loops (-1 = kPeerPolls, about 10 s; 1..2^21)
     kKnobScatterPart = 11, // Hash training: first grid level whose scatter stores per-slice partials (-1 default, 0..16)
     kKnobScatterCompact = 12, // Hash training: first grid level whose scatter queues its in-part corners (-1 default, 0..16)
-    kKnobCount = 13
+    kKnobHashTrainFeat = 13,  // Hash training: the batch's level features by 0 the LDS pass, 1 gathers (-1 = 1)
+    kKnobCount = 14
 };
 int knob(Knob k);
 

@@ -3182,6 +3182,36 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
     return launch_infer_variant(g_default_infer_variant, queries, out, n, wf, s, pools, parity);
 }
 
+// Round 5: a training step's level features by gathers from the f16 table (2 MB, L2-resident) instead of the LDS
+// pass: at 16,384 samples the LDS pass is 128 blocks each staging a 128-KiB level table into one CU (≈5 us of LDS-DMA
+// per block, half the chip idle), while the 2 M gathers of the step spread over every CU. Thread = (level, sample);
+// block k sits on XCD k % 8, which holds levels x and x + 8 (two level tables per XCD L2). Bitwise the LDS pass's
+// features (hash_level_feature: the same corners, weights and half-FMA order).
+template <int QD>
+__global__ __launch_bounds__(256) void hash_feature_gather_kernel(const float* __restrict__ q, int64_t n, int nchunk,
+                                                                  const uint32_t* __restrict__ table,
+                                                                  uint32_t* __restrict__ feat) {
+    const int k = (int)blockIdx.x, x = k & 7, j = k >> 3;
+    const int level = x + (j >= nchunk ? 8 : 0), chunk = j >= nchunk ? j - nchunk : j;
+    const int64_t s = (int64_t)chunk * 256 + threadIdx.x;
+    if (s >= n) return;
+    const float* r = q + s * QD;
+    const float px = r[0], py = r[1], pz = r[2];
+    feat[(int64_t)level * kHashFeatStride + s] = level <= 1 ? hash_level_feature<true>(px, py, pz, level, table)
+                                                            : hash_level_feature<false>(px, py, pz, level, table);
+}
+
+static void launch_hash_feature_gather(const float* q, int64_t n, const uint32_t* g, uint32_t* feat, bool padq,
+                                       hipStream_t s) {
+    const int nchunk = (int)((n + 255) / 256);
+    if (padq)
+        hipLaunchKernelGGL(hash_feature_gather_kernel<NRC_INPUT_DIMS_PADDED>, dim3(16 * nchunk), dim3(256), 0, s, q, n,
+                           nchunk, g, feat);
+    else
+        hipLaunchKernelGGL(hash_feature_gather_kernel<NRC_INPUT_DIMS>, dim3(16 * nchunk), dim3(256), 0, s, q, n, nchunk,
+                           g, feat);
+}
+
 // One feature pass of hash_feature_kernel over cnt <= kHashFeatStride queries (the launch shape of launch_infer_hash).
 // p_default: query ranges per level when the knob is unset (0: the inference choice below)
 static void launch_hash_feature_pass(const float* qc0, int64_t cnt, const uint32_t* g, uint32_t* feat, bool padq,
@@ -4077,7 +4107,12 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
         const bool fp = feat && b <= kHashFeatStride;
         // P = 8 query ranges per level (the minimum of the kernel's block map): 16,384-sample step 63.7 us vs 63.9 (16)
         // and 67.8 (32), profiles/r05_hash/
-        if (fp) launch_hash_feature_pass(queries, b, g, feat, padq, s, 8);
+        if (fp) {
+            // the gather pass by default: fused step 54.3 vs 55.8 us with the LDS pass, parameters bitwise equal
+            // (profiles/r05_hash/ab_train_feature_gather.json)
+            if (knob(kKnobHashTrainFeat) != 0) launch_hash_feature_gather(queries, b, g, feat, padq, s);
+            else launch_hash_feature_pass(queries, b, g, feat, padq, s, 8);
+        }
         const hipError_t e = launch_train16_hash(queries, targets, b, n_total, loss_scale, wf, wb,
                                                  reinterpret_cast<_Float16*>(slabs), loss_partials,
                                                  HashTrainOut{g, fp ? feat : nullptr, sc->pos, sc->dy, bcap}, s, padq);
