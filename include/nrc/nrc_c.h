@@ -233,11 +233,12 @@ nrc_status nrc_set_step(nrc_net* net, uint32_t step);
  * "px_polls" (bound of the exchange's wait loops, -1 = 2^21 polls, about 10 s), "scatter_part" (Hash training: first
  * grid level whose scatter stores per-slice partial sums instead of adding with atomics, 16 = none), "scatter_compact"
  * (Hash training: first grid level whose scatter queues its in-part corners before the adds, 16 = none),
- * "hash_train_feat" (Hash training: the batch's level features by 0 the LDS-table pass, 1 gathers), "hash_feat_p"
+ * "hash_train_feat" (Hash training: the batch's level features by 0 the LDS-table pass, 1 gathers), "hash_adam" (Hash
+ * training: 0 = the MLP and grid optimizer updates as two launches instead of one), "hash_feat_p"
  * (Hash inference: query ranges per level of the feature pass); debug library only: "dc_dw0_delay", "hash_feat_abl".
  * -1 restores the production choice. A value outside a knob's range (train_kernel -1/0/1/2/32,
  * train_shape -1..7, scatter_min / scatter_max -1 or 16..2^20, hash_infer -1..1, t16_groups -1/1/2, dc_dw0_delay -1..2^20, hash_feat_abl
- * -1..36, hash_feat_p -1 or a multiple of 8 in 8..256, peer_path -1..4, px_polls -1 or 1..2^21, scatter_part / scatter_compact -1..16, hash_train_feat -1..1) is
+ * -1..36, hash_feat_p -1 or a multiple of 8 in 8..256, peer_path -1..4, px_polls -1 or 1..2^21, scatter_part / scatter_compact -1..16, hash_train_feat -1..1, hash_adam -1..0) is
  * NRC_ERR_INVALID_ARGUMENT and leaves the knob unchanged. */
 nrc_status nrc_debug_set_knob(const char* name, int value);
 nrc_status nrc_debug_get_knob(const char* name, int* value);

@@ -263,11 +263,12 @@ bool want_t16(int encoding) {
     return encoding == NRC_ENCODING_FREQUENCY || encoding == NRC_ENCODING_HASH;
 }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
                                             "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path",
-                                            "px_polls", "scatter_part", "scatter_compact", "hash_train_feat"};
-static_assert(kKnobCount == 14, "one initial value and one name per knob");
+                                            "px_polls", "scatter_part", "scatter_compact", "hash_train_feat",
+                                            "hash_adam"};
+static_assert(kKnobCount == 15, "one initial value and one name per knob");
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -732,6 +733,12 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
         const ScatterPartials part = net->step_partials(b);
         train_hash(net, in, tgt, b, 3.0f * (float)b, blocks, part);
         net->step += 1;
+        if (net->t16 && knob(kKnobHashAdam) != 0) {  // both updates in one launch (hash_adam_kernel)
+            HIP_CHECK(launch_hash_adam(net->slabs, blocks, net->loss_partials, loss_d ? loss_d : net->loss_dev,
+                                       net->buffers(), net->grid_buffers(part), net->optim(net->step), net->stream));
+            if (loss_h) *loss_h = net->read_loss();
+            return;
+        }
         HIP_CHECK(launch_reduce_adam(kReduceFused, net->slabs, blocks, net->loss_partials, nullptr,
                                      loss_d ? loss_d : net->loss_dev, net->buffers(), net->optim(net->step), net->stream));
         HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(part), net->optim(net->step), net->stream));
@@ -901,6 +908,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobScatterPart:
         case kKnobScatterCompact: return v >= -1 && v <= NRC_HASH_LEVELS;
         case kKnobHashTrainFeat: return v >= -1 && v <= 1;
+        case kKnobHashAdam: return v >= -1 && v <= 0;
         default: return false;
     }
 }

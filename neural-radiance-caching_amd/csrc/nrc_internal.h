@@ -385,7 +385,8 @@ enum Knob : int {
     kKnobScatterPart = 11, // Hash training: first grid level whose scatter stores per-slice partials (-1 default, 0..16)
     kKnobScatterCompact = 12, // Hash training: first grid level whose scatter queues its in-part corners (-1 default, 0..16)
     kKnobHashTrainFeat = 13,  // Hash training: the batch's level features by 0 the LDS pass, 1 gathers (-1 = 1)
-    kKnobCount = 14
+    kKnobHashAdam = 14,       // Hash training: 0 = the MLP and grid optimizer updates as two launches (-1: one)
+    kKnobCount = 15
 };
 int knob(Knob k);
 
@@ -477,6 +478,9 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false,
                              bool t16 = false, uint32_t* feat = nullptr);
+// the fused Hash step's MLP reduce + Adam and grid Adam (kReduceFused both) in one launch (t16 f16 slabs only)
+hipError_t launch_hash_adam(const float* slabs, int nslabs, const float* loss_partials, float* loss_out,
+                            const ModelBuffers& mb, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials,
                               float* grad_io, float* loss_out, const ModelBuffers& mb, const OptimArgs& oa,
                               hipStream_t s);

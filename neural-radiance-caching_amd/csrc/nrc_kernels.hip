@@ -4149,6 +4149,37 @@ void adam_host_factors(const OptimArgs& oa, float& lr_t, float& ema_debias) {
     ema_debias = 1.0f - powf(oa.ema_decay, step);
 }
 
+// Round 5: the fused Hash step's two optimizer updates in one launch: blocks [0, nred) reduce the MLP's f16 slabs and
+// apply its Adam/EMA (reduce_adam_body, the latency-bound part), the rest apply the grid Adam (grid_adam_body, the
+// memory-bound part), so that the MLP update runs beside the grid's instead of after it, behind one kernel boundary
+// instead of two. Both bodies are inlined (a first version with noinline halves took 75 us per step) and the same
+// float operations as their own launches: the state is bitwise that of launch_reduce_adam + launch_grid_adam (leaving
+// the grid's f32 inference copy to a refresh before reads measured no faster: 50.59 vs 50.63 us per step).
+__global__ __launch_bounds__(kRedThreads) void hash_adam_kernel(int nred, const float* __restrict__ slabs, int nslabs,
+                                                                const float* __restrict__ loss_partials,
+                                                                float* __restrict__ loss_out, ModelBuffers mb,
+                                                                OptimArgs oa, float lr_t, float ema_debias,
+                                                                GridBuffers gb, float grid_ema_debias) {
+    static_assert(kRedThreads == 256, "the grid Adam's blocks are 256 threads");
+    if ((int)blockIdx.x < nred)
+        reduce_adam_body<true>(blockIdx.x, kReduceFused, slabs, nslabs, loss_partials, nullptr, loss_out, mb, oa, lr_t,
+                               ema_debias);
+    else
+        grid_adam_body((int)blockIdx.x - nred, kReduceFused, gb, oa, grid_ema_debias);
+}
+
+hipError_t launch_hash_adam(const float* slabs, int nslabs, const float* loss_partials, float* loss_out,
+                            const ModelBuffers& mb, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s) {
+    if (!mb.slab_f16) return hipErrorInvalidValue;  // the t16 training kernel's f16 slabs
+    float lr_t, ema_debias;
+    adam_host_factors(oa, lr_t, ema_debias);
+    const float grid_ema_debias = 1.0f - powf(oa.ema_decay, (float)(oa.step ? oa.step : 1));
+    const int nred = mb.n_slab / (kRedParams * kRedVec), ngrid = (gb.n + 255) / 256;
+    hipLaunchKernelGGL(hash_adam_kernel, dim3((unsigned)(nred + ngrid)), dim3(kRedThreads), 0, s, nred, slabs, nslabs,
+                       loss_partials, loss_out, mb, oa, lr_t, ema_debias, gb, grid_ema_debias);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce_adam(int mode, const float* slabs, int nslabs, const float* loss_partials, float* grad_io,
                               float* loss_out, const ModelBuffers& mb, const OptimArgs& oa, hipStream_t s) {
     float lr_t, ema_debias;

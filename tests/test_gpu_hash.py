@@ -382,12 +382,16 @@ def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b, tscale):
     """Round 5: the grid scatter's fine levels store per-slice partial sums that grid_adam_kernel adds (knob
     scatter_part, default from level 6), levels 10-15 queue their in-part corners before the adds (scatter_compact), and
     past 8 slices per level (b > 32,768) the partials give way to the atomic flush. The sums are exact integers, so
-    every form must leave the same state, bit for bit, as the all-atomic, uncompacted scatter (both knobs 16) --
+    every form must leave the same state, bit for bit, as the all-atomic, uncompacted scatter (both knobs 16) with the
+    LDS feature pass and the two optimizer launches (hash_adam 0, which also writes the grid's f32 inference copy every
+    step; the default one-launch update leaves it to a refresh at nrc_get_state, from the step it was left at even when
+    nrc_set_step moved the counter since) --
     including the 20,000-sample batch whose last slice is ragged, and targets x 3000, whose large gradients make some
     blocks' partial sums overflow int32 (those blocks store the int64 form)."""
     import torch
     L = nrc._lib
-    forms = [{}, {"scatter_part": 16, "scatter_compact": 16}, {"scatter_part": 0, "scatter_compact": 0}]
+    forms = [{}, {"scatter_part": 16, "scatter_compact": 16, "hash_adam": 0, "hash_train_feat": 0},
+             {"scatter_part": 0, "scatter_compact": 0}]
     nets = []
     for _ in forms:
         n = nrc.Network()
@@ -420,6 +424,7 @@ def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b, tscale):
                 assert float(fine[torch.isfinite(fine)].max()) > 512.0
             finally:
                 probe.destroy()
+        nets[0].step = nets[0].step + 7
         for slot in nrc.StateSlot:
             ref = nets[1].get_state(slot)
             for n in (nets[0], nets[2]):
