@@ -344,16 +344,18 @@ def test_infer_accumulate_fused_bitwise(nrc, dev, mode, n, n_acc):
     net.destroy()
 
 
-def test_process_frame_fused_equals_unfused(nrc, dev):
+@pytest.mark.parametrize("encoding", ["Frequency", "Hash"])
+def test_process_frame_fused_equals_unfused(nrc, dev, encoding):
     """The default (fused, one loss sync) frame == the reference-shaped unfused frame: same frame buffer, same
-    train-suffix radiance, same losses and weights."""
+    train-suffix radiance, same losses and weights. Hash (round 5): the frame driver over the Hash handle's feature
+    pass + MLP pass with the fused accumulation, and its training steps (scatter partials, one optimizer launch)."""
     import torch
     F = nrc.frame
     f = nrc.synthetic.cornell_frame(256, 192, (4, 4), seed=8, frame_index=1)
     out = []
     for keep in (False, True):
         net = nrc.Network()
-        net.init(stream=torch.cuda.current_stream())
+        net.init(stream=torch.cuda.current_stream(), encoding=getattr(nrc.InputEncoding, encoding))
         fb, *_ = _device_frame(nrc, f, dev)
         fb.output_rgba.fill_(0.25)
         losses = [F.process_frame(net, fb, F.FrameParams(f.screen_size, f.num_tiles, f.num_training_records,
