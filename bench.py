@@ -259,8 +259,17 @@ def wide_bench(nrc, dev, world: int, rank: int, steps: int, barrier) -> dict:
                        "sharded over the GPUs (xavier-init weights)", "queries_per_gpu": nq,
            "flop_per_query": FLOP_PER_QUERY_WIDE}
     for prec, name, peak in ((nrc.PRECISION_F16, "f16", PEAK_F16_TFLOPS), (nrc.PRECISION_FP8, "fp8", PEAK_FP8_TFLOPS)):
-        for _ in range(3):
-            net.infer_precision(prec, q, out, nq, stream=stream)
+        # clock settle as for the headline kernel: >= 60 ms of untimed launches (the first ones run while the clock
+        # ramps; a 1.5-s back-to-back run of the FP8 path takes 631.6 us per launch, profiles/r05_end/power_paths.json)
+        settled = 0.0
+        while settled < 60.0:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(5):
+                net.infer_precision(prec, q, out, nq, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            settled += e0.elapsed_time(e1)
         barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
