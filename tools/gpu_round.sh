@@ -13,6 +13,8 @@
 #   tools/gpu_round.sh power [power_paths.py args...]             power / clock / nJ per query of the product paths
 #   tools/gpu_round.sh hash-abl <knob values> [knob]              Hash feature-pass A/B over a knob (tools/ab_hash_p.py)
 #   tools/gpu_round.sh hash-train-ab [values] [knob] [tag] [k=v...] fused Hash training step A/B (tools/ab_hash_train.py)
+#   tools/gpu_round.sh bench-hash [k=v...]                        tools/bench_hash.py with knobs (Hash inference + train step)
+#   tools/gpu_round.sh pmc-train                                  PMC passes of the 64-wide training step
 #   tools/gpu_round.sh pmc-hash                                   PMC + kernel trace of tools/bench_hash.py
 #   tools/gpu_round.sh dp-timing                                  2-rank DP timing (tools/gpu_dp_timing.sh)
 #   tools/gpu_round.sh rehearse-dp2                               2 ranks on one GPU through bench.py (tools/rehearse_dp2.sh)
@@ -91,6 +93,16 @@ hash-train-ab)
   held=(); for kv in "$@"; do held+=(--set "$kv"); done
   timeout -k 10 300 python tools/ab_hash_train.py --knob "$knob" --values="$values" "${held[@]}" > "gpurun_out/ab_hash_train_$tag.json" 2> "gpurun_out/ab_hash_train_$tag.err" || { echo "hash train A/B failed"; tail -20 "gpurun_out/ab_hash_train_$tag.err"; exit 4; }
   cat "gpurun_out/ab_hash_train_$tag.json"
+  ;;
+bench-hash)  # tools/bench_hash.py (Hash inference + training step) with optional knobs: bench-hash [name=value ...]
+  kn=(); for kv in "$@"; do kn+=(--knob "$kv"); done
+  timeout -k 10 120 python tools/bench_hash.py --iters 30 "${kn[@]}" > gpurun_out/bench_hash.json || { echo "bench_hash failed"; exit 5; }
+  grep -E "train_step|infer_us" gpurun_out/bench_hash.json
+  ;;
+pmc-train)  # PMC passes of the 64-wide training step (tools/time_train.py)
+  bash tools/gpu_pmc.sh pmc_t16 python3 "$ROOT/tools/time_train.py" --rounds 1 --iters 10 || exit 6
+  python tools/pmc_summary.py gpurun_out/pmc_t16 train > gpurun_out/pmc_t16.txt || exit 7
+  cat gpurun_out/pmc_t16.txt
   ;;
 pmc-hash)
   bash tools/gpu_pmc.sh pmc_hash python3 "$ROOT/tools/bench_hash.py" --iters 5 || exit 6
