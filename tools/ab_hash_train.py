@@ -35,7 +35,7 @@ def main() -> None:
         nrc._lib.set_knob(k, int(v))
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
-    vals = [int(v) for v in args.values.split(",")]
+    vals = list(dict.fromkeys(int(v) for v in args.values.split(",")))  # one network per distinct value
     nets = {}
     for v in vals:
         n = nrc.Network()
