@@ -649,6 +649,10 @@ void wide_grad_partials(nrc_net* net, const float* in, const float* tgt, uint32_
 }
 
 int t16_groups() { return knob(kKnobT16Groups) == 1 ? 1 : 2; }
+// Hash: 64-sample blocks by default (every CU at 16,384 samples; the doubled MLP slabs are reduced inside the merged
+// optimizer launch, beside the grid Adam): step 48.6 vs 50.0 us (profiles/r05_hash/ab_hash_t16_groups.json); knob
+// t16_groups = 2 keeps 128-sample blocks
+int hash_t16_groups() { return knob(kKnobT16Groups) == 2 ? 2 : 1; }
 
 // dc shape of a b-sample step (train_shape knob, else by batch size)
 int dc_shape(uint32_t b) {
@@ -658,7 +662,10 @@ int dc_shape(uint32_t b) {
 
 // training blocks = weight-gradient slabs of a b-sample step of this handle's training kernel
 int train_block_count(const nrc_net* net, uint32_t b) {
-    if (net->t16 && net->hash()) return (int)((b + 127u) / 128u);  // the role-split kernel, 128 samples per block
+    if (net->t16 && net->hash()) {  // the role-split kernel, 64 x hash_t16_groups() samples per block
+        const uint32_t S = 64u * (uint32_t)hash_t16_groups();
+        return (int)((b + S - 1) / S);
+    }
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0) {
         const int S = dc_samples_per_block(dc_shape(b));
         if (S <= 0) throw ApiError(NRC_ERR_INVALID_ARGUMENT, "train_shape knob names no decoupled-chain shape");
@@ -703,7 +710,7 @@ void train_hash(nrc_net* net, const float* in, const float* tgt, uint32_t b, flo
     if (feat) net->hash_feat_acquire(net->stream);
     HIP_CHECK(launch_train_hash(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train, net->table_train,
                                 net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                net->step_scatter(blocks, part), net->padq(), net->t16, feat));
+                                net->step_scatter(blocks, part), net->padq(), net->t16, feat, hash_t16_groups()));
     if (feat) net->hash_feat_release(net->stream);
 }
 

@@ -350,7 +350,7 @@ struct HashTrainOut {
 };
 hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                                const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
-                               const HashTrainOut& ho, hipStream_t s, bool padq = false);
+                               const HashTrainOut& ho, hipStream_t s, bool padq = false, int groups = 2);
 // samples per block of the role-split t16 kernel: 64 x groups (knob "t16_groups"; 128 by default)
 int t16_groups();  // split: the role-split kernel (NRC_T16_SPLIT at init)
 // Decoupled-chain Frequency training kernel (nrc_train_dc.hip, round 3): shape 0..5 (dc_samples_per_block), same f16
@@ -477,7 +477,7 @@ hipError_t launch_infer_stamped(const float* queries, float* out, int64_t n, con
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc = nullptr, bool padq = false,
-                             bool t16 = false, uint32_t* feat = nullptr);
+                             bool t16 = false, uint32_t* feat = nullptr, int groups = 2);
 // the fused Hash step's MLP reduce + Adam and grid Adam (kReduceFused both) in one launch (t16 f16 slabs only)
 hipError_t launch_hash_adam(const float* slabs, int nslabs, const float* loss_partials, float* loss_out,
                             const ModelBuffers& mb, const GridBuffers& gb, const OptimArgs& oa, hipStream_t s);

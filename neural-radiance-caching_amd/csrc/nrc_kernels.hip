@@ -3924,9 +3924,12 @@ __device__ __forceinline__ int64_t f16_to_fixed_fast(uint32_t h) {
 // drain then collide on them at once.
 constexpr int kScatterQueue = 192;  // words per wave: 16 waves x 192 x 8 B = 24 KiB beside the 128-KiB table
 
+// bcap: the workspace's row stride (its capacity; the plan's slices may end before it); b: the step's samples -- the
+// training kernel writes positions and dy for the samples of its blocks only (64-sample blocks may end before the
+// plan's last slice), so the ones past b are not read
 __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const float4* __restrict__ pos,
                                                                        const uint32_t* __restrict__ dy, int64_t bcap,
-                                                                       ScatterPlan plan,
+                                                                       int64_t b, ScatterPlan plan,
                                                                        unsigned long long* __restrict__ grad,
                                                                        GridNonFinite nf, ScatterPartials pt) {
     __shared__ unsigned long long acc[kScatterPart][2];  // 128 KiB: one block per CU
@@ -3942,7 +3945,7 @@ __global__ __launch_bounds__(kScatterThreads) void grid_scatter_kernel(const flo
     const uint32_t e0 = (uint32_t)part * kScatterPart;
     const uint32_t ne = min((uint32_t)kScatterPart, lsize - e0);
     const uint32_t* dyl = dy + (int64_t)level * bcap;
-    const int64_t s1 = min(bcap, s0 + slice);
+    const int64_t s1 = min(min(bcap, b), s0 + slice);
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t* const q = queue[threadIdx.x >> 6];
     uint32_t qn = 0;  // words in this wave's queue (wave-uniform)
@@ -4102,11 +4105,13 @@ ScatterPartials scatter_partials_layout(int64_t b, int first_level) {
 hipError_t launch_train_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                              const _Float16* wf, const _Float16* wb, const _Float16* grid, int64_t* grid_grad,
                              float* slabs, float* loss_partials, hipStream_t s, const HashScatter* sc, bool padq,
-                             bool t16, uint32_t* feat) {
+                             bool t16, uint32_t* feat, int groups) {
     if (b <= 0) return hipSuccess;
     const int blocks = train_blocks(b);
-    const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock;
-    if (!sc || !sc->pos || !sc->dy || sc->bcap < bcap || !sc->nf.codes || !sc->nf.tag_dev || !sc->nf.tag)
+    // bcap: the samples the scatter plan covers (128-sample blocks); the workspace's row stride is its capacity
+    // sc->bcap (>= bcap), the same for every writer and reader (nrc_debug_hash_scatter_inputs too)
+    const int64_t bcap = (int64_t)blocks * kTrainSamplesPerBlock, stride = sc ? sc->bcap : 0;
+    if (!sc || !sc->pos || !sc->dy || stride < bcap || !sc->nf.codes || !sc->nf.tag_dev || !sc->nf.tag)
         return hipErrorInvalidValue;
     if (t16) {  // round 5: the t16 role-split kernel (nrc_train16.hip), f16 slabs in the t16 layout
         const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
@@ -4123,17 +4128,18 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
         }
         const hipError_t e = launch_train16_hash(queries, targets, b, n_total, loss_scale, wf, wb,
                                                  reinterpret_cast<_Float16*>(slabs), loss_partials,
-                                                 HashTrainOut{g, fp ? feat : nullptr, sc->pos, sc->dy, bcap}, s, padq);
+                                                 HashTrainOut{g, fp ? feat : nullptr, sc->pos, sc->dy, stride}, s, padq,
+                                                 groups);
         if (e != hipSuccess) return e;
     } else if (padq)
         hipLaunchKernelGGL((train_kernel<false, 1, true>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
                            loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
-                           reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy, bcap);
+                           reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy, stride);
     else
         hipLaunchKernelGGL((train_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
                            loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,
                            reinterpret_cast<const uint32_t*>(grid), nullptr, sc->pos, sc->dy,
-                           bcap);
+                           stride);
     // tuning overrides (A/B knobs scatter_min / scatter_max); defaults from the sweep of the exact 64-bit scatter,
     // profiles/r03_hash/scatter_plan_sweep.txt (round 1's f16 scatter: profiles/r01_hash/README.md)
     int nb = 0;
@@ -4145,7 +4151,7 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
         for (int l = 0; l < NRC_HASH_LEVELS; ++l)
             if (want.off[l] != sc->part.off[l] || want.nslice[l] != sc->part.nslice[l]) return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(grid_scatter_kernel, dim3(nb), dim3(kScatterThreads), 0, s, sc->pos, sc->dy, bcap, plan,
+    hipLaunchKernelGGL(grid_scatter_kernel, dim3(nb), dim3(kScatterThreads), 0, s, sc->pos, sc->dy, stride, b, plan,
                        reinterpret_cast<unsigned long long*>(grid_grad), sc->nf, sc->part);
     return hipGetLastError();
 }

@@ -897,11 +897,22 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
 
 hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                                const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
-                               const HashTrainOut& ho, hipStream_t s, bool padq) {
+                               const HashTrainOut& ho, hipStream_t s, bool padq, int groups) {
     if (b <= 0) return hipSuccess;
     if (!ho.table || !ho.pos || !ho.dy || ho.bcap < (int64_t)t16_blocks(b) * 128) return hipErrorInvalidValue;
     const dim3 grid(t16_blocks(b)), block(128 * kWaves);
     const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
+    if (groups == 1) {  // 64-sample blocks (A/B, knob t16_groups = 1): every CU at 16,384 samples, twice the slabs
+        if (!ho.feat) return hipErrorNotSupported;
+        const dim3 g1(t16_blocks(b, 1));
+        if (padq)
+            hipLaunchKernelGGL((train16_split_kernel<16, 1, true, 3>), g1, block, 0, s, queries, targets, b, n_total,
+                               loss_scale, f, bw, slabs, loss_partials, ho);
+        else
+            hipLaunchKernelGGL((train16_split_kernel<16, 1, false, 3>), g1, block, 0, s, queries, targets, b, n_total,
+                               loss_scale, f, bw, slabs, loss_partials, ho);
+        return hipGetLastError();
+    }
     if (ho.feat && padq)
         hipLaunchKernelGGL((train16_split_kernel<16, 2, true, 3>), grid, block, 0, s, queries, targets, b, n_total,
                            loss_scale, f, bw, slabs, loss_partials, ho);
