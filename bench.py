@@ -9,13 +9,18 @@ into 16,384 / N per rank with the gradient all-reduced over RCCL INSIDE the libr
 global batch 16,384, the reference's per-step semantics). The weak-scaling figures (2^21 queries per GPU) are kept
 as the extra key ``weak``.
 
-Launch: ``python bench.py [--gpus N --steps K --warmup W]``; N > 1 under torch.distributed.run.
+Launch: ``python bench.py [--gpus N --steps K --warmup W]``. N > 1 either under torch.distributed.run (WORLD_SIZE set) or
+on its own: with WORLD_SIZE unset the process starts N fresh child processes of itself (one rank per GPU, RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in their environment) before it makes any GPU call, passes rank 0's
+JSON line through and exits non-zero if any rank fails (``launch_ranks``).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -35,7 +40,7 @@ FLOP_PER_QUERY_WIDE = 2 * (66 * 128 + 4 * 128 * 128 + 128 * 3)  # 148,736 (SURVE
 PEAK_HBM_GBS = 8000.0
 QUERIES_PER_GPU = 1 << 21
 QUERIES_C4 = 1 << 22  # configs[3]: the 2K frame, sharded over the ranks
-ROUND = "r05"
+ROUND = "r06"
 
 
 def parse():
@@ -333,6 +338,45 @@ def graph_ms_per_call(net, stream, fn, k: int, reps: int) -> float:
     return e0.elapsed_time(e1) / (k * reps)
 
 
+def c4_frame_n1(nrc, net, dev, steps: int, warmup: int, barrier) -> dict:
+    """configs[3]'s workload at N = 1: the 2K frame's 2^22 queries (the same seeded frame the N > 1 ranks shard,
+    bench.main) through one GPU's inference, K timed steps between barriers; `value` comparable to the N > 1 line's."""
+    import torch
+
+    stream = torch.cuda.current_stream()
+    n = QUERIES_C4
+    q = torch.from_numpy(nrc.synthetic.cornell_queries(n, seed=nrc.synthetic.SEED)).to(dev)
+    out = torch.empty((n, 3), dtype=torch.float32, device=dev)
+    # clock settle as main()'s: making the frame leaves the GPU idle for seconds, and a first round's 20 + 50 launches
+    # then ran inside the clock ramp (185 us per 2^22 launch against 156 settled; tools/mall_probe.py)
+    settled = 0.0
+    while settled < 60.0:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(25):
+            net.infer(q, out, n)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        settled += e0.elapsed_time(e1)
+    for _ in range(max(warmup, 5)):
+        net.infer(q, out, n)
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        net.infer(q, out, n)
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kms = ev0.elapsed_time(ev1) / steps
+    del q, out
+    return {"workload": "configs[3] at N = 1: the 2K frame's 2^22 queries on one GPU (measured, not extrapolated)",
+            "queries": n, "steps": steps, "value": n * steps / wall / 1e6, "unit": "M queries/s",
+            "ms_per_step": wall / steps * 1e3, "kernel_ms": kms,
+            "frac": FLOP_PER_QUERY * n / (kms * 1e-3) / 1e12 / PEAK_F16_TFLOPS}
+
+
 def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_ms: float, step16k_ms: float) -> dict:
     """configs[3] (C4) per-rank work, measured on ONE GPU: what each of the 8 ranks runs.
     Inference: its 2^19-query shard (no collective). Training: one 2,048-sample slice of a 16,384-sample global
@@ -408,8 +452,8 @@ def c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, iters: int, t_full_m
                                        "per-call host cost (Python, ctypes, one hipLaunchKernel per kernel)"},
             "prediction_8gpu": {
                 "infer_speedup": (t_full_ms / infer_ms) if infer_ms > 0 else None,
-                "infer_what": "1-GPU kernel time of the whole 2^22-query frame / per-rank 2^19-query kernel time "
-                              "(no collective on the inference path)",
+                "infer_what": "measured 1-GPU kernel time of the whole 2^22-query frame (c4_n1) / per-rank "
+                              "2^19-query kernel time (no collective on the inference path)",
                 "xgmi_us_assumed": xgmi_assumed_us,
                 "train_step_ms_8gpu": dp_step + xgmi_assumed_us * 1e-3,
                 "train_speedup": step16k_ms / (dp_step + xgmi_assumed_us * 1e-3),
@@ -515,17 +559,89 @@ def power_window(smp, t0: float, t1: float, achieved_tflops: float) -> dict | No
 
 
 def pmc_traffic() -> float | None:
-    f = ROOT / "profiles" / f"pmc_infer_{ROUND}.json"
-    if f.exists():
+    """HBM bytes per headline launch from the newest committed PMC summary (this round's, else the latest before)."""
+    files = sorted(p for p in (ROOT / "profiles").glob("pmc_infer_r*.json") if p.stem.split("_")[-1] <= ROUND)
+    for f in reversed(files):
         try:
             return float(json.loads(f.read_text())["hbm_bytes_per_launch"])
         except Exception:
-            return None
+            continue
     return None
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def rank_env(base: dict, world: int, rank: int, port: int) -> dict:
+    """The environment of rank `rank` of a self-launched world (the variables torch.distributed.run sets)."""
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_WORLD_SIZE": str(world),
+                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "GROUP_RANK": "0"})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the peer exchange's buffer export)
+    return env
+
+
+def launch_ranks(cmd: list[str], world: int, port: int | None = None, poll_s: float = 0.05,
+                 timeout_s: float | None = None) -> int:
+    """Run `cmd` as `world` child processes, one per rank, and wait for them. Children inherit stdout / stderr (only
+    rank 0 prints the JSON line). The first child to fail takes the others down (a rank blocked in a barrier would
+    otherwise wait forever): they are terminated by their own Popen handles, then killed. Returns 0 if every rank
+    exited 0, else the first failing rank's exit code (a signal -> 128 + signal number), never 0."""
+    port = port or free_port()
+    procs = [subprocess.Popen(cmd, env=rank_env(os.environ, world, r, port)) for r in range(world)]
+    t0 = time.monotonic()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                return 0
+            if timeout_s is not None and time.monotonic() - t0 > timeout_s:
+                rc = 124
+                break
+            time.sleep(poll_s)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.terminate()
+        for p in live:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return 128 - rc if rc < 0 else rc
+
+
+def self_launch(args) -> int | None:
+    """--gpus N > 1 without a launcher (WORLD_SIZE unset): N fresh children of this script. Called before anything
+    touches the GPU; torch.cuda.device_count() does not initialise HIP on this image. None: run in this process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    if args.dist_backend == "nccl":
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} with the nccl (RCCL) backend needs {args.gpus} visible GPUs, "
+                  f"found {have} (one rank per GPU; --dist-backend gloo rehearses ranks sharing a GPU)",
+                  file=sys.stderr, flush=True)
+            return 2
+    return launch_ranks([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], args.gpus)
 
 
 def main() -> None:
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        raise SystemExit(rc)
     import torch
     import torch.distributed as dist
 
@@ -716,11 +832,15 @@ def main() -> None:
                      "M_queries_per_s": nq / (s_ms * 1e-3) / 1e6,
                      "power": power_window(sampler, t_s0, t_s1, s_tf)}
 
-    # ---- configs[3] per-rank work on one GPU (C4): 2^19-query shard + 2048-sample slices through nrc_train_dp
+    # ---- configs[3] at N = 1, measured: the whole 2^22-query 2K frame on this one GPU, timed
+    # exactly as the N > 1 line times its shards (K steps, barrier + synchronize on both sides, wall clock), so the
+    # 1 -> N strong-scaling ratio is read on one workload; then the per-rank work of 8 GPUs on one GPU
+    c4_n1 = None
     c4_per_rank = None
     if world == 1 and not args.no_c4:
+        c4_n1 = c4_frame_n1(nrc, net, dev, args.steps, args.warmup, barrier)
         c4_per_rank = c4_per_rank_bench(nrc, net, dev, q, frames_q, frames_t, max(10, args.steps // 4),
-                                         kernel_ms * QUERIES_C4 / nq, train_step_ms)
+                                         c4_n1["kernel_ms"], train_step_ms)
 
     # ---- one whole post-trace frame: fused infer+accumulate over the 1080p frame's
     # render + train-suffix queries, propagate, shuffle, 4 x train with the minibatch-loss read-back (1 GPU)
@@ -764,6 +884,7 @@ def main() -> None:
         "infer_kernel_ms": kernel_ms,
         "weak": weak,
         "settle": settle,
+        "c4_n1": c4_n1,
         "c4_per_rank": c4_per_rank,
         "dp_exchange": dp_exchange,
         "frame": frame,
