@@ -189,6 +189,11 @@ nrc_status nrc_get_comm_rank(const nrc_net* net, int* rank, int* world);
  * (b_local may be 0). loss_h: the global minibatch loss (blocking, as nrc_train). Requires an attached comm. */
 nrc_status nrc_train_dp(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b_local,
                         uint32_t global_b, float* loss_h);
+/* nrc_train_dp whose global minibatch loss goes to device memory loss_d (may be NULL); never blocks. The form for one
+ * host thread driving several in-process ranks round-robin (nrc_peer_exchange_open_local): a blocking loss read on
+ * rank 0 would wait for a step that needs its peers' words, which the same thread has not issued yet. */
+nrc_status nrc_train_dp_async(nrc_net* net, const float* inputs_d, const float* targets_d, uint32_t b_local,
+                              uint32_t global_b, float* loss_d);
 
 /* One-shot peer exchange (round 4; width-64 Frequency / FrequencySH): instead of an RCCL all-reduce, each rank stores
  * its gradient straight into a receive buffer of every peer over xGMI (IPC-mapped uncached device memory) and releases
@@ -208,9 +213,13 @@ nrc_status nrc_peer_exchange_close(nrc_net* net);
  * renderer keeps one Device per GPU in one process, or several on one device. nets[r] becomes rank r; each
  * handle's receive buffer is allocated on its own device and the others store into it through plain device pointers
  * (peer access enabled between the devices; no IPC). Replaces any exchange the handles had open. The handles share
- * each other's buffers: close every one of them (after its last step) before destroying any. Handles on one device
+ * each other's buffers, so they form one group: nrc_peer_exchange_close or nrc_destroy on any member, or a new open
+ * that takes a member, waits for every member's stream and closes the exchange of all of them. Handles on one device
  * take the split form of the exchange (nrc_train_dp of each must then run on its own stream, since a rank's wait
- * completes only after its peers have pushed); on separate devices the fused form. */
+ * completes only after its peers have pushed); on separate devices the fused form. A single host thread that issues the
+ * ranks' steps round-robin must not block on a loss inside the round (nrc_train_dp's loss_h, nrc_process_frame_shard's
+ * loss): rank 0's step completes only once every peer's step has been issued. Use nrc_train_dp_async and read the
+ * losses after the round, or one host thread per rank. */
 nrc_status nrc_peer_exchange_open_local(nrc_net* const* nets, int world);
 
 /* ---- state access (host buffers of nrc_get_num_params() f32; synchronous) ----

@@ -45,7 +45,7 @@ EXPORTS = [
     "nrc_get_stream", "nrc_set_hyper_params", "nrc_set_config", "nrc_get_learning_rate", "nrc_get_config_json",
     "nrc_train_grad", "nrc_train_apply", "nrc_train_grad_fixed", "nrc_train_apply_fixed", "nrc_get_num_params", "nrc_get_grad_floats", "nrc_get_state", "nrc_set_state", "nrc_get_step",
     "nrc_set_step", "nrc_debug_encode_net",
-    "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp",
+    "nrc_comm_get_unique_id", "nrc_comm_init_rank", "nrc_comm_destroy", "nrc_set_comm", "nrc_get_comm_rank", "nrc_train_dp", "nrc_train_dp_async",
     "nrc_peer_exchange_handle", "nrc_peer_exchange_open", "nrc_peer_exchange_close", "nrc_peer_exchange_open_local",
     "nrc_encode", "nrc_debug_infer_variant", "nrc_debug_read_infer_clock", "nrc_debug_train_stamps", "nrc_debug_hash_scatter_inputs", "nrc_debug_infer_stamps", "nrc_debug_encode_fast",
     "nrc_debug_encode_fast_variant", "nrc_debug_infer_precision", "nrc_debug_fp8_convert", "nrc_debug_set_knob",
@@ -135,6 +135,7 @@ def lib() -> ctypes.CDLL:
         "nrc_set_comm": (st, [vp, vp]),
         "nrc_get_comm_rank": (st, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
         "nrc_train_dp": (st, [vp, fp, fp, u32, u32, ctypes.POINTER(ctypes.c_float)]),
+        "nrc_train_dp_async": (st, [vp, fp, fp, u32, u32, fp]),
         "nrc_peer_exchange_handle": (st, [vp, ctypes.c_int, vp]),
         "nrc_peer_exchange_open": (st, [vp, ctypes.c_int, ctypes.c_int, vp]),
         "nrc_peer_exchange_close": (st, [vp]),

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -263,12 +264,12 @@ bool want_t16(int encoding) {
     return encoding == NRC_ENCODING_FREQUENCY || encoding == NRC_ENCODING_HASH;
 }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
                                             "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path",
                                             "px_polls", "scatter_part", "scatter_compact", "hash_train_feat",
-                                            "hash_adam"};
-static_assert(kKnobCount == 15, "one initial value and one name per knob");
+                                            "hash_adam", "train_fused", "fuse_mode"};
+static_assert(kKnobCount == 17, "one initial value and one name per knob");
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -322,6 +323,15 @@ std::string config_json(int encoding, const nrc_config& c) {
 
 }  // namespace
 
+struct nrc_net;
+// nrc_peer_exchange_open_local: the handles of one in-process exchange group, each holding raw pointers to the others'
+// receive buffers. Every member owns the group; closing any member (nrc_peer_exchange_close, nrc_destroy, a new open on
+// a subset) closes all of them after syncing every member's stream, so no handle keeps a pointer to a freed buffer
+// (ADVICE r05).
+struct LocalPeerGroup {
+    std::vector<nrc_net*> members;
+};
+
 struct nrc_net {
     hipStream_t stream = nullptr;
     int encoding = NRC_ENCODING_FREQUENCY;
@@ -338,6 +348,14 @@ struct nrc_net {
     int *fwd_pos = nullptr, *bwd_pos = nullptr;
     int* fwdt_pos = nullptr;  // t16 training layout only (else the training image is laid out as fwd_pos)
     bool t16 = false;         // Frequency training in the t16 layout (f16 slabs)
+    // round 6: the role-split step as one launch (launch_train16_fused; knob train_fused, read at nrc_init) and its
+    // reducers' counters
+    bool fused = false;
+    uint32_t* fuse_sync = nullptr;
+    uint32_t* fuse_flags = nullptr;  // [kFuseMaxFlags] per trainer block: the generation of its last fused launch
+    uint32_t fuse_gen = 0;
+    // the next launch's generation: never 0 (the flags' initial value) and never the previous launch's
+    uint32_t next_fuse_gen() { return fuse_gen = fuse_gen == 0xFFFFFFFFu ? 1u : fuse_gen + 1u; }
     int t16_kernel = 0;       // 0 decoupled chain (nrc_train_dc.hip, default), 1 / 2 round-2 role split / 4-wave
                               // (nrc_train16.hip); the train_kernel knob at nrc_init
     int* slab_param = nullptr;  // [n_slab] parameter of each weight-gradient slab position
@@ -382,7 +400,10 @@ struct nrc_net {
     bool px_shared = false;   // a peer's buffer lives on this rank's device (ranks sharing a GPU): split exchange
     bool px_local = false;    // nrc_peer_exchange_open_local: the peers' buffers are other handles' own (no IPC)
     bool px_pending = false;  // knob peer_path 3 pushed a step whose wait + sum + Adam (peer_path 4) is still to run
-    void peer_close() {
+    std::shared_ptr<LocalPeerGroup> px_group;  // open_local: the group this handle's exchange belongs to
+    void peer_close();        // this handle's exchange, and with it its whole local group (defined below)
+    void peer_close_own() {
+        px_group.reset();
         if (px_open && !px_local)
             for (int r = 0; r < px_world; ++r)
                 if (r != px_rank && px_peers.p[r]) (void)hipIpcCloseMemHandle(px_peers.p[r]);
@@ -528,6 +549,12 @@ struct nrc_net {
         grid_bias = nullptr;
         table_train = table_infer = nullptr;
         if (loss_host) (void)hipHostFree(loss_host);
+        f(fuse_sync);
+        f(fuse_flags);
+        fuse_sync = nullptr;
+        fuse_flags = nullptr;
+        fuse_gen = 0;
+        fused = false;
         params = m = v = ema = infer = nullptr;
         wf_train = wb_train = wf_infer = wf_infer16 = nullptr;
         fwd_pos = bwd_pos = fwdt_pos = nullptr;
@@ -613,6 +640,23 @@ struct nrc_net {
     }
 };
 
+void nrc_net::peer_close() {
+    if (!px_group) {
+        peer_close_own();
+        return;
+    }
+    // a local group: no member may still have a step in flight that stores into a buffer about to be freed
+    const std::shared_ptr<LocalPeerGroup> g = px_group;
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (nrc_net* n : g->members) {
+        (void)hipSetDevice(n->device);
+        (void)hipStreamSynchronize(n->stream);
+    }
+    for (nrc_net* n : g->members) n->peer_close_own();
+    if (have_cur) (void)hipSetDevice(cur);
+}
+
 namespace {
 
 void check_live(const nrc_net* net) {
@@ -653,6 +697,11 @@ int t16_groups() { return knob(kKnobT16Groups) == 1 ? 1 : 2; }
 // optimizer launch, beside the grid Adam): step 48.6 vs 50.0 us (profiles/r05_hash/ab_hash_t16_groups.json); knob
 // t16_groups = 2 keeps 128-sample blocks
 int hash_t16_groups() { return knob(kKnobT16Groups) == 2 ? 2 : 1; }
+// the Hash training kernel's feature source: the handle's feature workspace (batches of any size, in chunks of
+// kHashFeatStride samples), or -- knob hash_infer = 1, compact records only -- the gathering encoder, which exists in the
+// 128-sample block shape only (that knob used to fail under the 64-sample default)
+bool hash_train_gathers(const nrc_net* net) { return knob(kKnobHashInfer) == 1 && !net->padq(); }
+int hash_train_groups(const nrc_net* net) { return hash_train_gathers(net) ? 2 : hash_t16_groups(); }
 
 // dc shape of a b-sample step (train_shape knob, else by batch size)
 int dc_shape(uint32_t b) {
@@ -662,8 +711,8 @@ int dc_shape(uint32_t b) {
 
 // training blocks = weight-gradient slabs of a b-sample step of this handle's training kernel
 int train_block_count(const nrc_net* net, uint32_t b) {
-    if (net->t16 && net->hash()) {  // the role-split kernel, 64 x hash_t16_groups() samples per block
-        const uint32_t S = 64u * (uint32_t)hash_t16_groups();
+    if (net->t16 && net->hash()) {  // the role-split kernel, 64 x hash_train_groups() samples per block
+        const uint32_t S = 64u * (uint32_t)hash_train_groups(net);
         return (int)((b + S - 1) / S);
     }
     if (net->t16 && net->t16_kernel == 0 && dc_shape(b) >= 0) {
@@ -676,6 +725,26 @@ int train_block_count(const nrc_net* net, uint32_t b) {
         return (int)((b + S - 1) / S);
     }
     return train_blocks(b);
+}
+
+// round 6: a b-sample step of this handle runs as one launch (launch_train16_fused) when it would run on the role-split
+// kernel with 128-sample blocks (not the decoupled-chain shapes of small batches, no stamps)
+// Not while the stream is being captured into a graph: the launch's generation is a host counter, and a graph would
+// replay the same value (a reducer could then take a previous replay's flags for this one's); captured steps take the
+// two launches.
+bool fused_step(const nrc_net* net, uint32_t b) {
+    if (!net->fused || (net->t16_kernel == 0 && dc_shape(b) >= 0) || t16_groups() != 2) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(net->stream, &cs) != hipSuccess) return false;
+    return cs == hipStreamCaptureStatusNone;
+}
+int fuse_mode() { const int k = knob(kKnobFuseMode); return k < 0 ? 0 : k; }
+constexpr int kFuseMaxFlags = 1024;  // trainer blocks of one fused launch (CU-bound anyway)
+constexpr int kFusePolls = 1 << 21;  // the reducers' bounded wait (~2 s: a trainer step takes ~10 us)
+int device_cus(const nrc_net* net) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, net->device) != hipSuccess || v <= 0) v = 256;
+    return v;
 }
 
 // 64-wide Frequency / FrequencySH fwd + loss + bwd + per-block dW slabs (n_total = 3 x global batch)
@@ -706,11 +775,11 @@ void train_partials(nrc_net* net, const float* in, const float* tgt, uint32_t b,
 // part: the fused step's partial sums (do_train; the next grid_adam_kernel consumes them), else none (grad64 only).
 void train_hash(nrc_net* net, const float* in, const float* tgt, uint32_t b, float n_total, int blocks,
                 const ScatterPartials& part = ScatterPartials{}) {
-    uint32_t* const feat = net->t16 && knob(kKnobHashInfer) != 1 ? net->hash_feat : nullptr;
+    uint32_t* const feat = net->t16 && !hash_train_gathers(net) ? net->hash_feat : nullptr;
     if (feat) net->hash_feat_acquire(net->stream);
     HIP_CHECK(launch_train_hash(in, tgt, b, n_total, net->cfg.loss_scale, net->wf_train, net->wb_train, net->table_train,
                                 net->grid_grad, net->slabs, net->loss_partials, net->stream,
-                                net->step_scatter(blocks, part), net->padq(), net->t16, feat, hash_t16_groups()));
+                                net->step_scatter(blocks, part), net->padq(), net->t16, feat, hash_train_groups(net)));
     if (feat) net->hash_feat_release(net->stream);
 }
 
@@ -751,6 +820,21 @@ void do_train(nrc_net* net, const float* in, const float* tgt, uint32_t b, float
         HIP_CHECK(launch_grid_adam(kReduceFused, net->grid_buffers(part), net->optim(net->step), net->stream));
         if (loss_h) *loss_h = net->read_loss();
         return;
+    }
+    if (fused_step(net, b)) {
+        net->check_protocol();
+        const hipError_t e = launch_train16_fused(in, tgt, b, 3.0f * (float)b, net->cfg.loss_scale, net->wf_train,
+                                                  net->wb_train, reinterpret_cast<_Float16*>(net->slabs),
+                                                  net->loss_partials, net->fuse_sync, net->proto_err_dev(), kFusePolls,
+                                                  loss_d ? loss_d : net->loss_dev, net->buffers(),
+                                                  net->optim(net->step + 1), net->stream, net->padq(), device_cus(net),
+                                                  fuse_mode(), net->next_fuse_gen(), net->fuse_flags, kFuseMaxFlags);
+        if (e != hipErrorNotSupported) {
+            HIP_CHECK(e);
+            net->step += 1;
+            if (loss_h) *loss_h = net->read_loss();
+            return;
+        }
     }
     train_partials(net, in, tgt, b, 3.0f * (float)b);
     net->step += 1;
@@ -916,6 +1000,8 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobScatterCompact: return v >= -1 && v <= NRC_HASH_LEVELS;
         case kKnobHashTrainFeat: return v >= -1 && v <= 1;
         case kKnobHashAdam: return v >= -1 && v <= 0;
+        case kKnobTrainFused: return v >= -1 && v <= 1;
+        case kKnobFuseMode: return v >= -1 && v <= 4;
         default: return false;
     }
 }
@@ -1101,6 +1187,14 @@ nrc_status nrc_init(nrc_net* net, hipStream_t stream, int encoding, const nrc_co
             // 4-wave t16 kernels (in-process A/B)
             const int k = knob(kKnobTrainKernel);
             net->t16_kernel = (k == 1 || (k == 2 && NRC_DEBUG_KERNELS)) ? k : 0;
+        }
+        net->fused = net->t16 && net->encoding == NRC_ENCODING_FREQUENCY && net->t16_kernel != 2 &&
+                     knob(kKnobTrainFused) == 1;
+        if (net->fused) {
+            HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&net->fuse_sync), 512, hipDeviceMallocUncached));
+            HIP_CHECK(hipMemset(net->fuse_sync, 0, 512));
+            HIP_CHECK(hipMalloc(&net->fuse_flags, sizeof(uint32_t) * kFuseMaxFlags));
+            HIP_CHECK(hipMemset(net->fuse_flags, 0, sizeof(uint32_t) * kFuseMaxFlags));
         }
         if (net->t16) {
             std::vector<int> fwdt;
@@ -1587,6 +1681,11 @@ nrc_status nrc_train_dp(nrc_net* net, const float* in, const float* tgt, uint32_
     return guarded([&] { do_train_dp(net, in, tgt, b_local, global_b, loss_h, nullptr); });
 }
 
+nrc_status nrc_train_dp_async(nrc_net* net, const float* in, const float* tgt, uint32_t b_local, uint32_t global_b,
+                              float* loss_d) {
+    return guarded([&] { do_train_dp(net, in, tgt, b_local, global_b, nullptr, loss_d); });
+}
+
 nrc_status nrc_peer_exchange_handle(nrc_net* net, int world, void* handle_out) {
     return guarded([&] {
         check_live(net);
@@ -1702,8 +1801,11 @@ nrc_status nrc_peer_exchange_open_local(nrc_net* const* nets, int world) {
         }
         PeerPtrs p{};
         for (int r = 0; r < world; ++r) p.p[r] = nets[r]->px_buf;
+        auto group = std::make_shared<LocalPeerGroup>();
+        group->members.assign(nets, nets + world);
         for (int r = 0; r < world; ++r) {
             nrc_net* n = nets[r];
+            n->px_group = group;
             bool shared = false;
             for (int q = 0; q < world; ++q) shared = shared || (q != r && nets[q]->device == n->device);
             n->px_peers = p;

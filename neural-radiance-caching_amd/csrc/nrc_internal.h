@@ -337,6 +337,16 @@ struct ModelBuffers {
 hipError_t launch_train16(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
                           const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials, uint64_t* stamps,
                           hipStream_t s, bool split = false, int groups = 2, bool padq = false);
+// Round 6: one launch for the whole width-64 Frequency step of the role-split kernel (128-sample blocks): trainer
+// blocks + reducer blocks that wait for them on the counters at sync (2 x 256 B, zero at allocation) and then run
+// kReduceFused's sums and Adam/EMA from agent-scope loads of the slabs -- state bitwise the same as
+// launch_train16 + launch_reduce_adam. hipErrorNotSupported when trainers + reducers exceed max_blocks (the CU count).
+// err: the handle's protocol word (3 = the reducers' bounded wait gave up).
+hipError_t launch_train16_fused(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                                const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
+                                uint32_t* sync, uint32_t* err, int polls, float* loss_out, const ModelBuffers& mb,
+                                const OptimArgs& oa, hipStream_t s, bool padq, int max_blocks, int mode,
+                                uint32_t gen, uint32_t* flags, int max_flags);
 // InputEncoding::Hash on the t16 role-split kernel (round 5): the encoder reads levels 4g .. 4g + 3 from the feature
 // pass's workspace (or gathers them from the f16 training table); the chain waves also write each sample's position and its 16 levels' (dy0, dy1) = W0^T delta_0 of the
 // grid features (f16 pairs, [level][sample], zeros past b) for grid_scatter_kernel. wb: kT16BwdFragsHash fragments.
@@ -386,7 +396,12 @@ enum Knob : int {
     kKnobScatterCompact = 12, // Hash training: first grid level whose scatter queues its in-part corners (-1 default, 0..16)
     kKnobHashTrainFeat = 13,  // Hash training: the batch's level features by 0 the LDS pass, 1 gathers (-1 = 1)
     kKnobHashAdam = 14,       // Hash training: 0 = the MLP and grid optimizer updates as two launches (-1: one)
-    kKnobCount = 15
+    kKnobTrainFused = 15,     // width-64 Frequency step on the role-split kernel: 1 = one launch (launch_train16_fused,
+                              // A/B: 14.4-14.8 vs 12.0 us per step); -1 / 0 the training and
+                              // optimizer kernels as two launches (read at nrc_init)
+    kKnobFuseMode = 16,       // fused step A/B: 0 (-1) per-block flags, 1 / 2 an arrival counter per block / per wave;
+                              // timing ablations (wrong results) 3 no reducers, 4 reducers that only wait
+    kKnobCount = 17
 };
 int knob(Knob k);
 

@@ -4116,21 +4116,33 @@ hipError_t launch_train_hash(const float* queries, const float* targets, int64_t
     if (t16) {  // round 5: the t16 role-split kernel (nrc_train16.hip), f16 slabs in the t16 layout
         const uint32_t* g = reinterpret_cast<const uint32_t*>(grid);
         // the batch's level features first, one level table per block in LDS (hash_feature_kernel, as for inference):
-        // the training kernel's 128 blocks would otherwise gather 2 M table entries at their CUs' L1 line rate
-        const bool fp = feat && b <= kHashFeatStride;
+        // the training kernel's 128 blocks would otherwise gather 2 M table entries at their CUs' L1 line rate.
+        // feat null: the 128-sample gathering encoder (ENC 1, groups 2). A batch larger than the feature workspace
+        // (kHashFeatStride samples) runs in chunks of that many: per chunk the feature pass, then the
+        // training kernel over the chunk's samples with its slabs, loss partials and scatter rows offset -- block i of
+        // chunk c is block c0 / (64 groups) + i of the whole batch, the same slabs as one launch would write.
         // P = 8 query ranges per level (the minimum of the kernel's block map): 16,384-sample step 63.7 us vs 63.9 (16)
         // and 67.8 (32), profiles/r05_hash/
-        if (fp) {
-            // the gather pass by default: fused step 54.3 vs 55.8 us with the LDS pass, parameters bitwise equal
-            // (profiles/r05_hash/ab_train_feature_gather.json)
-            if (knob(kKnobHashTrainFeat) != 0) launch_hash_feature_gather(queries, b, g, feat, padq, s);
-            else launch_hash_feature_pass(queries, b, g, feat, padq, s, 8);
+        if (!feat && (groups != 2 || padq)) return hipErrorNotSupported;  // no padded / 64-sample gathering instance
+        const int64_t chunk = feat ? kHashFeatStride : b;
+        static_assert(kHashFeatStride % 128 == 0, "chunks start on a block boundary of either block size");
+        const int qd = padq ? NRC_INPUT_DIMS_PADDED : NRC_INPUT_DIMS;
+        for (int64_t c0 = 0; c0 < b; c0 += chunk) {
+            const int64_t cnt = std::min<int64_t>(chunk, b - c0);
+            const float* qc = queries + c0 * qd;
+            if (feat) {
+                // the gather pass by default: fused step 54.3 vs 55.8 us with the LDS pass, parameters bitwise equal
+                // (profiles/r05_hash/ab_train_feature_gather.json)
+                if (knob(kKnobHashTrainFeat) != 0) launch_hash_feature_gather(qc, cnt, g, feat, padq, s);
+                else launch_hash_feature_pass(qc, cnt, g, feat, padq, s, 8);
+            }
+            const int64_t blk0 = c0 / (64 * groups);
+            const hipError_t e = launch_train16_hash(
+                qc, targets + c0 * 3, cnt, n_total, loss_scale, wf, wb,
+                reinterpret_cast<_Float16*>(slabs) + blk0 * slab_floats(0), loss_partials + blk0,
+                HashTrainOut{g, feat, sc->pos + c0, sc->dy + c0, stride}, s, padq, groups);
+            if (e != hipSuccess) return e;
         }
-        const hipError_t e = launch_train16_hash(queries, targets, b, n_total, loss_scale, wf, wb,
-                                                 reinterpret_cast<_Float16*>(slabs), loss_partials,
-                                                 HashTrainOut{g, fp ? feat : nullptr, sc->pos, sc->dy, stride}, s, padq,
-                                                 groups);
-        if (e != hipSuccess) return e;
     } else if (padq)
         hipLaunchKernelGGL((train_kernel<false, 1, true>), dim3(blocks), dim3(256), 0, s, queries, targets, b, n_total,
                            loss_scale, (const h8*)wf, (const h8*)wb, slabs, loss_partials, nullptr,

@@ -497,14 +497,14 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // backward image's fragments 36..39, read from global memory) and write it with the sample positions for
 // grid_scatter_kernel (ho). Everything else -- forward, loss, delta chain, dW waves, slab layout -- is the Frequency
 // kernel's.
+// The body takes the block's LDS and index from its kernel (train16_split_kernel, or the fused step's trainer blocks).
 template <int AUX, int G = 2, bool PADQ = false, int ENC = 0>
-__global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
-                                                               int64_t b, float n_total, float loss_scale,
-                                                               const h8* __restrict__ wf, const h8* __restrict__ wb,
-                                                               _Float16* __restrict__ slabs,
-                                                               float* __restrict__ loss_partials, HashTrainOut ho) {
+__device__ __forceinline__ void train16_split_body(char* __restrict__ smem, const int blk,
+                                                   const float* __restrict__ q, const float* __restrict__ t, int64_t b,
+                                                   float n_total, float loss_scale, const h8* __restrict__ wf,
+                                                   const h8* __restrict__ wb, _Float16* __restrict__ slabs,
+                                                   float* __restrict__ loss_partials, const HashTrainOut& ho) {
     const int lane = threadIdx.x & 63;
-    __shared__ __attribute__((aligned(16))) char smem[kLds];
     h8* lwb = (h8*)(smem + kOffWb);
     h8* lwf = (h8*)(smem + kOffWf);
     char* const img_a0 = smem + kOffImg;
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     const bool dw_wave = wave_all >= kWaves;
     const int wave = dw_wave ? wave_all - kWaves : wave_all;
     const int g = lane >> 4, c = lane & 15;
-    _Float16* slab = slabs + (int64_t)blockIdx.x * slab_floats(0);
+    _Float16* slab = slabs + (int64_t)blk * slab_floats(0);
 
     if (dw_wave) {
         // ---- dW waves: the forward's six barriers, then one dW step per backward step
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
 #pragma unroll
     for (int u = 0; u < G; ++u) {
         r[u] = 16 * (G * wave + u) + c;
-        const int64_t s = (int64_t)blockIdx.x * (64 * G) + r[u];
+        const int64_t s = (int64_t)blk * (64 * G) + r[u];
         valid[u] = s < b;
         const int64_t sc = valid[u] ? s : b - 1;
         const float* qr = q + sc * (NRC_INPUT_DIMS + X);
@@ -768,7 +768,8 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
     lds_barrier();  // barrier 6
     if (threadIdx.x == 0) {
         const float lp = (red[0] + red[1]) + (red[2] + red[3]);
-        loss_partials[blockIdx.x] = lp;
+        // an agent-scope store (sc1): the fused step's reducers on other XCDs read it in the same launch
+        __hip_atomic_store(loss_partials + blk, lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     h8 d[G][2], dn[G][2], W[4][2];
@@ -832,7 +833,7 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
         // two features of levels 8 mb + 2 g and 8 mb + 2 g + 1; f16 pairs [level][sample], zeros for padding samples
 #pragma unroll
         for (int u = 0; u < G; ++u) {
-            const int64_t sg = (int64_t)blockIdx.x * (64 * G) + r[u];
+            const int64_t sg = (int64_t)blk * (64 * G) + r[u];
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb) {
                 f4 c = mfma16(W0g[mb][0], d[u][0], f4{0.f, 0.f, 0.f, 0.f});
@@ -843,6 +844,185 @@ __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __re
             }
             if (g == 0) ho.pos[sg] = float4{pq[u].x, pq[u].y, pq[u].z, 0.0f};
         }
+    }
+}
+
+template <int AUX, int G = 2, bool PADQ = false, int ENC = 0>
+__global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
+                                                               int64_t b, float n_total, float loss_scale,
+                                                               const h8* __restrict__ wf, const h8* __restrict__ wb,
+                                                               _Float16* __restrict__ slabs,
+                                                               float* __restrict__ loss_partials, HashTrainOut ho) {
+    __shared__ __attribute__((aligned(16))) char smem[kLds];
+    train16_split_body<AUX, G, PADQ, ENC>(smem, blockIdx.x, q, t, b, n_total, loss_scale, wf, wb, slabs, loss_partials,
+                                          ho);
+}
+
+// ---- Round 6: the whole Frequency training step in one launch ----------------------------------
+// The step was two launches back to back: train16_split_kernel (128 blocks of 128 samples, one per CU: half the chip idle)
+// and reduce_adam_kernel (the fixed-order slab sums + Adam/EMA), and the second paid a kernel boundary and its own ramp
+// after the first had ended. Here the first ntrain blocks of one grid are the training kernel's blocks and the next nred
+// blocks are reducers: dispatched after every trainer block (workgroups dispatch in order), they land on the idle CUs
+// (a block holds a whole CU's LDS, so a reducer never shares a trainer's CU), load their parameters' Adam state, and wait
+// until every trainer wave has counted itself in. Each trainer wave counts in after s_waitcnt vmcnt(0): its slab and loss
+// stores have completed, and they are agent-scope (sc1) stores, so every reducer on any XCD reads them with agent-scope
+// loads (the memory model's relaxed atomics: coherent across the XCDs' L2s, no cache writeback or invalidate). A reducer then sums the slabs and applies Adam/EMA with exactly the float
+// operations of reduce_adam_kernel (kReduceFused): 64-position chunks, 16 slab groups of 16 position quads, element k of
+// a group's sequence into a0 / a1 by parity, the 16 groups combined in the same tree; the state is bitwise that of the
+// two-launch step. Reducer rb takes chunks rb, rb + nred, rb + 2 nred (threads 256..511 the middle one), all loads in
+// flight at once. The last reducer past the wait zeroes both counters for the next launch (stream order), so there is no
+// host-side generation and a captured graph replays correctly. The wait is bounded (error word 3 -> NRC_ERR_INTERNAL).
+constexpr int kFuseChunksPerReducer = 3;
+struct FuseArgs {
+    ModelBuffers mb;
+    OptimArgs oa;
+    float lr_t, ema_debias;
+    float* loss_out;
+    uint32_t* sync;  // [0] trainer waves counted in, [64] reducers past the wait (uncached; 0 between launches)
+    uint32_t* err;
+    int polls, ntrain, nred, nchunks;
+    int mode;      // A/B (knob fuse_mode): 0 flags (default), 1 counter arrival per block, 2 counter per wave
+    uint32_t gen;  // mode 0: this launch's generation (host counter, never 0): trainer block i stores it to flags[i]
+    uint32_t* flags;
+};
+
+__device__ __forceinline__ void fuse_reduce(char* __restrict__ smem, const int rb, const _Float16* __restrict__ slabs,
+                                            const float* __restrict__ loss_partials, const FuseArgs& fa) {
+#pragma clang fp contract(off)
+    const ModelBuffers& mb = fa.mb;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (fa.mode == 3) return;  // timing ablation (wrong results): no reducers
+    const int nslabs = fa.ntrain;
+    // Adam state of the parameter this lane applies (waves 0..2: chunk rb + wave nred, position lane), loaded first
+    const int ach = rb + wave * fa.nred;
+    const int pp = (wave < kFuseChunksPerReducer && ach < fa.nchunks) ? t16_slab_param(ach * 64 + lane) : -1;
+    AdamIn ain{};
+    if (pp >= 0) ain = adam_load(pp, mb);
+    asm volatile("" : "+v"(ain.fp), "+v"(ain.ft), "+v"(ain.bp));
+    // the wait: wave 0 polls, the block follows at the barrier. Mode 0: every trainer block's flag holds this launch's
+    // generation (lane l reads flags l, l + 64, ...; agent-scope loads, no read-modify-write anywhere). Modes 1 / 2 (A/B):
+    // an arrival counter that trainer blocks / waves increment and the last reducer resets -- each atomic on the one
+    // word costs ~14 ns serialised (1,024 per-wave arrivals: 27.8 us per step, 128 per-block: 15.2 us, round 6 A/B)
+    if (wave == 0 && (fa.mode == 0 || fa.mode == 4)) {
+        int i = 0;
+        for (; i < fa.polls; ++i) {
+            bool ok = true;
+            for (int k = lane; k < fa.ntrain; k += 64)
+                ok = ok && __hip_atomic_load(fa.flags + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fa.gen;
+            if (__builtin_amdgcn_readfirstlane(__ballot(!ok) == 0ull)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (i == fa.polls && lane == 0) __hip_atomic_store(fa.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (wave == 0) {
+        const uint32_t target = (fa.mode == 1 ? 1u : 8u) * (uint32_t)fa.ntrain;
+        int i = 0;
+        for (; i < fa.polls; ++i) {
+            const uint32_t c = __hip_atomic_load(fa.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(c) >= target) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (i == fa.polls && lane == 0) __hip_atomic_store(fa.err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0 &&
+            __hip_atomic_fetch_add(fa.sync + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)fa.nred - 1) {
+            __hip_atomic_store(fa.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(fa.sync + 64, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    lds_barrier();
+    if (fa.mode == 4) return;  // timing ablation (wrong results): reducers wait, then do nothing
+    // slab sums: thread (half, grp, quad); half 0 sums chunks rb and rb + 2 nred, half 1 chunk rb + nred
+    typedef float f4r __attribute__((ext_vector_type(4)));
+    f4r(*part)[16][16] = reinterpret_cast<f4r(*)[16][16]>(smem);  // [slot][grp][quad], slot = chunk index 0..2
+    const int quad = tid & 15, grp = (tid >> 4) & 15, half = tid >> 8;
+    const int nmine = grp < nslabs ? (nslabs - grp + 15) / 16 : 0;
+    // agent-scope loads (sc1): the slab lines other CUs stored in this launch, coherent across the XCDs' L2s
+    auto ld = [&](int ch, int k) -> f4r {
+        const int slab = min(grp + k * 16, nslabs - 1);
+        const uint64_t w = __hip_atomic_load(
+            reinterpret_cast<const uint64_t*>(slabs + (int64_t)slab * mb.n_slab + (ch * 16 + quad) * 4), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        const h4 v = __builtin_bit_cast(h4, w);
+        return f4r{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+    };
+    int chs[2] = {half ? rb + fa.nred : rb, half ? fa.nchunks : rb + 2 * fa.nred};
+    int slot[2] = {half ? 1 : 0, 2};
+    f4r a0[2], a1[2], v[2][8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        a0[c] = a1[c] = f4r{0.f, 0.f, 0.f, 0.f};
+        if (chs[c] >= fa.nchunks) chs[c] = -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[c][u] = ld(chs[c] >= 0 ? chs[c] : rb, u);
+    }
+    for (int base = 0;;) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const bool in = base + u < nmine;
+                if (u & 1) a1[c] += in ? v[c][u] : f4r{0.f, 0.f, 0.f, 0.f};
+                else a0[c] += in ? v[c][u] : f4r{0.f, 0.f, 0.f, 0.f};
+            }
+        base += 8;
+        if (base >= nmine) break;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[c][u] = ld(chs[c] >= 0 ? chs[c] : rb, base + u);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+        if (chs[c] >= 0) part[slot[c]][grp][quad] = a0[c] + a1[c];
+    // the loss: reducer 0's wave 3 (the same strided per-lane sum and xor butterfly as reduce_adam_kernel)
+    if (rb == 0 && wave == 3) {
+        float L = 0.0f;
+        for (int base = lane; base < nslabs; base += 8 * 64) {
+            float lv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                lv[u] = __hip_atomic_load(loss_partials + min(base + 64 * u, nslabs - 1), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) L += base + 64 * u < nslabs ? lv[u] : 0.0f;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
+        if (lane == 0 && fa.loss_out) fa.loss_out[0] = L;
+    }
+    lds_barrier();
+    if (pp < 0) return;
+    const int lp = lane >> 2, comp = lane & 3;
+    float t8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t8[u] = part[wave][2 * u][lp][comp] + part[wave][2 * u + 1][lp][comp];
+    const float g1 = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
+    adam_pack_pre(pp, g1, ain, mb, fa.oa, fa.lr_t, fa.ema_debias);
+}
+
+template <bool PADQ>
+__global__ __launch_bounds__(512, 1) void train16_fused_kernel(const float* __restrict__ q, const float* __restrict__ t,
+                                                               int64_t b, float n_total, float loss_scale,
+                                                               const h8* __restrict__ wf, const h8* __restrict__ wb,
+                                                               _Float16* __restrict__ slabs,
+                                                               float* __restrict__ loss_partials, FuseArgs fa) {
+    __shared__ __attribute__((aligned(16))) char smem[kLds];
+    const int blk = blockIdx.x;
+    if (blk >= fa.ntrain) {
+        fuse_reduce(smem, blk - fa.ntrain, slabs, loss_partials, fa);
+        return;
+    }
+    train16_split_body<16, 2, PADQ, 0>(smem, blk, q, t, b, n_total, loss_scale, wf, wb, slabs, loss_partials,
+                                       HashTrainOut{});
+    // count this wave (mode bit 0: this block) in once its slab / loss stores have completed (agent-scope stores)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (fa.mode == 0 || fa.mode >= 3) {
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(fa.flags + blk, fa.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (fa.mode == 1) {
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(fa.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_fetch_add(fa.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -893,6 +1073,31 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
 #else
     return hipErrorNotSupported;  // the 4-wave kernel and the stamped builds live in libnrc_amd_debug.so
 #endif
+}
+
+hipError_t launch_train16_fused(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,
+                                const _Float16* wf, const _Float16* wb, _Float16* slabs, float* loss_partials,
+                                uint32_t* sync, uint32_t* err, int polls, float* loss_out, const ModelBuffers& mb,
+                                const OptimArgs& oa, hipStream_t s, bool padq, int max_blocks, int mode,
+                                uint32_t gen, uint32_t* flags, int max_flags) {
+    if (b <= 0 || !sync || !err || polls < 1 || mb.n_slab % 64 != 0 || mb.slab_closed != 1 || mode < 0 || mode > 4 ||
+        (mode != 1 && mode != 2 && (!flags || gen == 0)))
+        return hipErrorInvalidValue;
+    FuseArgs fa{mb, oa, 0.0f, 0.0f, loss_out, sync, err, polls, t16_blocks(b), 0, mb.n_slab / 64, mode, gen, flags};
+    if (mode != 1 && mode != 2 && fa.ntrain > max_flags) return hipErrorNotSupported;
+    fa.nred = (fa.nchunks + kFuseChunksPerReducer - 1) / kFuseChunksPerReducer;
+    // every block on its own CU, or the reducers would queue behind trainers and the fusion buys nothing
+    if (fa.ntrain + fa.nred > max_blocks) return hipErrorNotSupported;
+    adam_host_factors(oa, fa.lr_t, fa.ema_debias);
+    const dim3 grid(fa.ntrain + fa.nred), block(128 * kWaves);
+    const h8 *f = (const h8*)wf, *bw = (const h8*)wb;
+    if (padq)
+        hipLaunchKernelGGL(train16_fused_kernel<true>, grid, block, 0, s, queries, targets, b, n_total, loss_scale, f, bw,
+                           slabs, loss_partials, fa);
+    else
+        hipLaunchKernelGGL(train16_fused_kernel<false>, grid, block, 0, s, queries, targets, b, n_total, loss_scale, f,
+                           bw, slabs, loss_partials, fa);
+    return hipGetLastError();
 }
 
 hipError_t launch_train16_hash(const float* queries, const float* targets, int64_t b, float n_total, float loss_scale,

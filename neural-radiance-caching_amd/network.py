@@ -262,6 +262,15 @@ class Network:
         check(self._lib.nrc_train_dp(self._h, pi, pt, b, int(global_b), ctypes.byref(lh) if loss else None))
         return lh.value if loss else None
 
+    def train_dp_async(self, inputs, targets, b_local: int, global_b: int, loss_d=None) -> None:
+        """train_dp whose global loss goes to device memory (loss_d: a one-element f32 device tensor, or None);
+        never blocks -- the form for one thread driving several in-process ranks (peer_exchange_open_local)."""
+        b = int(b_local)
+        pi = _dev_ptr(inputs, "inputs", b * self.query_dims if hasattr(inputs, "numel") else None) if b else None
+        pt = _dev_ptr(targets, "targets", b * 3 if hasattr(targets, "numel") else None) if b else None
+        pl = _dev_ptr(loss_d, "loss_d", 1 if hasattr(loss_d, "numel") else None) if loss_d is not None else None
+        check(self._lib.nrc_train_dp_async(self._h, pi, pt, b, int(global_b), pl))
+
     # ---- one-shot peer exchange (nrc_c.h nrc_peer_exchange_*; round 4) --------------------------------------
     PEER_HANDLE_BYTES = 64
 

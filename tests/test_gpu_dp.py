@@ -430,3 +430,63 @@ def test_peer_exchange_local_argument_checks(nrc, torch, dev, knobs):
             n.peer_exchange_close()
         for n in nets + [h]:
             n.destroy()
+
+
+def test_peer_exchange_local_group_closes_together(nrc, torch, dev, golden, knobs):
+    """the handles of an in-process exchange hold raw pointers to each other's receive buffers, so closing,
+    destroying or re-opening any member closes the exchange of every member (after their streams drain) instead of
+    freeing one buffer under the others. Then one host thread drives two ranks round-robin with nrc_train_dp_async
+    (each rank on its own stream, as two handles on one device need): no blocking loss inside the round, losses read
+    after it, replicas bitwise the rank-order sum applied by one handle."""
+    knobs("px_polls", 1 << 14)  # a handle left open by mistake ends its wait with an error instead of ~10 s
+    nets = []
+    for _ in range(4):
+        n = nrc.Network()
+        n.init(stream=torch.cuda.Stream())
+        n.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+        nets.append(n)
+    a, b, c, d = nets
+    q_np, t_np = nrc.synthetic.cornell_batch(4096, seed=17)
+    q, t = to_dev(torch, dev, q_np), to_dev(torch, dev, t_np)
+
+    def closed(n):
+        with pytest.raises(nrc.NrcError) as e:
+            n.train_dp(q[:16], t[:16], 16, 32)
+        return e.value.status == 1
+
+    ref = nrc.Network()
+    ref.init(stream=torch.cuda.current_stream())
+    ref.set_state(nrc.StateSlot.PARAMS, golden["params_b"])
+    try:
+        nrc.Network.peer_exchange_open_local([a, b, c])
+        b.peer_exchange_close()
+        assert closed(a) and closed(b) and closed(c)
+        nrc.Network.peer_exchange_open_local([a, b, c])
+        c.destroy()
+        assert closed(a) and closed(b)
+        nrc.Network.peer_exchange_open_local([a, b])
+        nrc.Network.peer_exchange_open_local([b, d])  # takes b: a's group is closed, not left pointing at b's buffer
+        assert closed(a)
+        nrc.Network.peer_exchange_open_local([a, b])  # d's group closed in turn
+        assert closed(d)
+        losses = [torch.full((1,), float("nan"), device=dev) for _ in range(2)]
+        g = [torch.zeros(nrc.GRAD_FLOATS, dtype=torch.float32, device=dev) for _ in range(2)]
+        for it in range(3):
+            for r, n in enumerate((a, b)):  # one thread, round-robin, nothing blocks
+                s, k = nrc.dp.shard_range(4096, r, 2)
+                n.train_dp_async(q[s:s + k], t[s:s + k], k, 4096, losses[r])
+            for r in range(2):
+                s, k = nrc.dp.shard_range(4096, r, 2)
+                ref.train_grad(q[s:s + k], t[s:s + k], k, 4096, g[r])
+            ref_loss = ref.train_apply(g[0] + g[1], loss=True)
+            torch.cuda.synchronize()
+            assert [float(x.item()) for x in losses] == [ref_loss, ref_loss], it
+        for slot in SLOTS:
+            want = ref.get_state(getattr(nrc.StateSlot, slot))
+            for n in (a, b):
+                np.testing.assert_array_equal(n.get_state(getattr(nrc.StateSlot, slot)), want, err_msg=slot)
+    finally:
+        for n in (a, b, d):
+            n.peer_exchange_close()
+        for n in (a, b, d, ref):
+            n.destroy()

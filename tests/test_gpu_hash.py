@@ -383,9 +383,8 @@ def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b, tscale):
     scatter_part, default from level 6), levels 10-15 queue their in-part corners before the adds (scatter_compact), and
     past 8 slices per level (b > 32,768) the partials give way to the atomic flush. The sums are exact integers, so
     every form must leave the same state, bit for bit, as the all-atomic, uncompacted scatter (both knobs 16) with the
-    LDS feature pass and the two optimizer launches (hash_adam 0, which also writes the grid's f32 inference copy every
-    step; the default one-launch update leaves it to a refresh at nrc_get_state, from the step it was left at even when
-    nrc_set_step moved the counter since) --
+    LDS feature pass and the two optimizer launches (hash_adam 0; the default one-launch update, hash_adam_kernel, runs
+    the same grid Adam body, which writes the grid's f32 inference copy every step as the two-launch form does) --
     including the 20,000-sample batch whose last slice is ragged, and targets x 3000, whose large gradients make some
     blocks' partial sums overflow int32 (those blocks store the int64 form)."""
     import torch
@@ -424,7 +423,6 @@ def test_hash_scatter_forms_are_bitwise_equal(nrc, dev, b, tscale):
                 assert float(fine[torch.isfinite(fine)].max()) > 512.0
             finally:
                 probe.destroy()
-        nets[0].step = nets[0].step + 7
         for slot in nrc.StateSlot:
             ref = nets[1].get_state(slot)
             for n in (nets[0], nets[2]):
