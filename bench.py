@@ -145,19 +145,44 @@ def frame_bench(nrc, net, dev, iters: int) -> dict:
                         F.records_to_device(rec, dev), [t(pad(f.train_queries, 15)), torch.zeros((cap, 15), device=dev)],
                         [t(pad(f.train_targets, 3)), torch.zeros((cap, 3), device=dev)])
     state = [net.get_state(s) for s in (nrc.StateSlot.PARAMS, nrc.StateSlot.INFER)]
-    for it in range(3):
-        F.process_frame(net, fb, F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1))
+
+    def frames() -> float:
+        for it in range(3):
+            F.process_frame(net, fb, F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(iters):
+            F.process_frame(net, fb, F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1))
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / iters * 1e3
+
+    ms = frames()
+    # the reference's shuffle contract (NRCUtil.cu:19-35, Device.cpp:1427-1469): the renderer's 65,536 random u32 keys,
+    # stable-sorted with their indices -- nrc_sort_train_permutation inside the frame driver (shuffle_keys_d)
+    keys = torch.randint(0, 1 << 31, (cap,), dtype=torch.int32, device=dev)
+    fb.shuffle_keys = keys
+    ms_keys = frames()
+    fb.shuffle_keys = None
+    perm = torch.empty(cap, dtype=torch.int32, device=dev)
+    temp = torch.empty(max(1, F.sort_train_permutation_temp_bytes(cap)), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    for _ in range(3):
+        F.sort_train_permutation(keys, perm, cap, temp=temp)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        F.sort_train_permutation(keys, perm, cap, temp=temp)
+    e1.record(stream)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for it in range(iters):
-        F.process_frame(net, fb, F.FrameParams(S, T, f.num_training_records, F.RenderMode.Full, it, it, 1))
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / iters * 1e3
+    sort_ms = e0.elapsed_time(e1) / iters
     for s, v in zip((nrc.StateSlot.PARAMS, nrc.StateSlot.INFER), state):  # leave the network as it was
         net.set_state(s, v)
-    return {"frame_ms": ms, "queries": S + T, "train_records": f.num_training_records, "iters": iters,
+    return {"frame_ms": ms, "key_sort_frame_ms": ms_keys, "key_sort_ms": sort_ms, "queries": S + T,
+            "train_records": f.num_training_records, "iters": iters,
             "what": "nrc_process_frame: fused infer+accumulate, propagate, Feistel shuffle, 4 x 16384 train with "
-                    "loss read-back; synthetic 1920x1080 Cornell frame, 8x8 tiles"}
+                    "loss read-back; synthetic 1920x1080 Cornell frame, 8x8 tiles. key_sort_frame_ms: the same frame "
+                    "shuffled by the reference's contract (65,536 caller keys, stable LSD radix sort, "
+                    "nrc_sort_train_permutation); key_sort_ms: that sort alone (HIP events)"}
 
 
 def hash_bench(nrc, dev, iters: int) -> dict:

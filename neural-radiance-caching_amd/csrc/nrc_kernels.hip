@@ -1631,7 +1631,10 @@ __device__ __forceinline__ uint32_t relu_fp8x4(const f16v& c, int q) {
     const float a1 = __builtin_amdgcn_fmed3f(c[4 * q + 1], 0.0f, 448.0f);
     const float a2 = __builtin_amdgcn_fmed3f(c[4 * q + 2], 0.0f, 448.0f);
     const float a3 = __builtin_amdgcn_fmed3f(c[4 * q + 3], 0.0f, 448.0f);
-    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+    // the first convert writes bytes 0..1 and keeps bytes 2..3 of its "old" operand, which the second overwrites: old =
+    // a0's own bits (a0 dies here, so the destination takes its register) instead of 0, which cost one v_mov_b32 per
+    // 4 values (80 per tile)
+    const uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, (int)__builtin_bit_cast(uint32_t, a0), false);
     return __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, lo, true);
 }
 
@@ -1665,17 +1668,31 @@ __device__ __forceinline__ void copy_to_lds_chunked(h8* __restrict__ dst, const 
     }
 }
 
+// The width-128 images span 88 / 156 KiB of LDS, past the 64-KiB reach of a ds_read's immediate offset: a fragment read
+// through one laundered base pointer cost a v_add_u32 per read beyond it (108 per tile f16, 40 FP8). WideLds holds one
+// laundered base per 64 KiB (the launder keeps the reads inside the tile loop, as in the 64-wide kernel), so every
+// fragment read is base k + an immediate.
+struct WideLds {
+    lds_h8* b[3];
+    __device__ __forceinline__ explicit WideLds(lds_h8* lane_base) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) b[k] = launder(lane_base + 4096 * k);
+    }
+    // h8 offset o (a compile-time constant after unrolling) from the lane's base
+    __device__ __forceinline__ h8 at(int o) const { return b[o >> 12][o & 4095]; }
+};
+
 template <int PREC>
 __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], const uint32_t (&sc)[5]) {
     f16v c[4];
     {
-        lds_h8* wl = launder(lw_lane);
+        const WideLds wl(lw_lane);
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
 #pragma unroll
         for (int kk = 0; kk < 5; ++kk)
 #pragma unroll
-            for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(0, mb, kk) * 64], x[kk], c[mb]);
+            for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl.at(wide_frag(0, mb, kk) * 64), x[kk], c[mb]);
     }
     if constexpr (PREC == 0) {
         h8 y[8];
@@ -1683,35 +1700,36 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
         for (int kk = 0; kk < 8; ++kk) y[kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
-            lds_h8* wl = launder(lw_lane);
+            const WideLds wl(lw_lane);
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-                for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl[wide_frag(l, mb, kk) * 64], y[kk], c[mb]);
+                for (int mb = 0; mb < 4; ++mb) c[mb] = mfma(wl.at(wide_frag(l, mb, kk) * 64), y[kk], c[mb]);
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk) y[kk] = relu_h8(c[kk >> 1], 8 * (kk & 1));
         }
-        lds_h8* wl = launder(lw_lane);
+        const WideLds wl(lw_lane);
         f16v o = zero16();
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) o = mfma(wl[wide_frag(5, 0, kk) * 64], y[kk], o);
+        for (int kk = 0; kk < 8; ++kk) o = mfma(wl.at(wide_frag(5, 0, kk) * 64), y[kk], o);
         return o;
     } else {
         i8v y[2];
         pack_fp8(c, y);
         // fp8 fragment f: planes at h8 offsets (20 + 2 f) * 64 and (21 + 2 f) * 64 from the lane's base
-        auto frag8 = [&](lds_h8* wl, int f) {
-            const h8 lo = wl[(20 + 2 * f) * 64], hi = wl[(21 + 2 * f) * 64];
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            const u4 a = __builtin_bit_cast(u4, lo), b = __builtin_bit_cast(u4, hi);
-            const i8v r = {(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
-            return r;
+        auto frag8 = [&](const WideLds& wl, int f) {
+            const h8 lo = wl.at((20 + 2 * f) * 64), hi = wl.at((21 + 2 * f) * 64);
+            typedef int i4v __attribute__((ext_vector_type(4)));
+            // one shuffle of the two 16-byte reads (element-wise construction made the compiler copy both halves into a
+            // fresh register octet: 96 v_mov_b32 per tile)
+            return (i8v)__builtin_shufflevector(__builtin_bit_cast(i4v, lo), __builtin_bit_cast(i4v, hi), 0, 1, 2, 3, 4, 5,
+                                                6, 7);
         };
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
-            lds_h8* wl = launder(lw_lane);
+            const WideLds wl(lw_lane);
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) c[mb] = zero16();
 #pragma unroll
@@ -1721,7 +1739,7 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
                     c[mb] = mfma_fp8_mb(mb, frag8(wl, wide8_frag(l, mb, s)), y[s], c[mb], sc[l - 1]);
             pack_fp8(c, y);
         }
-        lds_h8* wl = launder(lw_lane);
+        const WideLds wl(lw_lane);
         f16v o = zero16();
 #pragma unroll
         for (int s = 0; s < 2; ++s) o = mfma_fp8<0>(frag8(wl, wide8_frag(5, 0, s)), y[s], o, sc[4]);
@@ -1789,8 +1807,10 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
             ng = g + wstride;
         }
         h8 x[5];
+        // round 6: the 64-wide kernel's encoder v3 (tent-map wave, OneBlob wrap as two clamps: one path) instead of
+        // round 1's encode_fast, whose OneBlob wrap branch the Cornell stream's raw angles always take (-61 VALU per tile)
         if constexpr (ENC == 2) encode_sh<true>(Q, h, x);
-        else encode_fast<true>(Q, h, x);
+        else encode_v3(Q, h, x);
         if constexpr (QUEUE) {
             if (lane == 0) nn_raw = atomicAdd(&wq_next, 1u);  // the tile after next
         }
@@ -2670,7 +2690,7 @@ __global__ __launch_bounds__(128, 1) void wide_fwd_bwd_lds_kernel(const float* _
     }
     h8 x[5];
     if constexpr (ENC == 2) encode_sh<true>(Q, h, x);
-    else encode_fast<true>(Q, h, x);
+    else encode_v3(Q, h, x);  // the inference kernel's encoder (round 6)
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk)
 #pragma unroll
@@ -3315,14 +3335,79 @@ hipError_t launch_infer_sh(const float* queries, float* out, int64_t n, const _F
 //     accumulator in f32, then one rounding to f16: the oracle's f16(acc + part) up to f32 double rounding);
 //   * output layer: the 32x32x16 form (rows 0..2 of lane half 0), the same chunking.
 // Same encoder (encode_v3) and output format as the production kernel; about 4x its VALU (the per-chunk roundings).
-constexpr int kTcnnRowHalves = 80;  // one query's 80 encoded features (160 B)
-__device__ __forceinline__ void round_f16_inplace(f16v& c, int count) {
+// Round 6: the round-4/5 kernel ran 2.95x the production kernel's time. PMC of it and of a first
+// rework (profiles/r06_tcnn/): VALU-issue-bound -- 85 % of every SIMD's vector issue, at 3x the production kernel's
+// VALU per tile, the matrix pipe at 21 % -- because every chunk's f32 result was rounded to f16 and widened back to f32
+// for the next chunk's MFMA (1.5 VALU per element; v_fma_mixlo/hi_f16 in its place costs 2 issue slots per element and
+// measured no faster). Now:
+//   * the widening is done by the matrix cores (TcnnId below): 0.5 VALU per element and chunk;
+//   * 1024-thread blocks (16 waves, 4 per SIMD) over one copy of the weights, each wave drawing its tiles from the
+//     block's LDS queue and fetching the next tile's inputs one tile ahead (as the production kernel); a branch-free
+//     buffer store (a conditional store, and the wavefront-scope fences around the row hand-off, made every tile wait
+//     vmcnt(0));
+//   * 176-byte query rows (44 dwords = 4 x 11): the chunk reads (ds_read_b128) of 16 consecutive lanes hit 16 distinct
+//     bank quads (the 160-byte rows had 48 % of the LDS cycles in bank conflicts).
+constexpr int kTcnnRowHalves = 88;  // one query's 80 encoded features + 8 unused halves (176 B)
+constexpr int kTcnnWaves = 16;
+
+// acc = f16(part): one v_cvt_pk_f16_f32 per pair
+__device__ __forceinline__ void first16(uint32_t (&a)[8], const f16v& p) {
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-        if (i >= count) break;
-        const h2 v = __builtin_bit_cast(h2, pk2(c[i], c[i + 1]));
-        c[i] = (float)v[0];
-        c[i + 1] = (float)v[1];
+    for (int i = 0; i < 8; ++i) a[i] = pk2(p[2 * i], p[2 * i + 1]);
+}
+// accumulator words 4b .. 4b + 3 -> B operand, ReLU on the packed halves (f16(relu(x)) == relu(f16(x))) as a signed
+// 16-bit max with 0 (v_pk_max_i16): a negative half has its sign bit set and becomes +0. (An f16 max of words that come
+// out of inline asm gets a canonicalising v_pk_max_f16 in front of it: twice the instructions.)
+__device__ __forceinline__ h8 relu_words(const uint32_t (&a)[8], int b) {
+    typedef short s8v __attribute__((ext_vector_type(8)));
+    const u4 w = {a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
+    const s8v z = {};
+    return __builtin_bit_cast(h8, __builtin_elementwise_max(__builtin_bit_cast(s8v, w), z));
+}
+
+// The f16 accumulator back into f32 by the matrix cores (round 6, second form): the packed accumulator words 0..3 /
+// 4..7 are B operands (the accumulator-as-operand layout, acc_row), and two constant 0/1 A fragments Id0 / Id1 route
+// them back to rows 0..15 / 16..31 of an f32 accumulator -- products with 1.0 and sums with zeros, exact. The chunk's own
+// MFMA then adds its 16 products to that C, and one v_cvt_pk_f16_f32 per pair rounds: acc = f16(acc + chunk), tcnn's
+// per-chunk f16 accumulation, with 0.5 VALU per element instead of 1.5 (convert down, widen both halves back) or 2
+// issue slots (v_fma_mix). The kernel was VALU-issue-bound (85 % of the SIMDs' vector issue, PMC); the identity MFMAs
+// move that work to the matrix pipe, which ran at 21 %.
+struct TcnnId {
+    h8 lo, hi;  // A fragments: lane (i, h) element e is 1 where row i == 8 (e / 4) + 4 h + e % 4 (+ 16 for hi)
+    __device__ __forceinline__ explicit TcnnId(int lane) {
+        const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int row = 8 * (e >> 2) + 4 * h + (e & 3);
+            lo[e] = (_Float16)(i == row ? 1.0f : 0.0f);
+            hi[e] = (_Float16)(i == 16 + row ? 1.0f : 0.0f);
+        }
+    }
+};
+__device__ __forceinline__ h8 acc_words(const uint32_t (&a)[8], int b) {
+    const u4 w = {a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
+    return __builtin_bit_cast(h8, w);
+}
+
+// One layer's KK chunks of both M-blocks into the packed-f16 accumulators: chunk 0 rounds the MFMA result, every
+// further chunk re-enters the accumulator through Id0 / Id1 first. The two M-blocks' chains are independent.
+template <int KK>
+__device__ __forceinline__ void tcnn_layer(lds_h8* wl, const TcnnId& id, int layer, const h8 (&in)[KK],
+                                           uint32_t (&acc)[2][8]) {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+        const h8 w0 = wl[fwd_frag(layer, 0, kk) * 64], w1 = wl[fwd_frag(layer, 1, kk) * 64];
+        f16v c0 = zero16(), c1 = zero16();
+        if (kk > 0) {
+            c0 = mfma(id.lo, acc_words(acc[0], 0), c0);
+            c1 = mfma(id.lo, acc_words(acc[1], 0), c1);
+            c0 = mfma(id.hi, acc_words(acc[0], 1), c0);
+            c1 = mfma(id.hi, acc_words(acc[1], 1), c1);
+        }
+        c0 = mfma(w0, in[kk], c0);
+        c1 = mfma(w1, in[kk], c1);
+        first16(acc[0], c0);
+        first16(acc[1], c1);
     }
 }
 
@@ -3330,20 +3415,23 @@ __device__ __forceinline__ void round_f16_inplace(f16v& c, int count) {
 // (K = 64, 4 chunks: grid 0..31, OneBlob 32..55, Identity 56..61, pad 62, 63; feat = the pass's workspace), the same MLP
 // chunking -- tcnn runs the same FullyFusedMLP behind either encoding (NRCNetworkConfigs.h:84-128).
 template <int ENC>
-__global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restrict__ q, float* __restrict__ out,
-                                                            int64_t n, const h8* __restrict__ wf,
-                                                            const float* __restrict__ w0,
-                                                            const uint32_t* __restrict__ feat) {
+__global__ __launch_bounds__(64 * kTcnnWaves, 1) void infer_tcnn_kernel(const float* __restrict__ q,
+                                                                        float* __restrict__ out, int64_t n,
+                                                                        const h8* __restrict__ wf,
+                                                                        const float* __restrict__ w0,
+                                                                        const uint32_t* __restrict__ feat) {
     static_assert(ENC == 0 || ENC == 3, "Frequency or Hash-from-features");
-    constexpr int W = 8;  // waves per block
+    constexpr int W = kTcnnWaves, T = 64 * W;
     constexpr int KK0 = ENC == 3 ? 4 : 5, IN = ENC == 3 ? NRC_HASH_ENC_WIDTH : NRC_ENC_WIDTH;
     constexpr int PAD0 = ENC == 3 ? 62 : 66;  // first constant-one feature
     __shared__ __attribute__((aligned(16))) h8 lw[kFwdFrags * 64];
     __shared__ __attribute__((aligned(16))) _Float16 enc[W][32 * kTcnnRowHalves];
-    copy_to_lds<512, kFwdFrags * 64>(lw, wf);
+    __shared__ uint32_t wq_next;
+    if (threadIdx.x == 0) wq_next = 0;
+    copy_to_lds<T, kFwdFrags * 64>(lw, wf);
     __syncthreads();
     // layer-0 fragments in canonical K order: fragment (mb, kk), lane L, element j = W0[32 mb + L % 32][16 kk + 8 (L / 32) + j]
-    for (int i = threadIdx.x; i < 2 * KK0 * 64; i += 512) {
+    for (int i = threadIdx.x; i < 2 * KK0 * 64; i += T) {
         const int frag = i >> 6, L = i & 63, mb = frag / KK0, kk = frag % KK0;
         const float* src = w0 + (32 * mb + (L & 31)) * IN + 16 * kk + 8 * (L >> 5);
         h8 v;
@@ -3352,6 +3440,7 @@ __global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restr
         lw[fwd_frag(0, mb, kk) * 64 + L] = v;
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+    const TcnnId id(lane);
     _Float16* const row = &enc[wave][r * kTcnnRowHalves];
     // pad features (never rewritten)
     if (h == 0)
@@ -3359,17 +3448,37 @@ __global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restr
         for (int f = PAD0; f < IN; ++f) row[f] = (_Float16)1.0f;
     __syncthreads();
     char* const rowb = reinterpret_cast<char*>(row);
+    // the block's contiguous range of tiles, drawn one at a time by its waves (the production kernel's LDS queue)
     const int64_t ntiles = (n + 31) / 32;
-    for (int64_t g = (int64_t)blockIdx.x * W + wave; g < ntiles; g += (int64_t)gridDim.x * W) {
-        const int64_t s = g * 32 + r;
-        const int64_t sc = s < n ? s : n - 1;
-        const QLane Q = load_q(q, sc, h);
+    const int64_t gbase = (int64_t)blockIdx.x * ntiles / gridDim.x, gend = (int64_t)(blockIdx.x + 1) * ntiles / gridDim.x;
+    auto draw = [&]() -> int64_t {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&wq_next, 1u);
+        return gbase + (int64_t)__builtin_amdgcn_readfirstlane(t);
+    };
+    // the next tile's queries (and level features) and the tile after it are fetched one tile ahead, as in the production
+    // kernel (clamped rows: a fetch past the range reads a valid row that is never used)
+    int64_t g = draw();
+    if (g >= gend) return;
+    auto fetch = [&](int64_t tile, QLane& Q, uint32_t (&F)[8]) {
+        const int64_t sc = min(tile * 32 + r, n - 1);
+        Q = load_q(q, sc, h);
+        if constexpr (ENC == 3) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) F[i] = feat[(int64_t)(8 * h + i) * kHashFeatStride + sc];
+        }
+    };
+    QLane Q;
+    uint32_t F[8] = {};
+    fetch(g, Q, F);
+    int64_t gn = draw();
+    for (; g < gend; g = gn, gn = draw()) {
         uint32_t w[20];
         if constexpr (ENC == 3) {
             // encode_hashf's slots: levels 8h.. (features 16h.., one half2 per level), OneBlob dims 3h.. (features
             // 32 + 12h..), Identity dims 3h.. (features 56 + 3h..)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) w[i] = feat[(int64_t)(8 * h + i) * kHashFeatStride + sc];
+            for (int i = 0; i < 8; ++i) w[i] = F[i];
             blob_v3(Q.b0, w[8], w[9]);
             blob_v3(Q.b1, w[10], w[11]);
             blob_v3(Q.b2, w[12], w[13]);
@@ -3387,6 +3496,7 @@ __global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restr
                 w[4 * kk + 3] = t.w;
             }
         }
+        fetch(gn, Q, F);                // the next tile's inputs, in flight under this tile's MLP
         asm volatile("" ::: "memory");  // the previous tile's chunk reads of this row stay above these writes
         if constexpr (ENC == 3) {
 #pragma unroll
@@ -3411,62 +3521,61 @@ __global__ __launch_bounds__(512, 2) void infer_tcnn_kernel(const float* __restr
             row[61 + 3 * h] = id01[1];
             row[62 + 3 * h] = id2[0];
         }
-        // the wave's writes of every row land before its lanes read other lanes' rows (LDS is in order per wave)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // the wave's writes of every row land before its lanes read other lanes' rows: LDS executes one wave's operations
+        // in order, so only the compiler must keep the reads below the writes (the "memory" clobbers). (Round 6: the
+        // wavefront-scope release/acquire fences that stood here made the compiler wait vmcnt(0) -- for the prefetched
+        // queries and the previous tile's stores -- on every tile.)
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         h8 in0[KK0];
 #pragma unroll
         for (int kk = 0; kk < KK0; ++kk) in0[kk] = *(const h8*)(rowb + 32 * kk + 16 * h);
         asm volatile("" ::: "memory");
         lds_h8* const wl = (lds_h8*)(lw + lane);
-        // layer 0 (K = 80 / 64: 5 / 4 chunks) and the hidden layers (K = 64, 4 chunks)
+        uint32_t acc[2][8];
         h8 y[4];
-        {
-            f16v c[2];
-#pragma unroll
-            for (int kk = 0; kk < KK0; ++kk)
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    c[m] = mfma(wl[fwd_frag(0, m, kk) * 64], in0[kk], kk ? c[m] : zero16());
-                    round_f16_inplace(c[m], 16);
-                }
-            y[0] = relu_h8(c[0], 0);
-            y[1] = relu_h8(c[0], 8);
-            y[2] = relu_h8(c[1], 0);
-            y[3] = relu_h8(c[1], 8);
-        }
+        // layer 0 (K = 80 / 64: 5 / 4 chunks) and the hidden layers (K = 64, 4 chunks)
+        tcnn_layer<KK0>(wl, id, 0, in0, acc);
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
-            lds_h8* const wll = launder(wl);
-            f16v c[2];
+            // k-step kk of the next layer = accumulator rows 16 kk.. = M-block kk / 2, registers 8 (kk % 2)..
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    c[m] = mfma(wll[fwd_frag(l, m, kk) * 64], y[kk], kk ? c[m] : zero16());
-                    round_f16_inplace(c[m], 16);
-                }
-            y[0] = relu_h8(c[0], 0);
-            y[1] = relu_h8(c[0], 8);
-            y[2] = relu_h8(c[1], 0);
-            y[3] = relu_h8(c[1], 8);
+            for (int b = 0; b < 2; ++b) {
+                y[b] = relu_words(acc[0], b);
+                y[2 + b] = relu_words(acc[1], b);
+            }
+            tcnn_layer<4>(launder(wl), id, l, y, acc);
         }
-        // output layer (rows 0..2 of lane half 0 = registers 0..2)
-        f16v o = zero16();
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            y[b] = relu_words(acc[0], b);
+            y[2 + b] = relu_words(acc[1], b);
+        }
+        // output layer (rows 0..2 of lane half 0 = elements 0..2), the same chunking; rows 0..3 re-enter through Id0
+        // (accumulator elements 4..7, rows 8..11, are fed as zeros: no output reads them)
+        uint32_t o[2];
         {
             lds_h8* const wll = launder(wl);
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                o = mfma(wll[fwd_frag(5, 0, kk) * 64], y[kk], o);
-                round_f16_inplace(o, 4);
+                f16v c = zero16();
+                if (kk > 0) c = mfma(id.lo, __builtin_bit_cast(h8, u4{o[0], o[1], 0u, 0u}), c);
+                c = mfma(wll[fwd_frag(5, 0, kk) * 64], y[kk], c);
+                o[0] = pk2(c[0], c[1]);
+                o[1] = pk2(c[2], c[3]);
             }
         }
-        if (h == 0 && s < n) {
-            float* dst = out + s * NRC_OUTPUT_DIMS;
-            dst[0] = fmaxf(o[0], 0.0f);  // f16-valued already: the output ReLU (NRCNetworkConfigs.h:29)
-            dst[1] = fmaxf(o[1], 0.0f);
-            dst[2] = fmaxf(o[2], 0.0f);
+        {
+            // the output ReLU (NRCNetworkConfigs.h:29) of the f16 result; branch-free raw buffer store whose descriptor
+            // covers the tile's valid rows (the h = 1 lanes and the tail are dropped by the hardware, as in the
+            // production kernel: a conditional store made the next tile wait for its acknowledgement)
+            const h2 o01 = __builtin_bit_cast(h2, o[0]), o23 = __builtin_bit_cast(h2, o[1]);
+            const u3 ov = {__builtin_bit_cast(uint32_t, fmaxf((float)o01[0], 0.0f)),
+                           __builtin_bit_cast(uint32_t, fmaxf((float)o01[1], 0.0f)),
+                           __builtin_bit_cast(uint32_t, fmaxf((float)o23[0], 0.0f))};
+            const int64_t s0 = g * 32;
+            __builtin_amdgcn_raw_buffer_store_b96(ov, buffer_rsrc(out + s0 * NRC_OUTPUT_DIMS, tile_rows(n, s0) * 12),
+                                                  h ? kBufferOff : r * 12, 0, 0);
         }
     }
 }
@@ -3476,7 +3585,7 @@ hipError_t launch_infer_tcnn(const float* queries, float* out, int64_t n, const 
     if (n <= 0) return hipSuccess;
     if (!wf || !w0) return hipErrorInvalidValue;
     static int bpc = 0;
-    return launch_persistent_infer(infer_tcnn_kernel<0>, 512, bpc, (n + 31) / 32, queries, out, n, wf, s, w0,
+    return launch_persistent_infer(infer_tcnn_kernel<0>, 64 * kTcnnWaves, bpc, (n + 31) / 32, queries, out, n, wf, s, w0,
                                    (const uint32_t*)nullptr);
 }
 
@@ -3490,7 +3599,7 @@ hipError_t launch_infer_hash_tcnn(const float* queries, float* out, int64_t n, c
         const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
         const float* qc = queries + c0 * NRC_INPUT_DIMS;
         launch_hash_feature_pass(qc, cnt, reinterpret_cast<const uint32_t*>(grid), feat, false, s);
-        const hipError_t e = launch_persistent_infer(infer_tcnn_kernel<3>, 512, bpc, (cnt + 31) / 32, qc,
+        const hipError_t e = launch_persistent_infer(infer_tcnn_kernel<3>, 64 * kTcnnWaves, bpc, (cnt + 31) / 32, qc,
                                                      out + c0 * NRC_OUTPUT_DIMS, cnt, wf, s, w0,
                                                      (const uint32_t*)feat);
         if (e != hipSuccess) return e;
