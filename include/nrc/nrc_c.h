@@ -280,7 +280,9 @@ nrc_status nrc_debug_hash_scatter_inputs(nrc_net* net, float* pos_d, uint32_t* d
 nrc_status nrc_debug_infer_stamps(nrc_net* net, const float* inputs_d, float* outputs_d, uint32_t n,
                                   uint64_t* stamps_d, uint64_t* waves_h);
 /* Width-128 networks: inference with either precision's weight image (both are packed from the inference
- * weights), regardless of the configured infer_precision (A/B timing and parity tests). */
+ * weights), regardless of the configured infer_precision (A/B timing and parity tests). Bits 4+ of precision pick a
+ * kernel variant of the debug library (Frequency only): 1 = 1024-thread blocks, 2 = FP8 with the ReLU on the
+ * converted bytes. */
 nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* inputs_d, float* outputs_d, uint32_t n,
                                      hipStream_t stream);
 /* e4m3 conversion exactly as the FP8 kernels do it: clamp to [relu ? 0 : -448, 448], round to nearest even. */

@@ -2007,9 +2007,11 @@ nrc_status nrc_debug_infer_precision(nrc_net* net, int precision, const float* i
             return;
         }
         if (!net->wide()) throw ApiError(NRC_ERR_UNSUPPORTED, "precision selection is for the width-128 network");
-        // bits 4+: kernel variant (0 = production; 1 = 1024-thread blocks, Frequency only)
+        // bits 4+: kernel variant (0 = production; 1 = 1024-thread blocks, Frequency only; 2 = FP8 with the ReLU on
+        // the converted bytes)
         const int prec = precision & 15, variant = precision >> 4;
-        if ((prec != NRC_PRECISION_F16 && prec != NRC_PRECISION_FP8) || variant < 0 || variant > 1)
+        if ((prec != NRC_PRECISION_F16 && prec != NRC_PRECISION_FP8) || variant < 0 || variant > 2 ||
+            (variant == 2 && prec != NRC_PRECISION_FP8))
             throw ApiError(NRC_ERR_INVALID_ARGUMENT, "unknown precision");
         if (variant && wide_enc(net) != 0) throw ApiError(NRC_ERR_UNSUPPORTED, "kernel variants are Frequency-only");
         if (n == 0) return;

@@ -243,16 +243,20 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __res
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const uint32_t nblk = gridDim.x, b = blockIdx.x;
     const uint32_t per = chunk / 4u, w0 = b * chunk + (uint32_t)w * per, w1 = min(n, w0 + per);
-    // this wave's first group of keys and values, in flight with the count-table reads below
+    // this wave's first group of keys and values, in flight with the count-table reads below. Branch-free: every lane
+    // loads at a clamped index (< n) and the value array is selected, not branched on -- a load behind a scalar branch
+    // and an exec-masked store in one loop is the combination tools/asm_hazard_check.py rule 3 bans
     uint32_t key[kSortPerLane];
     int val[kSortPerLane];
+    const int* const vsrc = vin ? vin : reinterpret_cast<const int*>(kin);
     auto load_group = [&](uint32_t g0) {
 #pragma unroll
         for (int j = 0; j < kSortPerLane; ++j) {
             const uint32_t i = g0 + 64u * j + lane;
             const uint32_t ic = i < w1 ? i : (w1 > 0 ? w1 - 1 : 0);
-            key[j] = w0 < w1 ? kin[ic] : 0u;
-            val[j] = vin ? (w0 < w1 ? vin[ic] : 0) : (int)i;
+            key[j] = kin[ic];
+            const int v = vsrc[ic];
+            val[j] = vin ? v : (int)i;
         }
     };
     load_group(w0);
@@ -298,14 +302,13 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __res
         run += c;
     }
     __syncthreads();
-    // wave w: its range in order, 64 at a time (the loop is wave-uniform); lanes holding the same digit are matched
-    // by 8 ballots, rank = the matching lanes below this one, the lowest of them advances the digit's position
-    for (uint32_t g0 = w0; g0 < w1; g0 += 64u * kSortPerLane) {
-        if (g0 != w0 || w1 - w0 > 64u * kSortPerLane) load_group(g0);  // the counting loop moved past the first group
+    // wave w: its range in order, 64 at a time (wave-uniform); lanes holding the same digit are matched by 8 ballots,
+    // rank = the matching lanes below this one, the lowest of them advances the digit's position
+    auto scatter_group = [&](uint32_t g0) {
 #pragma unroll
         for (int j = 0; j < kSortPerLane; ++j) {
             const uint32_t i0 = g0 + 64u * j;
-            if (i0 >= w1) break;  // wave-uniform
+            if (i0 >= w1) continue;  // wave-uniform
             const bool valid = i0 + lane < w1;
             const uint32_t d = (key[j] >> shift) & 255u;
             uint64_t m = __ballot(valid);
@@ -326,6 +329,14 @@ __global__ __launch_bounds__(256) void sort_scatter_kernel(const uint32_t* __res
                     __hip_atomic_fetch_add(hist_next + ((key[j] >> (shift + 8)) & 255u) * kSortBlocks + pos / chunk, 1u,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+        }
+    };
+    if (w1 <= w0 + 64u * kSortPerLane) {
+        scatter_group(w0);  // one group (every wave at n <= 65,536 keys): still in registers, no loop
+    } else {
+        for (uint32_t g0 = w0; g0 < w1; g0 += 64u * kSortPerLane) {
+            load_group(g0);  // the counting loop moved past the first group
+            scatter_group(g0);
         }
     }
 }

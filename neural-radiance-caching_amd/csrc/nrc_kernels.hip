@@ -1607,8 +1607,8 @@ __global__ void encode_hash_kernel(const float* __restrict__ q, const uint32_t* 
 //   PREC 0 (f16): 4 M-blocks x 8 k-steps of v_mfma_f32_32x32x16_f16 per hidden layer; 156 KiB of fragments in LDS.
 //   PREC 1 (FP8): layer 0 f16; layers 1..5 on v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 x e4m3, 2x the f16 rate), the
 //   weights e4m3 with one E8M0 scale per output row (the MX scale-A operand: byte mb of the lane's scale word via
-//   op_sel), activations clamped to [0, 448] and converted with v_cvt_pk_fp8_f32 (RNE; med3 does ReLU + saturation
-//   in one op); 88 KiB of fragments in LDS.
+//   op_sel), activations converted with v_cvt_scalef32_pk_fp8_f32 (RNE, saturating at +-448 under MODE.FP16_OVFL)
+//   and ReLU'd on the e4m3 bytes (pack_fp8; round 5 clamped every value with a med3 first); 88 KiB of fragments in LDS.
 // ------------------------------------------------------------------------------------------------
 typedef int i8v __attribute__((ext_vector_type(8)));  // 32 e4m3 bytes: one operand of the 32x32x64 MX MFMA
 
@@ -1625,8 +1625,9 @@ __device__ __forceinline__ f16v mfma_fp8_mb(int mb, const i8v& a, const i8v& b, 
     }
 }
 
-// e4m3 bytes of ReLU(accumulator registers 4q .. 4q+3), saturated at 448
-__device__ __forceinline__ uint32_t relu_fp8x4(const f16v& c, int q) {
+// e4m3 bytes of ReLU(accumulator registers 4q .. 4q+3), saturated at 448: the round-5 form (debug variant 2),
+// one med3 per value before the convert.
+__device__ __forceinline__ uint32_t relu_fp8x4_med3(const f16v& c, int q) {
     const float a0 = __builtin_amdgcn_fmed3f(c[4 * q + 0], 0.0f, 448.0f);
     const float a1 = __builtin_amdgcn_fmed3f(c[4 * q + 1], 0.0f, 448.0f);
     const float a2 = __builtin_amdgcn_fmed3f(c[4 * q + 2], 0.0f, 448.0f);
@@ -1638,12 +1639,56 @@ __device__ __forceinline__ uint32_t relu_fp8x4(const f16v& c, int q) {
     return __builtin_amdgcn_cvt_pk_fp8_f32(a2, a3, lo, true);
 }
 
+// MODE.FP16_OVFL (bit 23): overflowing f16 / FP8 results clamp to the largest finite value instead of inf / NaN
+__device__ __forceinline__ void fp8_saturating_converts() {
+    __builtin_amdgcn_s_setreg((0 << 11) | (23 << 6) | 1 /* hwreg(HW_REG_MODE, 23, 1) */, 1u);
+}
+// two e4m3 bytes into word half `hi` of `old` (scale 1), saturating under fp8_saturating_converts()
+template <bool HI>
+__device__ __forceinline__ uint32_t cvt_sat_fp8(float a, float b, uint32_t old) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(__builtin_bit_cast(s2, old), a, b,
+                                                                                  1.0f, HI));
+}
+
+// Zero every e4m3 byte of w whose sign bit is set (a negative value or -0): v_perm_b32's selectors 8..11 replicate the
+// sign bits of bytes 1, 3 of its second source and bytes 1, 3 of its first, so (w << 8, w) with 0x090B080A gives 0xFF
+// for each such byte.
+__device__ __forceinline__ uint32_t relu_e4m3x4(uint32_t w, uint32_t sh) {
+    return w & ~__builtin_amdgcn_perm(sh, w, 0x090B080Au);
+}
+
 // next layer's fp8 B operands from the 4 accumulator blocks: k-step s byte j = row f8_row(s, h, j)
+template <bool MED3 = false>
 __device__ __forceinline__ void pack_fp8(const f16v (&c)[4], i8v (&y)[2]) {
+    if constexpr (!MED3) {
+        // round 6: ReLU on the converted bytes. Under MODE.FP16_OVFL (set at kernel start,
+        // fp8_saturating_converts) the scaled convert saturates at +-448, infinities included, as the med3 clamp does
+        // (tools/probe_fp8_cvt.hip: without the mode bit a finite value past 464 becomes 0x7F, a NaN), then
+        // relu_e4m3x4: 3 VALU per 4 values instead of 4 med3 (FP8 width-128 kernel 632.7 -> 590.2 us per 2^23
+        // queries, bitwise equal, profiles/r06_wide/).
+        // The first convert's "old" operand (bytes 2..3 kept, then overwritten by the second convert) must be a register
+        // that dies there: an accumulator element would be copied first (its tuple is still live), so it is the
+        // previous group's shifted word
+        uint32_t spare = 0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                const f16v& cc = c[2 * s + (d >> 2)];
+                const int q = d & 3;
+                const uint32_t lo = cvt_sat_fp8<false>(cc[4 * q + 0], cc[4 * q + 1], spare);
+                const uint32_t w = cvt_sat_fp8<true>(cc[4 * q + 2], cc[4 * q + 3], lo);
+                const uint32_t sh = w << 8;
+                y[s][d] = (int)relu_e4m3x4(w, sh);
+                spare = sh;
+            }
+        return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int d = 0; d < 8; ++d) y[s][d] = (int)relu_fp8x4(c[2 * s + (d >> 2)], d & 3);
+        for (int d = 0; d < 8; ++d) y[s][d] = (int)relu_fp8x4_med3(c[2 * s + (d >> 2)], d & 3);
 }
 
 // wait for LDS reads at this point only (the image copy) — a full __syncthreads() would also wait for the
@@ -1682,7 +1727,7 @@ struct WideLds {
     __device__ __forceinline__ h8 at(int o) const { return b[o >> 12][o & 4095]; }
 };
 
-template <int PREC>
+template <int PREC, bool MED3 = false>
 __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], const uint32_t (&sc)[5]) {
     f16v c[4];
     {
@@ -1717,7 +1762,7 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
         return o;
     } else {
         i8v y[2];
-        pack_fp8(c, y);
+        pack_fp8<MED3>(c, y);
         // fp8 fragment f: planes at h8 offsets (20 + 2 f) * 64 and (21 + 2 f) * 64 from the lane's base
         auto frag8 = [&](const WideLds& wl, int f) {
             const h8 lo = wl.at((20 + 2 * f) * 64), hi = wl.at((21 + 2 * f) * 64);
@@ -1737,7 +1782,7 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
 #pragma unroll
                 for (int mb = 0; mb < 4; ++mb)
                     c[mb] = mfma_fp8_mb(mb, frag8(wl, wide8_frag(l, mb, s)), y[s], c[mb], sc[l - 1]);
-            pack_fp8(c, y);
+            pack_fp8<MED3>(c, y);
         }
         const WideLds wl(lw_lane);
         f16v o = zero16();
@@ -1752,7 +1797,8 @@ __device__ __forceinline__ f16v wide_mlp(lds_h8* lw_lane, const h8 (&x)[5], cons
 // THREADS 1024 (debug variant 1): 4 waves per SIMD within 128 VGPRs.
 // QUEUE (round 2, default): the block owns a contiguous range of tiles and its waves draw from an LDS counter (as the
 // 64-wide variant 39) instead of a fixed tile sequence per wave.
-template <int ENC, int PREC, int EPI, int THREADS = 512, bool QUEUE = false>
+// MED3 (debug variant 2): the FP8 activations clamped by one med3 per value before the convert (round 5).
+template <int ENC, int PREC, int EPI, int THREADS = 512, bool QUEUE = false, bool MED3 = false>
 __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(const float* __restrict__ q,
                                                                             float* __restrict__ out, int64_t n,
                                                                             const h8* __restrict__ img,
@@ -1762,6 +1808,7 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
     __shared__ __attribute__((aligned(16))) h8 lw[NH8];
     __shared__ uint32_t wq_next;
     fp32_flush_output_denorms();  // the omod doubling-chain encoder
+    if constexpr (PREC == 1 && !MED3) fp8_saturating_converts();  // pack_fp8
     copy_to_lds_chunked<THREADS, NH8>(lw, img);
     if (QUEUE && threadIdx.x == 0) wq_next = 0;
     __syncthreads();
@@ -1833,7 +1880,7 @@ __global__ __launch_bounds__(THREADS, THREADS / 256) void infer_wide_kernel(cons
                 acc = __builtin_bit_cast(float4, av);
             }
         }
-        const f16v o = wide_mlp<PREC>((lds_h8*)(lw + lane), x, sc);
+        const f16v o = wide_mlp<PREC, MED3>((lds_h8*)(lw + lane), x, sc);
         const float L0 = (float)(_Float16)fmaxf(o[0], 0.0f);
         const float L1 = (float)(_Float16)fmaxf(o[1], 0.0f);
         const float L2 = (float)(_Float16)fmaxf(o[2], 0.0f);
@@ -1878,8 +1925,10 @@ __host__ __device__ constexpr int wide_off(int layer) {
 __global__ void fp8_convert_kernel(const float* __restrict__ x, uint8_t* __restrict__ y, int64_t n, int relu) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float a = __builtin_amdgcn_fmed3f(x[i], relu ? 0.0f : -448.0f, 448.0f);
-    y[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(a, 0.0f, 0, false) & 0xffu);
+    fp8_saturating_converts();  // the FP8 inference kernel's conversion (pack_fp8)
+    uint32_t w = cvt_sat_fp8<false>(x[i], 0.0f, 0u);
+    if (relu) w = relu_e4m3x4(w, w << 8);
+    y[i] = (uint8_t)(w & 0xffu);
 }
 
 // Standalone encoding kernel (HBM-bound; used by the parity tests of the encoding): writes the f32
@@ -3623,9 +3672,20 @@ hipError_t launch_infer_wide(int prec, int enc, const float* queries, float* out
     if (n <= 0) return hipSuccess;
     const int variant = prec >> 4;  // debug: kernel variant (nrc_debug_infer_precision)
     prec &= 15;
-    if ((prec != 0 && prec != 1) || (enc != 0 && enc != 2) || (mode != -1 && mode != 0 && mode != 2) || variant > 1)
+    if ((prec != 0 && prec != 1) || (enc != 0 && enc != 2) || (mode != -1 && mode != 0 && mode != 2) || variant > 2)
         return hipErrorInvalidValue;
     const int64_t ntiles = (n + 31) / 32;
+    if (variant == 2) {
+#if NRC_DEBUG_KERNELS  // FP8 with round 5's med3 clamp (relu_fp8x4_med3): A/B only, debug library
+        if (enc != 0 || mode != -1 || prec != 1) return hipErrorInvalidValue;
+        static int bv2 = 0;
+        const InferEpilogue e{};
+        return launch_persistent_infer(infer_wide_kernel<0, 1, -1, 512, true, true>, 512, bv2, ntiles, queries, out, n,
+                                       reinterpret_cast<const _Float16*>(img), s, e, scales);
+#else
+        return hipErrorNotSupported;
+#endif
+    }
     if (variant == 1) {
 #if NRC_DEBUG_KERNELS  // 1024-thread blocks (4 waves per SIMD): A/B only, debug library
         if (enc != 0 || mode != -1) return hipErrorInvalidValue;

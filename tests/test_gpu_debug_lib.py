@@ -64,6 +64,7 @@ def test_debug_library_variants_in_subprocess():
            "tests/test_gpu_train_dc.py::test_t16_64_sample_blocks",
            "tests/test_gpu_parity.py::test_pooled_variant_bitwise_and_reusable",
            "tests/test_gpu_wide.py::test_wide_kernel_variant_bit_identical",
+           "tests/test_gpu_wide.py::test_wide_fp8_byte_relu_variant_bit_identical",
            "tests/test_gpu_debug_lib.py::test_debug_entry_points",
            "tests/test_gpu_train_dc.py::test_dc_gradient_is_deterministic_with_a_slow_dw_wave",
            "tests/test_gpu_train_dc.py::test_dc_protocol_timeout_is_reported"]

@@ -4,7 +4,8 @@
 Tolerances:
 * f16 path vs ORC_MIXED (same numerics model as the 64-wide network): relative L2 <= 1e-3 and at most 0.1 % of the
   queries beyond 16 f16 ulps of their output scale (north_star tolerance);
-* e4m3 conversion (med3 clamp + v_cvt_pk_fp8_f32) vs the oracle's RNE: bit-exact;
+* e4m3 conversion (the FP8 kernel's: saturating v_cvt_scalef32_pk_fp8_f32 under MODE.FP16_OVFL, ReLU on the bytes) vs
+  the oracle's RNE of the clamped value: bit-exact;
 * FP8 path vs ORC_FP8: relative L2 <= 2.2e-2 (70,001 queries; 3e-2 at 1 and 33) and >= 98 % of outputs within 2^-10
   relative
   (measured 1.4-1.9e-2 and 99.3 % at 70,001 queries). Not bit-exact by construction: the MX MFMA's 64-element fp8 block sum is
@@ -309,5 +310,28 @@ def test_wide_kernel_variant_bit_identical(nrc, dev, n):
             base = run(net, nrc, dev, q, prec)
             var = run(net, nrc, dev, q, prec | (1 << 4))
             assert np.array_equal(base, var), f"precision {prec}: variant differs"
+    finally:
+        net.destroy()
+
+
+@pytest.mark.parametrize("gain", [1.6, 6.0])
+def test_wide_fp8_byte_relu_variant_bit_identical(nrc, dev, gain):
+    """The production FP8 kernel (round 6: ReLU on the converted e4m3 bytes, saturation by the convert under
+    MODE.FP16_OVFL, tools/probe_fp8_cvt.hip) against debug variant 2 (round 5: a med3 clamp per value before the
+    convert): bitwise, on xavier weights (gain 1.6) and on weights large enough that the hidden activations pass 448
+    (gain 6: the clamp and the saturating convert must agree there)."""
+    import torch
+    if not nrc._lib.is_debug_library():
+        pytest.skip("A/B variant of the debug library (libnrc_amd_debug.so)")
+    net = nrc.Network()
+    net.init(stream=torch.cuda.current_stream(), encoding=nrc.InputEncoding.Frequency,
+             config=nrc.default_config(nrc.InputEncoding.Frequency, width=128))
+    try:
+        net.set_state(nrc.StateSlot.INFER, wide_params(13, gain))
+        q = nrc.synthetic.cornell_queries(70001, seed=17)
+        base = run(net, nrc, dev, q, nrc._lib.PRECISION_FP8)
+        var = run(net, nrc, dev, q, nrc._lib.PRECISION_FP8 | (2 << 4))
+        assert np.isfinite(base).all()
+        assert np.array_equal(base, var)
     finally:
         net.destroy()

@@ -25,8 +25,8 @@ sys.path.insert(0, __file__.rsplit("/", 1)[0])
 import isa_stats  # noqa: E402
 
 
-def loop_lines(path: str, sub: str) -> list[tuple[str, bool]]:
-    """(instruction, inside inline asm) of the loop blocks, in order."""
+def loop_lines(path: str, sub: str, full: bool = False) -> list[tuple[str, bool]]:
+    """(opcode, inside inline asm) of the loop blocks, in order (full: the whole instruction text instead)."""
     lines = isa_stats.kernel_lines(path, sub)
     # block boundaries and their instructions, keeping the asm flag
     blocks: dict[str, list[tuple[str, bool]]] = {"entry": []}
@@ -55,7 +55,7 @@ def loop_lines(path: str, sub: str) -> list[tuple[str, bool]]:
         if not s or s.startswith((";", ".")):
             continue
         op = s.split()[0]
-        blocks[cur].append((op, in_asm))
+        blocks[cur].append((s if full else op, in_asm))
         t = re.search(r"(\.LBB\S+)", s)
         if op.startswith("s_branch") or op.startswith("s_cbranch"):
             if t:
@@ -78,15 +78,31 @@ def loop_lines(path: str, sub: str) -> list[tuple[str, bool]]:
     return [x for b in loop for x in blocks[b]]
 
 
-def bucket(op: str, in_asm: bool) -> str | None:
+def clamp_registers(ins: list[tuple[str, bool]]) -> set[str]:
+    """Third operands of v_med3_f32 shared by >= 16 instructions of the loop: the FP8 activation clamp (ReLU and
+    saturation, med3(x, 0, 448.0) with 448.0 held in one register), not encoder arithmetic."""
+    c = Counter(t.rsplit(",", 1)[-1].strip() for t, _ in ins if t.startswith("v_med3_f32"))
+    regs = {r for r, n in c.items() if n >= 16}
+    if sum(1 for t, _ in ins if t.startswith("v_cvt_scalef32_pk_fp8")) >= 16:
+        regs.add("relu_e4m3")  # marker: the FP8 loop, whose v_perm / v_bitop3 / shifts by 8 are the byte ReLU
+    return regs
+
+
+def bucket(text: str, in_asm: bool, clamps: frozenset[str] = frozenset()) -> str | None:
+    op = text.split()[0]
     if op.startswith("v_mfma"):
         return "mfma"
     if not op.startswith("v_"):
         return None
     if in_asm:
         return "encoder"
-    if op.startswith(("v_cvt_pk_f16_f32", "v_pk_max_f16", "v_pk_max_i16")):
+    if op.startswith(("v_cvt_pk_f16_f32", "v_pk_max_f16", "v_pk_max_i16", "v_cvt_pk_fp8_f32", "v_cvt_scalef32_pk_fp8")):
         return "relu_pack"
+    if op.startswith("v_med3_f32") and text.rsplit(",", 1)[-1].strip() in clamps:
+        return "relu_pack"
+    if "relu_e4m3" in clamps and (op.startswith(("v_bitop3_b32", "v_perm_b32"))
+                                  or (op.startswith("v_lshlrev_b32") and text.split()[2] == "8,")):
+        return "relu_pack"  # the FP8 kernel's byte ReLU (relu_e4m3x4: shift, v_perm sign mask, and-not)
     if op.startswith(("v_permlane32_swap", "v_add_f32", "v_cvt_f32_f16")):
         return "epilogue"
     if op.startswith(("v_mov_b32", "v_accvgpr")):
@@ -100,14 +116,16 @@ def bucket(op: str, in_asm: bool) -> str | None:
 
 def main() -> None:
     path, sub = sys.argv[1], sys.argv[2]
-    ins = loop_lines(path, sub)
-    c = Counter(b for op, a in ins if (b := bucket(op, a)))
-    ops = Counter(op for op, a in ins if bucket(op, a) == "address")
+    ins = loop_lines(path, sub, full=True)
+    cl = frozenset(clamp_registers(ins))
+    c = Counter(b for t, a in ins if (b := bucket(t, a, cl)))
+    ops = Counter(t.split()[0] for t, a in ins if bucket(t, a, cl) == "address")
     valu = sum(v for k, v in c.items() if k != "mfma")
     out = {"kernel": sub, "per_tile": dict(c), "valu_non_mfma": valu, "mfma": c["mfma"],
            "valu_per_mfma_excl": valu / max(c["mfma"], 1),
            "pmc_style_valu_per_mfma": (valu + c["mfma"]) / max(c["mfma"], 1),
-           "address_ops": dict(ops.most_common())}
+           "address_ops": dict(ops.most_common()),
+           "opcodes": dict(Counter(t.split()[0] for t, a in ins if t.startswith("v_")).most_common())}
     print(json.dumps(out, indent=1))
 
 
