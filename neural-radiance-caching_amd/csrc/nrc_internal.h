@@ -401,7 +401,9 @@ enum Knob : int {
                               // optimizer kernels as two launches (read at nrc_init)
     kKnobFuseMode = 16,       // fused step A/B: 0 (-1) per-block flags, 1 / 2 an arrival counter per block / per wave;
                               // timing ablations (wrong results) 3 no reducers, 4 reducers that only wait
-    kKnobCount = 17
+    kKnobTcnnReentry = 17,    // tcnn-numerics inference: the f16 accumulator back into f32 by 0 two 32x32x16 identity
+                              // MFMAs per block and chunk (round 6, first form), 1 (-1) four 4x4x4 identity MFMAs
+    kKnobCount = 18
 };
 int knob(Knob k);
 

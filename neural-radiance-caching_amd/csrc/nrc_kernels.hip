@@ -3421,8 +3421,16 @@ __device__ __forceinline__ h8 relu_words(const uint32_t (&a)[8], int b) {
 // per-chunk f16 accumulation, with 0.5 VALU per element instead of 1.5 (convert down, widen both halves back) or 2
 // issue slots (v_fma_mix). The kernel was VALU-issue-bound (85 % of the SIMDs' vector issue, PMC); the identity MFMAs
 // move that work to the matrix pipe, which ran at 21 %.
+// Second form (round 6, RE 1, the default): v_mfma_f32_4x4x4_16b_f16 runs 16 independent 4x4x4 products, block
+// b = lane / 4 taking its B columns from lanes 4b..4b+3 and writing column lane % 4 of its 4-row result into that lane's
+// 4 registers. With A = the 4x4 identity (lane l: a one at element l % 4) the result is the lane's own 4 B halves as
+// f32, in order: one such MFMA widens accumulator words 2q, 2q + 1 into registers 4q .. 4q + 3, four of them the whole
+// 32x32 block -- about 12.5 cycles each against 34 for a 32x32x16 (tools/microbench/mfma_4x4.hip), so 4 x 4x4x4 instead
+// of 2 x 32x32x16 per block and chunk.
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 struct TcnnId {
     h8 lo, hi;  // A fragments: lane (i, h) element e is 1 where row i == 8 (e / 4) + 4 h + e % 4 (+ 16 for hi)
+    h4v q;      // 4x4x4 identity: element lane % 4 is 1
     __device__ __forceinline__ explicit TcnnId(int lane) {
         const int i = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -3431,16 +3439,33 @@ struct TcnnId {
             lo[e] = (_Float16)(i == row ? 1.0f : 0.0f);
             hi[e] = (_Float16)(i == 16 + row ? 1.0f : 0.0f);
         }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = (_Float16)((lane & 3) == e ? 1.0f : 0.0f);
     }
 };
 __device__ __forceinline__ h8 acc_words(const uint32_t (&a)[8], int b) {
     const u4 w = {a[4 * b], a[4 * b + 1], a[4 * b + 2], a[4 * b + 3]};
     return __builtin_bit_cast(h8, w);
 }
+// accumulator words 0..7 widened to the f32 32x32 accumulator by four 4x4x4 identity MFMAs
+__device__ __forceinline__ f16v widen4(const TcnnId& id, const uint32_t (&a)[8]) {
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f8v __attribute__((ext_vector_type(8)));
+    f4 d[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+        d[qq] = __builtin_amdgcn_mfma_f32_4x4x4f16(id.q, __builtin_bit_cast(h4v, u2v{a[2 * qq], a[2 * qq + 1]}),
+                                                   f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const f8v lo = __builtin_shufflevector(d[0], d[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    const f8v hi = __builtin_shufflevector(d[2], d[3], 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+}
 
 // One layer's KK chunks of both M-blocks into the packed-f16 accumulators: chunk 0 rounds the MFMA result, every
-// further chunk re-enters the accumulator through Id0 / Id1 first. The two M-blocks' chains are independent.
-template <int KK>
+// further chunk re-enters the accumulator first (RE 0: through Id0 / Id1, RE 1: widen4). The two M-blocks' chains are
+// independent.
+template <int KK, int RE>
 __device__ __forceinline__ void tcnn_layer(lds_h8* wl, const TcnnId& id, int layer, const h8 (&in)[KK],
                                            uint32_t (&acc)[2][8]) {
 #pragma unroll
@@ -3448,10 +3473,15 @@ __device__ __forceinline__ void tcnn_layer(lds_h8* wl, const TcnnId& id, int lay
         const h8 w0 = wl[fwd_frag(layer, 0, kk) * 64], w1 = wl[fwd_frag(layer, 1, kk) * 64];
         f16v c0 = zero16(), c1 = zero16();
         if (kk > 0) {
-            c0 = mfma(id.lo, acc_words(acc[0], 0), c0);
-            c1 = mfma(id.lo, acc_words(acc[1], 0), c1);
-            c0 = mfma(id.hi, acc_words(acc[0], 1), c0);
-            c1 = mfma(id.hi, acc_words(acc[1], 1), c1);
+            if constexpr (RE == 1) {
+                c0 = widen4(id, acc[0]);
+                c1 = widen4(id, acc[1]);
+            } else {
+                c0 = mfma(id.lo, acc_words(acc[0], 0), c0);
+                c1 = mfma(id.lo, acc_words(acc[1], 0), c1);
+                c0 = mfma(id.hi, acc_words(acc[0], 1), c0);
+                c1 = mfma(id.hi, acc_words(acc[1], 1), c1);
+            }
         }
         c0 = mfma(w0, in[kk], c0);
         c1 = mfma(w1, in[kk], c1);
@@ -3463,7 +3493,7 @@ __device__ __forceinline__ void tcnn_layer(lds_h8* wl, const TcnnId& id, int lay
 // ENC 0: Frequency (K = 80, 5 chunks, pad features 66..79); ENC 3: Hash (round 5) from hash_feature_kernel's level features
 // (K = 64, 4 chunks: grid 0..31, OneBlob 32..55, Identity 56..61, pad 62, 63; feat = the pass's workspace), the same MLP
 // chunking -- tcnn runs the same FullyFusedMLP behind either encoding (NRCNetworkConfigs.h:84-128).
-template <int ENC>
+template <int ENC, int RE = 1>
 __global__ __launch_bounds__(64 * kTcnnWaves, 1) void infer_tcnn_kernel(const float* __restrict__ q,
                                                                         float* __restrict__ out, int64_t n,
                                                                         const h8* __restrict__ wf,
@@ -3584,7 +3614,7 @@ __global__ __launch_bounds__(64 * kTcnnWaves, 1) void infer_tcnn_kernel(const fl
         uint32_t acc[2][8];
         h8 y[4];
         // layer 0 (K = 80 / 64: 5 / 4 chunks) and the hidden layers (K = 64, 4 chunks)
-        tcnn_layer<KK0>(wl, id, 0, in0, acc);
+        tcnn_layer<KK0, RE>(wl, id, 0, in0, acc);
 #pragma unroll
         for (int l = 1; l < 5; ++l) {
             // k-step kk of the next layer = accumulator rows 16 kk.. = M-block kk / 2, registers 8 (kk % 2)..
@@ -3593,22 +3623,35 @@ __global__ __launch_bounds__(64 * kTcnnWaves, 1) void infer_tcnn_kernel(const fl
                 y[b] = relu_words(acc[0], b);
                 y[2 + b] = relu_words(acc[1], b);
             }
-            tcnn_layer<4>(launder(wl), id, l, y, acc);
+            tcnn_layer<4, RE>(launder(wl), id, l, y, acc);
         }
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             y[b] = relu_words(acc[0], b);
             y[2 + b] = relu_words(acc[1], b);
         }
-        // output layer (rows 0..2 of lane half 0 = elements 0..2), the same chunking; rows 0..3 re-enter through Id0
-        // (accumulator elements 4..7, rows 8..11, are fed as zeros: no output reads them)
+        // output layer (rows 0..2 of lane half 0 = elements 0..2), the same chunking; RE 0: rows 0..3 re-enter through
+        // Id0 (accumulator elements 4..7, rows 8..11, are fed as zeros); RE 1: elements 0..3 through one 4x4x4 identity
+        // MFMA, elements 4..15 (rows no output reads) keep the previous chunk's values
         uint32_t o[2];
         {
             lds_h8* const wll = launder(wl);
+            f16v c = zero16();
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
-                f16v c = zero16();
-                if (kk > 0) c = mfma(id.lo, __builtin_bit_cast(h8, u4{o[0], o[1], 0u, 0u}), c);
+                if constexpr (RE == 1) {
+                    if (kk > 0) {
+                        typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+                        typedef float f4 __attribute__((ext_vector_type(4)));
+                        const f4 d = __builtin_amdgcn_mfma_f32_4x4x4f16(id.q, __builtin_bit_cast(h4v, u2v{o[0], o[1]}),
+                                                                        f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) c[e] = d[e];
+                    }
+                } else {
+                    c = zero16();
+                    if (kk > 0) c = mfma(id.lo, __builtin_bit_cast(h8, u4{o[0], o[1], 0u, 0u}), c);
+                }
                 c = mfma(wll[fwd_frag(5, 0, kk) * 64], y[kk], c);
                 o[0] = pk2(c[0], c[1]);
                 o[1] = pk2(c[2], c[3]);
@@ -3633,9 +3676,12 @@ hipError_t launch_infer_tcnn(const float* queries, float* out, int64_t n, const 
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!wf || !w0) return hipErrorInvalidValue;
-    static int bpc = 0;
-    return launch_persistent_infer(infer_tcnn_kernel<0>, 64 * kTcnnWaves, bpc, (n + 31) / 32, queries, out, n, wf, s, w0,
-                                   (const uint32_t*)nullptr);
+    static int bpc[2] = {};
+    if (knob(kKnobTcnnReentry) == 0)
+        return launch_persistent_infer(infer_tcnn_kernel<0, 0>, 64 * kTcnnWaves, bpc[0], (n + 31) / 32, queries, out, n,
+                                       wf, s, w0, (const uint32_t*)nullptr);
+    return launch_persistent_infer(infer_tcnn_kernel<0, 1>, 64 * kTcnnWaves, bpc[1], (n + 31) / 32, queries, out, n, wf,
+                                   s, w0, (const uint32_t*)nullptr);
 }
 
 // tcnn-numerics Hash inference (NRC_PRECISION_F16_ACC16, round 5): the feature pass, then infer_tcnn_kernel<3> per pass
@@ -3643,14 +3689,17 @@ hipError_t launch_infer_hash_tcnn(const float* queries, float* out, int64_t n, c
                                   const _Float16* grid, uint32_t* feat, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!wf || !w0 || !grid || !feat) return hipErrorInvalidValue;
-    static int bpc = 0;
+    static int bpc[2] = {};
+    const int re = knob(kKnobTcnnReentry) == 0 ? 0 : 1;
     for (int64_t c0 = 0; c0 < n; c0 += kHashFeatStride) {
         const int64_t cnt = std::min<int64_t>(kHashFeatStride, n - c0);
         const float* qc = queries + c0 * NRC_INPUT_DIMS;
         launch_hash_feature_pass(qc, cnt, reinterpret_cast<const uint32_t*>(grid), feat, false, s);
-        const hipError_t e = launch_persistent_infer(infer_tcnn_kernel<3>, 64 * kTcnnWaves, bpc, (cnt + 31) / 32, qc,
-                                                     out + c0 * NRC_OUTPUT_DIMS, cnt, wf, s, w0,
-                                                     (const uint32_t*)feat);
+        const hipError_t e =
+            re == 0 ? launch_persistent_infer(infer_tcnn_kernel<3, 0>, 64 * kTcnnWaves, bpc[0], (cnt + 31) / 32, qc,
+                                              out + c0 * NRC_OUTPUT_DIMS, cnt, wf, s, w0, (const uint32_t*)feat)
+                    : launch_persistent_infer(infer_tcnn_kernel<3, 1>, 64 * kTcnnWaves, bpc[1], (cnt + 31) / 32, qc,
+                                              out + c0 * NRC_OUTPUT_DIMS, cnt, wf, s, w0, (const uint32_t*)feat);
         if (e != hipSuccess) return e;
     }
     return hipGetLastError();
