@@ -3426,7 +3426,9 @@ __device__ __forceinline__ h8 relu_words(const uint32_t (&a)[8], int b) {
 // 4 registers. With A = the 4x4 identity (lane l: a one at element l % 4) the result is the lane's own 4 B halves as
 // f32, in order: one such MFMA widens accumulator words 2q, 2q + 1 into registers 4q .. 4q + 3, four of them the whole
 // 32x32 block -- about 12.5 cycles each against 34 for a 32x32x16 (tools/microbench/mfma_4x4.hip), so 4 x 4x4x4 instead
-// of 2 x 32x32x16 per block and chunk.
+// of 2 x 32x32x16 per block and chunk. (An infinite f16 accumulator element -- an overflow of tcnn's f16 accumulation --
+// makes the other elements that share its identity product NaN, 0 x inf: those are the same query's other neurons,
+// whose output is then not finite in tcnn's arithmetic either; no other query is touched.)
 typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 struct TcnnId {
     h8 lo, hi;  // A fragments: lane (i, h) element e is 1 where row i == 8 (e / 4) + 4 h + e % 4 (+ 16 for hi)
