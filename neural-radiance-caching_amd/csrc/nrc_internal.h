@@ -248,7 +248,7 @@ hipError_t launch_infer(const float* queries, float* out, int64_t n, const _Floa
 constexpr int kProductInferVariant = 47;
 hipError_t launch_infer_variant(int variant, const float* queries, float* out, int64_t n, const _Float16* wf,
                                 hipStream_t s, uint32_t* pools = nullptr, int* parity = nullptr);
-constexpr int kNumInferVariants = 63;  // 50: launch_infer16 (the t16 image)
+constexpr int kNumInferVariants = 65;  // 50: launch_infer16 (the t16 image)
 // Frequency inference on v_mfma_f32_16x16x32_f16 (nrc_infer16.hip) from the t16-layout inference image
 hipError_t launch_infer16(const float* queries, float* out, int64_t n, const _Float16* wf16, hipStream_t s);
 // per-wave (cycles, 100 MHz ticks) of the last clocked variant launch (31, 32)

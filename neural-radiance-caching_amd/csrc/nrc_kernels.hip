@@ -973,6 +973,10 @@ __device__ __forceinline__ void mlp_tiles(lds_h8* lw_lane, const h8 (&x)[TILES][
 // prefetch and buffer load/store epilogue (variant 23).
 constexpr int kDefaultAbl = 48;
 constexpr int kAblPadQ = 1 << 20;  // padded RadianceQuery records (nrc_config.query_layout = NRC_QUERY_PADDED)
+// Round 6 (with the per-block LDS queue, ABL & 2048): a wave's first tile is block range start + its wave index, not a
+// queue draw, so its query loads issue before the weight copy and their latency overlaps the copy's (the queue counter
+// starts past the first tiles). The same tiles, so the same rows: outputs are unchanged.
+constexpr int kAblEarlyQ = 1 << 21;
 
 // Optional epilogue: accumulate_render_radiance (nrc_helpers.cu:77-129) fused into inference for the render
 // queries [0, n_acc) (EPI = RenderMode Full 0 / CacheOnly 2); their radiance is consumed in registers and never
@@ -1031,13 +1035,43 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
         for (int b = blockIdx.x + gridDim.x * (int)threadIdx.x; b < kStealMaxBlocks; b += gridDim.x * THREADS)
             __hip_atomic_store(other + b * kStealStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    constexpr bool kEarly = (ABL & kAblEarlyQ) != 0;
+    static_assert(!kEarly || ((ABL & 2048) != 0 && (ABL & (4096 | 16384 | 32768)) == 0 && (ABL & 8192) != 0 && TILES == 1),
+                  "early first-tile loads: the per-block LDS queue with buffer-loaded queries");
+    if constexpr (kEarly) {
+        if (threadIdx.x == 0) wq_next = THREADS / 64;  // the first tiles are taken by wave index (below)
+    }
+    // kEarly: the first tile's loads, issued before the weight copy (declared here, used by the loop below)
+    const int lane = threadIdx.x & 63;
+    const int h = lane >> 5, r = lane & 31;
+    const int64_t ngroups_all = (((n + 31) >> 5) + TILES - 1) / TILES;
+    constexpr bool kBufQ = (ABL & 8192) != 0 && (ENC == 0 || ENC == 3) && TILES == 1;
+    constexpr bool kPadQ = (ABL & kAblPadQ) != 0;
+    static_assert(!kPadQ || kBufQ, "padded queries: the buffer-load prefetch path");
+    const QOffsets vo = q_offsets<kPadQ>(r, h);
+    [[maybe_unused]] uint32_t F[8];
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rfeat =
+        buffer_rsrc(grid, ENC == 3 ? (int)(NRC_HASH_LEVELS * kHashFeatStride * 4) : 0);
+    auto load_f = [&](int64_t tile) {
+        if constexpr (ENC == 3) {
+            const int vo = (8 * h * (int)kHashFeatStride + (int)tile * 32 + r) * 4;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                F[i] = __builtin_amdgcn_raw_buffer_load_b32(rfeat, vo, i * (int)kHashFeatStride * 4, 0);
+        }
+    };
+    QLane Q[TILES];
+    [[maybe_unused]] int64_t g_early = 0;
+    if constexpr (kEarly) {
+        // a tile past the launch reads zeros (empty buffer descriptor) and is never used
+        g_early = (int64_t)blockIdx.x * ngroups_all / gridDim.x + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        load_f(g_early);
+        Q[0] = load_q_tile<kPadQ>(q, n, g_early, vo);
+    }
     copy_to_lds<THREADS, kFwdFrags * 64>(lw, wf);
     __syncthreads();
 
-    const int lane = threadIdx.x & 63;
-    const int h = lane >> 5, r = lane & 31;
     const bool out16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-    const int64_t ngroups_all = (((n + 31) >> 5) + TILES - 1) / TILES;
     int64_t ngroups = ngroups_all, wstride = (int64_t)gridDim.x * (THREADS / 64), gbase = 0;
     // wave-uniform tile index (readfirstlane: scalar address arithmetic, scalar buffer descriptors)
     int64_t g = (int64_t)blockIdx.x * (THREADS / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1067,7 +1101,8 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     if constexpr ((ABL & 2048) != 0 && (ABL & 4096) == 0) {
         gbase = (int64_t)blockIdx.x * ngroups_all / gridDim.x;
         ngroups = (int64_t)(blockIdx.x + 1) * ngroups_all / gridDim.x;  // end of this block's range
-        g = draw();
+        if constexpr (kEarly) g = g_early;
+        else g = draw();
     }
     // steal state (ABL & 32768): the range the wave draws from (own block first)
     [[maybe_unused]] int scur = blockIdx.x;
@@ -1170,32 +1205,19 @@ __device__ __forceinline__ void infer_v2_body(const float* __restrict__ q, float
     }
     const int64_t last = n - 1;
 
-    QLane Q[TILES];
-    // ABL & 8192 (ENC 0 / 3, TILES 1): queries through raw buffer loads (load_q_tile)
-    constexpr bool kBufQ = (ABL & 8192) != 0 && (ENC == 0 || ENC == 3) && TILES == 1;
-    // ABL kAblPadQ: padded RadianceQuery records (nrc_config.query_layout), through load_q_tile only
-    constexpr bool kPadQ = (ABL & kAblPadQ) != 0;
-    static_assert(!kPadQ || kBufQ, "padded queries: the buffer-load prefetch path");
-    const QOffsets vo = q_offsets<kPadQ>(r, h);
-    // ENC 3: the lane's 8 level features of the tile's query (levels 8h .. 8h + 7), prefetched with the query, as raw
-    // buffer loads: one 32-bit lane offset per tile and the level stride in the scalar offset (instead of 8 64-bit
-    // addresses); rows past the workspace read 0, rows past n are never stored
-    [[maybe_unused]] uint32_t F[8];
-    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rfeat =
-        buffer_rsrc(grid, ENC == 3 ? (int)(NRC_HASH_LEVELS * kHashFeatStride * 4) : 0);
-    auto load_f = [&](int64_t tile) {
-        if constexpr (ENC == 3) {
-            const int vo = (8 * h * (int)kHashFeatStride + (int)tile * 32 + r) * 4;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                F[i] = __builtin_amdgcn_raw_buffer_load_b32(rfeat, vo, i * (int)kHashFeatStride * 4, 0);
-        }
-    };
+    // ABL & 8192 (ENC 0 / 3, TILES 1): queries through raw buffer loads (load_q_tile); ABL kAblPadQ: padded
+    // RadianceQuery records (nrc_config.query_layout), through load_q_tile only. ENC 3: the lane's 8 level features of
+    // the tile's query (levels 8h .. 8h + 7), prefetched with the query, as raw buffer loads (load_f): one 32-bit lane
+    // offset per tile and the level stride in the scalar offset (instead of 8 64-bit addresses); rows past the
+    // workspace read 0, rows past n are never stored
     static_assert(ENC != 3 || TILES == 1, "ENC 3 prefetches one tile");
-    load_f(g);
-    if constexpr (kBufQ) {
+    if constexpr (kEarly) {
+        // loaded before the weight copy
+    } else if constexpr (kBufQ) {
+        load_f(g);
         Q[0] = load_q_tile<kPadQ>(q, n, g, vo);
     } else {
+        load_f(g);
 #pragma unroll
         for (int t = 0; t < TILES; ++t) Q[t] = load_q_enc<ENC>(q, min((g * TILES + t) * 32 + r, last), h);
     }
@@ -3194,6 +3216,9 @@ hipError_t launch_infer_variant(int variant, const float* queries, float* out, i
         // about half / three quarters of the 4-wave tile time
         case 61: bpc[61] = 1; return launch_persistent_infer(infer_kernel_v2<1, 2, 512, false, 48 | 1024 | 2048 | 8192 | 65536>, 512, bpc[61], ntiles, queries, out, n, wf, s);
         case 62: bpc[62] = 1; return launch_persistent_infer(infer_kernel_v2<1, 3, 768, false, 48 | 1024 | 2048 | 8192 | 65536>, 768, bpc[62], ntiles, queries, out, n, wf, s);
+        // round 6: 63 / 64 = 47 / 62 with the first tile's loads issued before the weight copy (kAblEarlyQ)
+        case 63: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | kAblEarlyQ>, 1024, bpc[63], ntiles, queries, out, n, wf, s);
+        case 64: bpc[64] = 1; return launch_persistent_infer(infer_kernel_v2<1, 3, 768, false, 48 | 1024 | 2048 | 8192 | 65536 | kAblEarlyQ>, 768, bpc[64], ntiles, queries, out, n, wf, s);
         // 60: energy probe (wrong outputs): 47 with 12 of the 14 pad slots of layer 0 fed as zeros
         case 60: return launch_persistent_infer(infer_kernel_v2<1, 4, 1024, false, 48 | 1024 | 2048 | 8192 | 65536 | 524288>, 1024, bpc[60], ntiles, queries, out, n, wf, s);
 #endif

@@ -61,6 +61,7 @@ def test_debug_library_variants_in_subprocess():
     cmd = [sys.executable, "-u", "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
            "--timeout", "120", "--timeout-method", "thread",
            "tests/test_gpu_parity.py::test_every_infer_variant_per_sample",
+           "tests/test_gpu_parity.py::test_early_first_tile_variants_bitwise",
            "tests/test_gpu_train_dc.py::test_t16_64_sample_blocks",
            "tests/test_gpu_parity.py::test_pooled_variant_bitwise_and_reusable",
            "tests/test_gpu_wide.py::test_wide_kernel_variant_bit_identical",

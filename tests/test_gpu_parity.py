@@ -87,7 +87,7 @@ def test_encode_fast_parity(nrc, orc, torch, dev, golden, encoder):
         assert bad.size == 0, f"{len(bad)} features off, first (query, feature): {bad[:5].tolist()}"
 
 
-@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40, 41, 42, 47, 48, 61, 62])
+@pytest.mark.parametrize("variant", [0, 23, 30, 39, 40, 41, 42, 47, 48, 61, 62, 63, 64])
 def test_every_infer_variant_per_sample(nrc, orc, torch, dev, net, golden, variant):
     """Per-query max error (not an aggregate) for every kernel variant kept for A/B at sizes
     that exercise partial tiles / single blocks. The product library holds variant 47 only; the A/B variants are
@@ -413,3 +413,24 @@ def test_pooled_variant_bitwise_and_reusable(nrc, torch, dev, net, golden):
             net.infer(q, torch.empty_like(b), n)  # the handle's own launch (product default) in between
         torch.cuda.synchronize()
         assert torch.equal(a, b), f"n={n}: {int((a != b).any(dim=1).sum())} rows differ"
+
+
+@pytest.mark.parametrize("pair", [(47, 63), (62, 64)])
+def test_early_first_tile_variants_bitwise(nrc, torch, dev, net, golden, pair):
+    """Round 6: variants 63 / 64 take a wave's first tile by wave index and load its queries before the weight copy
+    (kAblEarlyQ); the tiles and the per-query arithmetic are those of 47 / 62, so every row must be bit-identical,
+    including launches with fewer tiles than waves and ragged tails."""
+    if not nrc._lib.is_debug_library():
+        pytest.skip("A/B variant of the debug library (libnrc_amd_debug.so)")
+    net.set_state(nrc.StateSlot.INFER, golden["params_b"])
+    L = nrc._lib.lib()
+    sp = int(torch.cuda.current_stream().cuda_stream)
+    for n in [1, 33, 1000, 70001, (1 << 19) + 5]:
+        q = to_dev(torch, dev, nrc.synthetic.cornell_queries(n, seed=900 + n))
+        outs = []
+        for v in pair:
+            o = torch.full((n + 8, 3), 777.0, device=dev)
+            nrc._lib.check(L.nrc_debug_infer_variant(net._h, v, q.data_ptr(), o.data_ptr(), n, sp))
+            outs.append(o)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), f"n={n}"
