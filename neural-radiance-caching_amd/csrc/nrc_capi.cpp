@@ -991,7 +991,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobScatterMax: return v == -1 || (v >= 16 && v <= (1 << 20));
         case kKnobDcDw0Delay: return v >= -1 && v <= (1 << 20);
         case kKnobHashInfer: return v >= -1 && v <= 1;
-        case kKnobHashFeatAbl: return v >= -1 && v <= 36;
+        case kKnobHashFeatAbl: return v >= -1 && (v <= 36 || v == 128);
         case kKnobT16Groups: return v == -1 || v == 1 || v == 2;
         case kKnobHashFeatP: return v == -1 || (v >= 8 && v <= 256 && v % 8 == 0);
         case kKnobPeerPath: return v >= -1 && v <= 4;

@@ -556,7 +556,8 @@ __device__ __forceinline__ uint32_t hash_interp_pk(const float (&w)[8], const ui
     return __builtin_bit_cast(uint32_t, acc);
 }
 
-template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores;
+template <int ABL = 0>  // ablations (timing only, knob hash_feat_abl): 1 no LDS gathers, 2 no position loads, 4 no stores,
+                        // 128 positions 5 steps ahead (same results);
                         // 8 the round-3 scalar arithmetic, 16 the round-3 unpipelined loop (same results), 32 hashed
                         // synthetic positions instead of the position loads
 __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __restrict__ q, int64_t n, int P,
@@ -667,6 +668,40 @@ __global__ __launch_bounds__(1024, 1) void hash_feature_kernel(const float* __re
         while (phase(std::integral_constant<int, 0>{}) && phase(std::integral_constant<int, 1>{})) {
         }
     };
+    // ABL & 128 (round 6, A/B): the positions 5 steps ahead instead of 3 (a ring of 4 position sets): step s prepares step
+    // s + 1 from set (s + 1) % 4 and reloads that set with step s + 5's positions
+    auto body_deep = [&](auto dense_c) {
+        f3 PP[4] = {PB[0][0], PB[0][1], PB[1][0], PB[1][1]};  // steps 0..3
+        LdsCorners C[2];
+        uint32_t v[2][8];
+        corners(PP[0], C[0], dense_c);
+        PP[0] = load_pos(i + 4096);  // step 4
+        gather(C[0], v[0]);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        auto phase = [&](auto cur_c, auto slot_c) -> bool {
+            constexpr int cur = decltype(cur_c)::value, nxt = 1 - cur, slot = decltype(slot_c)::value;
+            if (i - (int)threadIdx.x >= cnt) return false;  // block-uniform
+            corners(PP[slot], C[nxt], dense_c);
+            PP[slot] = load_pos(i + 5120);  // step s + 5
+            gather(C[nxt], v[nxt]);
+            __builtin_amdgcn_raw_buffer_store_b32(interp(C[cur], v[cur]), rf, (ABL & 4) ? kBufferOff : i * 4, 0, 0);
+            i += 1024;
+            return true;
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        while (phase(I0{}, I1{}) && phase(I1{}, I2{}) && phase(I0{}, I3{}) && phase(I1{}, I0{})) {
+        }
+    };
+    if constexpr ((ABL & 128) != 0) {
+        if (level <= 1) body_deep(std::integral_constant<bool, true>{});
+        else body_deep(std::integral_constant<bool, false>{});
+        return;
+    }
     if constexpr ((ABL & 16) == 0) {
         if (level <= 1) body_pipe(std::integral_constant<bool, true>{});
         else body_pipe(std::integral_constant<bool, false>{});
@@ -3326,6 +3361,7 @@ static void launch_hash_feature_pass(const float* qc0, int64_t cnt, const uint32
                  : fa == 32 ? hash_feature_kernel<32>  // no position loads, scattered positions
                  : fa == 33 ? hash_feature_kernel<33>  // 32 without the gathers
                  : fa == 36 ? hash_feature_kernel<36>  // 32 without the stores
+                 : fa == 128 ? hash_feature_kernel<128>  // positions 5 steps ahead (round 6)
                            : hash_feature_kernel<7>;
         hipLaunchKernelGGL(k, dim3(16 * P), dim3(1024), 0, s, qc0, cnt, P, g, feat);
         return;
