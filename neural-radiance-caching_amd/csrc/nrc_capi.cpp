@@ -264,12 +264,12 @@ bool want_t16(int encoding) {
     return encoding == NRC_ENCODING_FREQUENCY || encoding == NRC_ENCODING_HASH;
 }
 
-std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+std::atomic<int> g_knobs[kKnobCount] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 const char* const kKnobNames[kKnobCount] = {"train_kernel", "train_shape", "scatter_min", "scatter_max", "dc_dw0_delay",
                                             "hash_infer", "hash_feat_abl", "t16_groups", "hash_feat_p", "peer_path",
                                             "px_polls", "scatter_part", "scatter_compact", "hash_train_feat",
-                                            "hash_adam", "train_fused", "fuse_mode", "tcnn_reentry"};
-static_assert(kKnobCount == 18, "one initial value and one name per knob");
+                                            "hash_adam", "train_fused", "fuse_mode", "tcnn_reentry", "train_prio"};
+static_assert(kKnobCount == 19, "one initial value and one name per knob");
 
 std::string config_json(int encoding, const nrc_config& c) {
     char buf[2048];
@@ -1003,6 +1003,7 @@ bool knob_value_ok(Knob k, int v) {
         case kKnobTrainFused: return v >= -1 && v <= 1;
         case kKnobFuseMode: return v >= -1 && v <= 4;
         case kKnobTcnnReentry: return v >= -1 && v <= 1;
+        case kKnobTrainPrio: return v >= -1 && v <= 2;
         default: return false;
     }
 }

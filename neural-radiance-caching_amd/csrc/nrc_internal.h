@@ -403,7 +403,9 @@ enum Knob : int {
                               // timing ablations (wrong results) 3 no reducers, 4 reducers that only wait
     kKnobTcnnReentry = 17,    // tcnn-numerics inference: the f16 accumulator back into f32 by 0 two 32x32x16 identity
                               // MFMAs per block and chunk (round 6, first form), 1 (-1) four 4x4x4 identity MFMAs
-    kKnobCount = 18
+    kKnobTrainPrio = 18,      // debug library, A/B: role-split training kernel with 1 the dW waves / 2 the chain waves
+                              // at s_setprio 1 (-1 / 0: no priority)
+    kKnobCount = 19
 };
 int knob(Knob k);
 

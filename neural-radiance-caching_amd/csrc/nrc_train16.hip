@@ -498,7 +498,9 @@ __global__ __launch_bounds__(256, 1) void train16_kernel(const float* __restrict
 // grid_scatter_kernel (ho). Everything else -- forward, loss, delta chain, dW waves, slab layout -- is the Frequency
 // kernel's.
 // The body takes the block's LDS and index from its kernel (train16_split_kernel, or the fused step's trainer blocks).
-template <int AUX, int G = 2, bool PADQ = false, int ENC = 0>
+// PRIO (debug library, A/B): 1 = the dW waves at s_setprio 1, 2 = the chain waves at s_setprio 1 (issue arbitration
+// is by priority, then age; the chain waves are the older half)
+template <int AUX, int G = 2, bool PADQ = false, int ENC = 0, int PRIO = 0>
 __device__ __forceinline__ void train16_split_body(char* __restrict__ smem, const int blk,
                                                    const float* __restrict__ q, const float* __restrict__ t, int64_t b,
                                                    float n_total, float loss_scale, const h8* __restrict__ wf,
@@ -520,6 +522,7 @@ __device__ __forceinline__ void train16_split_body(char* __restrict__ smem, cons
     _Float16* slab = slabs + (int64_t)blk * slab_floats(0);
 
     if (dw_wave) {
+        if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
         // ---- dW waves: the forward's six barriers, then one dW step per backward step
         for (int i = 0; i < 6; ++i) lds_barrier();
         const int lg = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
@@ -589,6 +592,7 @@ __device__ __forceinline__ void train16_split_body(char* __restrict__ smem, cons
     }
 
     // ---- chain waves: as train16_kernel
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     int r[G];
     bool valid[G];
     typedef float f3 __attribute__((ext_vector_type(3)));
@@ -847,15 +851,15 @@ __device__ __forceinline__ void train16_split_body(char* __restrict__ smem, cons
     }
 }
 
-template <int AUX, int G = 2, bool PADQ = false, int ENC = 0>
+template <int AUX, int G = 2, bool PADQ = false, int ENC = 0, int PRIO = 0>
 __global__ __launch_bounds__(512, 1) void train16_split_kernel(const float* __restrict__ q, const float* __restrict__ t,
                                                                int64_t b, float n_total, float loss_scale,
                                                                const h8* __restrict__ wf, const h8* __restrict__ wb,
                                                                _Float16* __restrict__ slabs,
                                                                float* __restrict__ loss_partials, HashTrainOut ho) {
     __shared__ __attribute__((aligned(16))) char smem[kLds];
-    train16_split_body<AUX, G, PADQ, ENC>(smem, blockIdx.x, q, t, b, n_total, loss_scale, wf, wb, slabs, loss_partials,
-                                          ho);
+    train16_split_body<AUX, G, PADQ, ENC, PRIO>(smem, blockIdx.x, q, t, b, n_total, loss_scale, wf, wb, slabs,
+                                                loss_partials, ho);
 }
 
 // ---- Round 6: the whole Frequency training step in one launch ----------------------------------
@@ -1057,6 +1061,18 @@ hipError_t launch_train16(const float* queries, const float* targets, int64_t b,
             return hipErrorNotSupported;
 #endif
         }
+#if NRC_DEBUG_KERNELS
+        const int tp = knob(kKnobTrainPrio);
+        if (tp == 1 || tp == 2) {
+            if (tp == 1)
+                hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 0, 1>), grid, dim3(128 * kWaves), 0, s, queries,
+                                   targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, HashTrainOut{});
+            else
+                hipLaunchKernelGGL((train16_split_kernel<16, 2, false, 0, 2>), grid, dim3(128 * kWaves), 0, s, queries,
+                                   targets, b, n_total, loss_scale, f, bw, slabs, loss_partials, HashTrainOut{});
+            return hipGetLastError();
+        }
+#endif
         hipLaunchKernelGGL((train16_split_kernel<16, 2>), grid, dim3(128 * kWaves), 0, s, queries, targets, b, n_total,
                            loss_scale, f, bw, slabs, loss_partials, HashTrainOut{});
         return hipGetLastError();
