@@ -74,9 +74,10 @@ def test_knob_values_are_range_checked(nrc):
     zero (SIGFPE). Out-of-range values are NRC_ERR_INVALID_ARGUMENT now and leave the knob unchanged (no GPU needed)."""
     L = nrc._lib
     bad = {"train_shape": [8, 100, -2], "train_kernel": [3, 31, 33, -5], "t16_groups": [0, 3], "hash_infer": [2, -2],
-           "scatter_min": [0, 15, 1 << 21], "scatter_max": [7], "hash_feat_abl": [37, 128], "dc_dw0_delay": [-2, 1 << 21],
+           "scatter_min": [0, 15, 1 << 21], "scatter_max": [7], "hash_feat_abl": [37, 127, 129], "dc_dw0_delay": [-2, 1 << 21],
            "hash_feat_p": [0, 12, 264], "peer_path": [5, -2], "px_polls": [0, -2, (1 << 21) + 1],
-           "scatter_part": [17, -2], "scatter_compact": [17, -2], "hash_train_feat": [2, -2], "hash_adam": [1, -2]}
+           "scatter_part": [17, -2], "scatter_compact": [17, -2], "hash_train_feat": [2, -2], "hash_adam": [1, -2],
+           "train_fused": [2, -2], "fuse_mode": [5, -2], "tcnn_reentry": [2, -2], "train_prio": [3, -2]}
     for name, values in bad.items():
         before = L.get_knob(name)
         for v in values:
@@ -84,7 +85,7 @@ def test_knob_values_are_range_checked(nrc):
                 L.set_knob(name, v)
             assert e.value.status == 1 and "out of range" in str(e.value), (name, v)
             assert L.get_knob(name) == before
-    for name, v in [("train_shape", 7), ("train_kernel", 32), ("t16_groups", 1), ("scatter_min", 1024), ("peer_path", 0), ("peer_path", 4), ("px_polls", 1), ("scatter_part", 16), ("scatter_compact", 0), ("hash_train_feat", 1), ("hash_adam", 0)]:
+    for name, v in [("train_shape", 7), ("train_kernel", 32), ("t16_groups", 1), ("scatter_min", 1024), ("peer_path", 0), ("peer_path", 4), ("px_polls", 1), ("scatter_part", 16), ("scatter_compact", 0), ("hash_train_feat", 1), ("hash_adam", 0), ("hash_feat_abl", 128), ("tcnn_reentry", 0), ("train_prio", 2)]:
         L.set_knob(name, v)
         assert L.get_knob(name) == v
         L.set_knob(name, -1)
