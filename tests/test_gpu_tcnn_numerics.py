@@ -243,3 +243,32 @@ def test_hash_debug_precision_entry_matches_config(nrc, orc, torch, dev, hnet):
         assert torch.equal(a, b) and not torch.equal(a, c)
     finally:
         d.destroy()
+
+
+@pytest.mark.parametrize("encoding", ["Frequency", "Hash"])
+def test_reentry_forms_bitwise_equal(nrc, torch, dev, encoding):
+    """Round 6: the f16 accumulator re-enters the f32 MFMA accumulator through four 4x4x4 identity MFMAs per block and
+    chunk (knob tcnn_reentry = 1, the default) or two 32x32x16 identity MFMAs (0, the first form). Both are exact
+    widenings of the same f16 values, so outputs must be bit-identical -- ragged sizes, a Hash launch past one feature
+    pass (2^21 + 77 queries runs two passes) and wide random weights (large activations)."""
+    enc = getattr(nrc.InputEncoding, encoding)
+    cfg = nrc.default_config(enc, infer_precision=nrc.PRECISION_F16_ACC16)
+    n = nrc.Network()
+    n.init(stream=torch.cuda.current_stream(), encoding=enc, config=cfg)
+    try:
+        p = n.get_state(nrc.StateSlot.INFER)
+        n.set_state(nrc.StateSlot.INFER, (p * np.float32(2.0)).astype(np.float32))
+        for size in ([1, 33, 70001, (1 << 21) + 77] if encoding == "Hash" else [1, 33, 70001]):
+            q = torch.from_numpy(nrc.synthetic.cornell_queries(size, seed=1300 + size)).to(dev)
+            outs = []
+            for kv in (0, 1):
+                nrc._lib.set_knob("tcnn_reentry", kv)
+                o = torch.full((size + 8, 3), 777.0, device=dev)
+                n.infer(q, o, size)
+                outs.append(o)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (encoding, size)
+            assert bool((outs[1][size:] == 777.0).all())
+    finally:
+        nrc._lib.set_knob("tcnn_reentry", -1)
+        n.destroy()
