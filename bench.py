@@ -5,9 +5,11 @@ batch); configs[2]: the per-frame self-training (4 x 16,384-sample steps) report
 
 N > 1 — configs[3] (C4): the 2K frame's 2^22 queries sharded contiguously over the ranks
 (2^19 per GPU at 8; strong scaling, no collective on the inference path), and every 16,384-sample minibatch split
-into 16,384 / N per rank with the gradient all-reduced over RCCL INSIDE the library (nrc_set_comm + nrc_train_dp:
-global batch 16,384, the reference's per-step semantics). The weak-scaling figures (2^21 queries per GPU) are kept
-as the extra key ``weak``.
+into 16,384 / N per rank with the gradients combined INSIDE the library (nrc_train_dp: global batch 16,384, the
+reference's per-step semantics) -- through the one-shot peer exchange inside the reduction when every rank could open it
+and run a frame through it (``train_dp_path``), else over the RCCL communicator (nrc_set_comm); the RCCL figure is
+kept beside it (``train_step_rccl_ms``). The weak-scaling figures (2^21 queries per GPU) are kept as the extra key
+``weak``.
 
 Launch: ``python bench.py [--gpus N --steps K --warmup W]``. N > 1 either under torch.distributed.run (WORLD_SIZE set) or
 on its own: with WORLD_SIZE unset the process starts N fresh child processes of itself (one rank per GPU, RANK /
@@ -561,6 +563,40 @@ def dp_exchange_bench(nrc, net, dev, world: int, rank: int, frames_q, frames_t, 
     return res
 
 
+def open_peer_training(nrc, net, dev, warm_frame) -> bool:
+    """N > 1: open the library's one-shot peer exchange on every rank and run one training frame through it
+    (``warm_frame``: nrc_train_dp takes the exchange while it is open). True when every rank succeeded (agreed with a
+    MIN all-reduce after each stage); otherwise the exchange is closed again, the reason is left in
+    ``net._peer_training_error`` and the caller keeps the RCCL communicator."""
+    import torch
+    import torch.distributed as dist
+
+    ok = torch.ones(1, dtype=torch.int32, device=dev if dist.get_backend() == "nccl" else "cpu")
+    err = None
+    try:
+        nrc.dp.open_peer_exchange(net)
+    except Exception as e:  # noqa: BLE001
+        err = f"open: {e}"
+        ok.zero_()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()):
+        try:
+            warm_frame()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001
+            err = f"step: {e}"
+            ok.zero_()
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()):
+        return True
+    net._peer_training_error = err or "failed on another rank"
+    try:
+        net.peer_exchange_close()
+    except Exception:  # noqa: BLE001
+        pass
+    return False
+
+
 PEAK_CLOCK_MHZ = 2400.0  # the clock the 2.5 PF dense f16 peak is quoted at (1,024 SIMDs x 1,024 FLOP per cycle)
 
 
@@ -820,16 +856,37 @@ def main() -> None:
                 "ms_per_step": ww / args.steps * 1e3, "scaling": "weak"}
         del qw, ow
 
-    # ---- training: frames of 4 x 16384 (N > 1: each minibatch split over the ranks, RCCL all-reduce per step)
-    for f in range(2):
-        train_frame(f)
-    barrier()
-    t0 = time.perf_counter()
-    for f in range(args.train_frames):
-        train_frame(f)
-    barrier()
-    train_frame_ms = max_over_ranks(time.perf_counter() - t0) / args.train_frames * 1e3
+    # ---- training: frames of 4 x 16384 (N > 1: each minibatch split over the ranks). N > 1 over RCCL: the library's
+    # production data-parallel path first -- the one-shot peer exchange inside the reduction (nrc_train_dp takes it
+    # while it is open) -- when every rank opened it and ran one frame through it; otherwise, and
+    # beside it, the RCCL all-reduce path
+    train_dp_path = "single" if not distributed else ("rccl" if comm is not None else "python all-reduce (gloo)")
+    train_dp_error = None
+    if distributed and comm is not None and not args.no_peer:
+        if open_peer_training(nrc, net, dev, lambda: train_frame(0)):
+            train_dp_path = "peer exchange"
+        else:
+            train_dp_error = getattr(net, "_peer_training_error", "failed")
+
+    def time_train_frames() -> float:
+        for f in range(2):
+            train_frame(f)
+        barrier()
+        t0 = time.perf_counter()
+        for f in range(args.train_frames):
+            train_frame(f)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0) / args.train_frames * 1e3
+
+    train_frame_ms = time_train_frames()
     train_step_ms = train_frame_ms / 4
+    train_step_rccl_ms = None
+    if train_dp_path == "peer exchange":
+        net.peer_exchange_close()  # the same frames over the RCCL communicator, for comparison
+        barrier()
+        train_step_rccl_ms = time_train_frames() / 4
+    elif train_dp_path == "rccl":
+        train_step_rccl_ms = train_step_ms
     # the same training frames replayed from a HIP graph (N = 1): the GPU's own step time, without the per-call host
     # cost (Python + ctypes + one hipLaunchKernel per kernel) that the eager figure above includes
     train_step_graph_ms = None
@@ -842,7 +899,7 @@ def main() -> None:
     if distributed and not args.no_peer:
         dp_exchange = dp_exchange_bench(nrc, net, dev, world, rank, frames_q, frames_t, b0, bn, args.train_frames,
                                         barrier, max_over_ranks)
-        dp_exchange["rccl_split_step_ms"] = train_step_ms if comm is not None else None
+        dp_exchange["rccl_split_step_ms"] = train_step_rccl_ms
 
     # ---- sustained inference: the clock the chip holds under a long run of back-to-back
     # launches is lower than in a short burst; the average of the last `sustained` of 2 x `sustained` launches
@@ -918,6 +975,9 @@ def main() -> None:
         "train_step_ms": train_step_ms,
         "train_step_graph_ms": train_step_graph_ms,
         "train_frame_ms": train_frame_ms,
+        "train_dp_path": train_dp_path,
+        "train_step_rccl_ms": train_step_rccl_ms,
+        "train_dp_error": train_dp_error,
         "infer_kernel_ms": kernel_ms,
         "weak": weak,
         "settle": settle,
