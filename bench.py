@@ -7,8 +7,8 @@ N > 1 — configs[3] (C4): the 2K frame's 2^22 queries sha
 (2^19 per GPU at 8; strong scaling, no collective on the inference path), and every 16,384-sample minibatch split
 into 16,384 / N per rank with the gradients combined INSIDE the library (nrc_train_dp: global batch 16,384, the
 reference's per-step semantics) -- through the one-shot peer exchange inside the reduction when every rank could open it
-and run a frame through it (``train_dp_path``), else over the RCCL communicator (nrc_set_comm); the RCCL figure is
-kept beside it (``train_step_rccl_ms``). The weak-scaling figures (2^21 queries per GPU) are kept as the extra key
+and run a frame through it (``train_dp_path``), else over the RCCL communicator (nrc_set_comm); the all-reduce figure
+is kept beside it (``train_step_allreduce_ms``). The weak-scaling figures (2^21 queries per GPU) are kept as the extra key
 ``weak``.
 
 Launch: ``python bench.py [--gpus N --steps K --warmup W]``. N > 1 either under torch.distributed.run (WORLD_SIZE set) or
@@ -779,9 +779,11 @@ def main() -> None:
     mb_views = [[(frames_q[fi][b * nrc.BATCH_SIZE + b0:], frames_t[fi][b * nrc.BATCH_SIZE + b0:]) for b in range(4)]
                 for fi in range(4)]
 
+    peer = {"on": False}  # N > 1: the library's peer exchange is open (nrc_train_dp takes it)
+
     def train_frame(fi: int) -> None:
         for tqv, ttv in mb_views[fi % 4]:
-            if comm is not None:
+            if comm is not None or peer["on"]:
                 net.train_dp(tqv, ttv, bn, nrc.BATCH_SIZE)
             elif trainer is not None:
                 trainer.step(tqv, ttv, bn, nrc.BATCH_SIZE)
@@ -860,12 +862,17 @@ def main() -> None:
     # production data-parallel path first -- the one-shot peer exchange inside the reduction (nrc_train_dp takes it
     # while it is open) -- when every rank opened it and ran one frame through it; otherwise, and
     # beside it, the RCCL all-reduce path
-    train_dp_path = "single" if not distributed else ("rccl" if comm is not None else "python all-reduce (gloo)")
+    allreduce_path = "rccl" if comm is not None else "python all-reduce (gloo)"
+    train_dp_path = "single" if not distributed else allreduce_path
     train_dp_error = None
-    if distributed and comm is not None and not args.no_peer:
+    if distributed and not args.no_peer:
+        # (a gloo rehearsal of several ranks on one GPU takes the same path: the exchange's split form for ranks that
+        # share a device, the Python all-reduce as the fallback)
+        peer["on"] = True
         if open_peer_training(nrc, net, dev, lambda: train_frame(0)):
             train_dp_path = "peer exchange"
         else:
+            peer["on"] = False
             train_dp_error = getattr(net, "_peer_training_error", "failed")
 
     def time_train_frames() -> float:
@@ -880,13 +887,15 @@ def main() -> None:
 
     train_frame_ms = time_train_frames()
     train_step_ms = train_frame_ms / 4
-    train_step_rccl_ms = None
+    train_step_allreduce_ms = None
     if train_dp_path == "peer exchange":
-        net.peer_exchange_close()  # the same frames over the RCCL communicator, for comparison
+        net.peer_exchange_close()  # the same frames over the all-reduce path (RCCL), for comparison
+        peer["on"] = False
         barrier()
-        train_step_rccl_ms = time_train_frames() / 4
-    elif train_dp_path == "rccl":
-        train_step_rccl_ms = train_step_ms
+        train_step_allreduce_ms = time_train_frames() / 4
+    elif distributed:
+        train_step_allreduce_ms = train_step_ms
+    train_step_rccl_ms = train_step_allreduce_ms if comm is not None else None
     # the same training frames replayed from a HIP graph (N = 1): the GPU's own step time, without the per-call host
     # cost (Python + ctypes + one hipLaunchKernel per kernel) that the eager figure above includes
     train_step_graph_ms = None
@@ -976,7 +985,8 @@ def main() -> None:
         "train_step_graph_ms": train_step_graph_ms,
         "train_frame_ms": train_frame_ms,
         "train_dp_path": train_dp_path,
-        "train_step_rccl_ms": train_step_rccl_ms,
+        "train_step_allreduce_ms": train_step_allreduce_ms,
+        "train_allreduce_path": allreduce_path if distributed else None,
         "train_dp_error": train_dp_error,
         "infer_kernel_ms": kernel_ms,
         "weak": weak,
